@@ -1,0 +1,107 @@
+"""Global importance-table sampler (`util.py:94-160`, ``Groupwise_Sampler``).
+
+State and field names match the reference so sampler checkpoints interchange:
+``importance`` (per-sample loss table), ``group_indicator`` (group id per
+sample), ``cur_sample_index``, ``group_index``, ``last_update_iteration``.
+
+Semantics kept: group 0 is the whole dataset with uniform
+importance; each new ``iteration`` opens a new group; several
+``update_importance`` calls in one iteration extend the same group; slices
+truncate at the dataset end and the cursor wraps; iteration re-reads state
+every draw (updates apply live) and stops after ``len(dataset)`` yields; the
+per-group weight is ``imp + mean(imp)`` (alpha = 1 smoothing).
+
+Fixes: ``__len__`` works (reference references an undefined ``num_samples``),
+scoring runs under ``no_grad``, and the table can live on the GPU
+(``device='cuda'``) where the MI355X path keeps it resident in HBM and the
+per-draw work (masked normalise + weighted draw) runs as one fused HIP
+kernel (``mercury_amd.ops.table_sample``) instead of a numpy round trip.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.utils.data import Sampler
+
+
+class Groupwise_Sampler(Sampler):
+
+    def __init__(self, dataset, replacement=True, num_samples=None, device='cpu'):
+        self.dataset = dataset
+        self.replacement = replacement
+        self.device = torch.device(device)
+        n = len(dataset)
+        self.group_indicator = torch.zeros(n, dtype=torch.int64, device=self.device)
+        self.importance = torch.ones(n, dtype=torch.float32, device=self.device)
+        self.cur_sample_index = 0
+        self.group_index = 0
+        self.last_update_iteration = -1
+        self.num_samples = n if num_samples is None else int(num_samples)
+
+    # ---- scoring --------------------------------------------------------------------------
+    def update_importance(self, iteration, update_batchsize, model, device='cuda', losses=None):
+        """Score the next contiguous slice and stamp it into the current group.
+
+        ``losses`` may be supplied pre-computed (e.g. by the native engine's
+        scorer), otherwise ``model`` is run on ``dataset.get_slice``."""
+        if iteration > self.last_update_iteration:
+            self.group_index += 1
+            self.last_update_iteration = iteration
+        n = len(self.dataset)
+        start = self.cur_sample_index
+        end = min(start + update_batchsize, n)
+        if losses is None:
+            data, label = self.dataset.get_slice(start, end)
+            with torch.no_grad():
+                out = model(data.to(device))
+                losses = F.cross_entropy(out.float(), label.to(device), reduction='none')
+        self.write_scores(start, end, losses)
+        self.cur_sample_index = 0 if end == n else end
+        return start, end
+
+    def write_scores(self, start, end, losses):
+        self.importance[start:end] = torch.as_tensor(losses).detach().to(
+            self.importance.device, torch.float32).reshape(-1)[:end - start]
+        self.group_indicator[start:end] = self.group_index
+
+    # ---- drawing --------------------------------------------------------------------------
+    def group_distribution(self):
+        """(member indices, normalised probabilities) of the current group."""
+        members = torch.nonzero(self.group_indicator == self.group_index).flatten()
+        if members.numel() == 0:
+            return members, members.float()
+        imp = self.importance[members]
+        w = imp + imp.mean()
+        return members, w / w.sum()
+
+    def __iter__(self):
+        counter = 0
+        n = self.num_samples
+        while True:
+            members, p = self.group_distribution()
+            j = torch.multinomial(p.cpu(), 1, self.replacement).item()
+            yield int(members[j].item())
+            counter += 1
+            if counter >= n:
+                return
+
+    def __len__(self):
+        return self.num_samples
+
+    # ---- checkpoint -----------------------------------------------------------------------
+    def state_dict(self):
+        return {'importance': self.importance.cpu().numpy().astype(np.float64),
+                'group_indicator': self.group_indicator.cpu().numpy().astype(np.float64),
+                'cur_sample_index': self.cur_sample_index,
+                'group_index': self.group_index,
+                'last_update_iteration': self.last_update_iteration}
+
+    def load_state_dict(self, sd):
+        self.importance = torch.as_tensor(np.asarray(sd['importance']), dtype=torch.float32,
+                                          device=self.device)
+        self.group_indicator = torch.as_tensor(np.asarray(sd['group_indicator']),
+                                               dtype=torch.int64, device=self.device)
+        self.cur_sample_index = int(sd['cur_sample_index'])
+        self.group_index = int(sd['group_index'])
+        self.last_update_iteration = int(sd['last_update_iteration'])

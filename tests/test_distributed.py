@@ -1,0 +1,87 @@
+"""Multi-process CPU tests over gloo (SURVEY §4 layer 3)."""
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mercury_amd.parallel import (BucketedAllReduce, FlatParams, ScoreExchange, allreduce,
+                                  spawn)
+
+
+def _ring(rank, ws, numel):
+    torch.manual_seed(rank)
+    t = torch.randn(numel)
+    out = allreduce(t)
+    ref = t.clone()
+    dist.all_reduce(ref)
+    assert torch.allclose(out, ref, atol=1e-5), (rank, numel)
+    avg = allreduce(t, op='avg')
+    assert torch.allclose(avg, ref / ws, atol=1e-5)
+
+
+@pytest.mark.parametrize('ws', [2, 3, 4])
+def test_ring_allreduce(ws):
+    for numel in (1, ws - 1, 1000, 1001):
+        if numel >= 1:
+            spawn(_ring, ws, args=(numel,))
+
+
+class Small(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Linear(16, 64)
+        self.b = nn.Linear(64, 64)
+        self.c = nn.Linear(64, 10)
+
+    def forward(self, x):
+        return self.c(F.relu(self.b(F.relu(self.a(x)))))
+
+
+def _bucketed(rank, ws):
+    torch.manual_seed(0)
+    m = Small()
+    flat = FlatParams(m)
+    br = BucketedAllReduce(flat, bucket_bytes=4096).attach()
+    assert len(br.buckets) > 1
+    torch.manual_seed(100 + rank)
+    x = torch.randn(8, 16)
+    flat.zero_grad()
+    m(x).pow(2).mean().backward()
+    local = flat.grad.clone()
+    br.finish()
+    ref = local.clone()
+    dist.all_reduce(ref)
+    assert torch.allclose(flat.grad, ref / ws, atol=1e-6)
+    # score exchange
+    se = ScoreExchange(5, 'cpu').start(torch.full((5,), float(rank)))
+    g = se.wait()
+    assert torch.equal(g[:, 0], torch.arange(ws, dtype=torch.float32))
+
+
+def test_bucketed_allreduce_overlap_hooks():
+    spawn(_bucketed, 2)
+
+
+def _trainer_dp(rank, ws):
+    from mercury_amd.config import Config
+    from mercury_amd.trainer import Trainer
+    from test_importance import FakeLoader, TinyNet
+    torch.manual_seed(rank)            # different init per rank: broadcast must fix it
+    net = TinyNet()
+    cfg = Config(print_every=0, eval_every=0, bucket_mb=0.001)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    loader = FakeLoader(n=6, seed=rank)   # non-IID: different shards
+    t = Trainer(net, opt, FakeLoader(n=4), loader, None, 'cpu', cfg)
+    t.fit(2)
+    flat = t.flat.data.clone()
+    gathered = [torch.zeros_like(flat) for _ in range(ws)]
+    dist.all_gather(gathered, flat)
+    for g in gathered:
+        assert torch.equal(g, gathered[0]), 'replicas diverged'
+    assert t.step == 9
+
+
+def test_trainer_dp_replicas_identical():
+    spawn(_trainer_dp, 2)
