@@ -1,0 +1,240 @@
+// Python bindings for the mercury_amd HIP kernels.
+//
+// Deliberately thin: tensors cross the boundary as raw device addresses (int)
+// plus the caller's hipStream_t, so this translation unit needs only pybind11 and
+// the HIP runtime -- no PyTorch headers -- and builds in seconds.  All shape,
+// dtype, device and contiguity validation happens in mercury_amd/ops/*.py, which
+// also fails loudly if this extension is missing on a GPU machine.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+
+template <typename T>
+static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+static hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mercury_amd CDNA4 (gfx950) kernels";
+
+  m.def("igemm", [](uintptr_t src, uintptr_t wt, uintptr_t out, int ldo, uintptr_t bias,
+                    uintptr_t stats, int stats_ld, int group_rows, int accumulate, uintptr_t slab,
+                    int SH, int SW, int SC, int RP, int RQ, int R, int Sk, int stride, int pad, int Kc,
+                    int Ncols, int M, int bm, int bn, int splits, bool trans, uintptr_t st) {
+    ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
+    EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows,
+                accumulate, P<float>(slab)};
+    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
+    check_launch("igemm");
+  });
+  m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
+    ConvGeom g{};
+    g.M = M;
+    g.Ncols = Ncols;
+    return igemm_slab_bytes(g, bm, bn, splits);
+  });
+
+  m.def("wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C, int Pp,
+                    int Q, int K, int R, int Sk, int stride, int pad, int Creal, int bm, int bn,
+                    int splits, uintptr_t st) {
+    WgradGeom g{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal};
+    wgrad_launch(P<const bf16>(dy), P<const bf16>(x), g, P<float>(dw), bm, bn, splits, S(st));
+    check_launch("wgrad");
+  });
+
+  m.def("bn_apply", [](uintptr_t y, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
+                       uintptr_t rmean, uintptr_t rvar, int use_running, int res_mode, uintptr_t res,
+                       uintptr_t stats2, uintptr_t gamma2, uintptr_t beta2, uintptr_t rmean2,
+                       uintptr_t rvar2, uintptr_t out, int M, int C, int group_rows, int act,
+                       float eps, uintptr_t st) {
+    BnApplyArgs a{P<const bf16>(y), P<const float>(stats), P<const float>(gamma),
+                  P<const float>(beta), P<const float>(rmean), P<const float>(rvar), use_running,
+                  res_mode, P<const bf16>(res), P<const float>(stats2), P<const float>(gamma2),
+                  P<const float>(beta2), P<const float>(rmean2), P<const float>(rvar2),
+                  P<bf16>(out), M, C, group_rows, act, eps};
+    bn_apply_launch(a, S(st));
+    check_launch("bn_apply");
+  });
+
+  m.def("bn_bwd", [](uintptr_t dout, uintptr_t out, uintptr_t y, uintptr_t stats, uintptr_t gamma,
+                     uintptr_t y2, uintptr_t stats2, uintptr_t gamma2, uintptr_t sums, uintptr_t dy,
+                     uintptr_t dy2, uintptr_t dz, uintptr_t dgamma, uintptr_t dbeta,
+                     uintptr_t dgamma2, uintptr_t dbeta2, int M, int C, int act, float eps,
+                     uintptr_t st) {
+    BnBwdArgs a{P<const bf16>(dout), P<const bf16>(out), P<const bf16>(y), P<const float>(stats),
+                P<const float>(gamma), P<const bf16>(y2), P<const float>(stats2),
+                P<const float>(gamma2), P<float>(sums), P<bf16>(dy), P<bf16>(dy2), P<bf16>(dz),
+                P<float>(dgamma), P<float>(dbeta), P<float>(dgamma2), P<float>(dbeta2), M, C, act,
+                eps};
+    bn_bwd_launch(a, S(st));
+    check_launch("bn_bwd");
+  });
+
+  m.def("pack_bn_table", [](const std::vector<std::vector<double>>& rows) {
+    std::vector<BnRunEntry> v;
+    for (const auto& r : rows) {
+      BnRunEntry e{};
+      e.rmean = P<float>((uintptr_t)r[0]);
+      e.rvar = P<float>((uintptr_t)r[1]);
+      e.stats_train = P<const float>((uintptr_t)r[2]);
+      e.stats_score = P<const float>((uintptr_t)r[3]);
+      e.nbt = P<long long>((uintptr_t)r[4]);
+      e.C = (int)r[5];
+      e.n_train = (int)r[6];
+      e.n_score = (int)r[7];
+      e.cnt_train = (float)r[8];
+      e.cnt_score = (float)r[9];
+      v.push_back(e);
+    }
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(BnRunEntry));
+  });
+  m.def("bn_running", [](uintptr_t tab, int nlayers, int maxC, float momentum, uintptr_t st) {
+    bn_running_launch(P<const BnRunEntry>(tab), nlayers, maxC, momentum, S(st));
+    check_launch("bn_running");
+  });
+
+  m.def("head_fwd", [](uintptr_t act, uintptr_t w, uintptr_t b, uintptr_t label, uintptr_t isw,
+                       uintptr_t pooled, uintptr_t logits, uintptr_t dlogits, uintptr_t losses,
+                       uintptr_t meters, int B, int HW, int C, int classes, int mode, uintptr_t st) {
+    HeadArgs a{P<const bf16>(act), P<const float>(w), P<const float>(b), P<const int>(label),
+               P<const float>(isw), P<float>(pooled), P<float>(logits), P<float>(dlogits),
+               P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0};
+    head_fwd_launch(a, S(st));
+    check_launch("head_fwd");
+  });
+  m.def("head_bwd", [](uintptr_t pooled, uintptr_t dlogits, uintptr_t w, uintptr_t dw, uintptr_t db,
+                       uintptr_t dact, int B, int HW, int C, int classes, uintptr_t st) {
+    HeadBwdArgs a{P<const float>(pooled), P<const float>(dlogits), P<const float>(w), P<float>(dw),
+                  P<float>(db), P<bf16>(dact), B, HW, C, classes};
+    head_bwd_launch(a, S(st));
+    check_launch("head_bwd");
+  });
+
+  m.def("pool_build", [](uintptr_t shard, uintptr_t labels, uintptr_t ctrl, uintptr_t pool,
+                         uintptr_t pool_label, uintptr_t pool_index, int Ns, int H, int W, int Pn,
+                         int batch, int pad, int flip, int augment, uint32_t seed,
+                         std::vector<float> mean, std::vector<float> inv_std, uintptr_t st) {
+    PoolBuildArgs a{P<const uint8_t>(shard), P<const int64_t>(labels), P<const int64_t>(ctrl),
+                    P<bf16>(pool), P<int>(pool_label), P<int>(pool_index), Ns, H, W, Pn, batch,
+                    pad, flip, augment, seed, {mean[0], mean[1], mean[2]},
+                    {inv_std[0], inv_std[1], inv_std[2]}};
+    pool_build_launch(a, S(st));
+    check_launch("pool_build");
+  });
+  m.def("is_sample", [](uintptr_t losses, uintptr_t ema, uintptr_t ctrl, uintptr_t idx, uintptr_t w,
+                        uintptr_t meters, int Pn, int B, int group, int importance, float alpha,
+                        float ema_alpha, uint32_t seed, uintptr_t st) {
+    IsSampleArgs a{P<const float>(losses), P<float>(ema), P<int64_t>(ctrl), P<int>(idx), P<float>(w),
+                   P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed};
+    is_sample_launch(a, S(st));
+    check_launch("is_sample");
+  });
+  m.def("gather", [](uintptr_t pool, uintptr_t pool_label, uintptr_t pool_index, uintptr_t idx,
+                     uintptr_t batch, uintptr_t batch_label, uintptr_t batch_index, int B,
+                     int chunks_per_img, uintptr_t st) {
+    GatherArgs a{P<const bf16>(pool), P<const int>(pool_label), P<const int>(pool_index),
+                 P<const int>(idx), P<bf16>(batch), P<int>(batch_label), P<int>(batch_index), B,
+                 chunks_per_img};
+    gather_launch(a, S(st));
+    check_launch("gather");
+  });
+  m.def("table_write", [](uintptr_t imp, uintptr_t grp, uintptr_t losses, int start, int n,
+                          int64_t gi, uintptr_t st) {
+    table_write_launch(P<float>(imp), P<int64_t>(grp), P<const float>(losses), start, n, gi, S(st));
+    check_launch("table_write");
+  });
+  m.def("table_sample", [](uintptr_t imp, uintptr_t grp, int N, int64_t gi, int ndraw, uint32_t seed,
+                           uint64_t counter, uintptr_t out, uintptr_t st) {
+    table_sample_launch(P<const float>(imp), P<const int64_t>(grp), N, gi, ndraw, seed, counter,
+                        P<int64_t>(out), S(st));
+    check_launch("table_sample");
+  });
+
+  m.def("pack_opt_segs", [](const std::vector<std::vector<long long>>& rows) {
+    std::vector<OptSeg> v;
+    for (const auto& r : rows) {
+      OptSeg s{};
+      s.off = r[0];
+      s.numel = (int)r[1];
+      s.kind = (int)r[2];
+      s.K = (int)r[3];
+      s.R = (int)r[4];
+      s.S = (int)r[5];
+      s.C = (int)r[6];
+      s.Cpad = (int)r[7];
+      s.w_krsc = P<bf16>((uintptr_t)r[8]);
+      s.w_crsk = P<bf16>((uintptr_t)r[9]);
+      v.push_back(s);
+    }
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(OptSeg));
+  });
+  m.def("optimizer", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t segs,
+                        int nsegs, long long total, uintptr_t hyper, uintptr_t step, int algo,
+                        int zero_grad, uintptr_t st) {
+    OptArgs a{P<float>(p), P<float>(g), P<float>(mm), P<float>(v), P<const OptSeg>(segs), nsegs,
+              total, P<const float>(hyper), P<const int64_t>(step), algo, zero_grad};
+    optimizer_launch(a, S(st));
+    check_launch("optimizer");
+  });
+  m.def("pack_weights", [](uintptr_t p, uintptr_t segs, int nsegs, long long total, uintptr_t st) {
+    pack_weights_launch(P<const float>(p), P<const OptSeg>(segs), nsegs, total, S(st));
+    check_launch("pack_weights");
+  });
+  m.def("step_begin", [](uintptr_t ctrl, uintptr_t st) {
+    step_begin_launch(P<int64_t>(ctrl), S(st));
+    check_launch("step_begin");
+  });
+
+  m.def("quantize", [](uintptr_t x, uintptr_t out, uintptr_t ws, long long n, uint32_t seed,
+                       uint64_t counter, uintptr_t st) {
+    quantize_launch(P<const float>(x), P<float>(out), P<float>(ws), n, seed, counter, S(st));
+    check_launch("quantize");
+  });
+  m.def("pool2d_fwd", [](uintptr_t x, uintptr_t y, uintptr_t argmax, int N, int H, int W, int C,
+                         int Pp, int Q, int k, int stride, int pad, int is_max, uintptr_t st) {
+    PoolArgs a{P<const bf16>(x), P<bf16>(y), P<int>(argmax), N, H, W, C, Pp, Q, k, stride, pad, is_max};
+    pool2d_fwd_launch(a, S(st));
+    check_launch("pool2d_fwd");
+  });
+  m.def("maxpool2d_bwd", [](uintptr_t dy, uintptr_t argmax, uintptr_t dx, int N, int H, int W, int C,
+                            int Pp, int Q, int k, int stride, int pad, uintptr_t st) {
+    PoolArgs a{nullptr, nullptr, P<int>(argmax), N, H, W, C, Pp, Q, k, stride, pad, 1};
+    maxpool2d_bwd_launch(a, P<const bf16>(dy), P<bf16>(dx), S(st));
+    check_launch("maxpool2d_bwd");
+  });
+  m.def("dwconv_fwd", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W,
+                         int C, int Pp, int Q, int stride, int pad, int group_rows, uintptr_t st) {
+    DwArgs a{P<const bf16>(x), P<const float>(w), P<bf16>(y), P<float>(stats), N, H, W, C, Pp, Q,
+             stride, pad, group_rows};
+    dwconv_fwd_launch(a, S(st));
+    check_launch("dwconv_fwd");
+  });
+  m.def("dwconv_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int H, int W, int C,
+                           int Pp, int Q, int stride, int pad, uintptr_t st) {
+    dwconv_dgrad_launch(P<const bf16>(dy), P<const float>(w), P<bf16>(dx), N, H, W, C, Pp, Q, stride,
+                        pad, S(st));
+    check_launch("dwconv_dgrad");
+  });
+  m.def("dwconv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C,
+                           int Pp, int Q, int stride, int pad, uintptr_t st) {
+    dwconv_wgrad_launch(P<const bf16>(dy), P<const bf16>(x), P<float>(dw), N, H, W, C, Pp, Q, stride,
+                        pad, S(st));
+    check_launch("dwconv_wgrad");
+  });
+  m.def("nchw_to_nhwc8", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int Cpad,
+                            uintptr_t st) {
+    nchw_to_nhwc8_launch(P<const float>(x), P<bf16>(y), N, C, H, W, Cpad, S(st));
+    check_launch("nchw_to_nhwc8");
+  });
+  m.def("arch", []() { return std::string("gfx950"); });
+}

@@ -1,0 +1,42 @@
+// Host-visible parameter blocks for the implicit-GEMM conv kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+typedef __bf16 bf16;
+
+// A-operand gather geometry.  "S*" = the tensor A is gathered from (NHWC), "R*" =
+// the spatial dims the GEMM rows enumerate.  forward: S = input x, R = output (P,Q);
+// dgrad (trans): S = dy, R = input (H,W).
+struct ConvGeom {
+  int SH, SW, SC;    // source spatial dims and (padded) channels
+  int RP, RQ;        // row-space spatial dims
+  int R, S, stride, pad;
+  int Kc;            // reduction length in 8-element chunks = R*S*SC/8
+  int Ncols;         // GEMM N (output channels)
+  int M;             // GEMM M = images * RP * RQ
+};
+
+struct EpiParams {
+  bf16* out;          // [M][ldo] bf16
+  int ldo;
+  const float* bias;  // [N] or null
+  float* stats;       // BN sums: [G][2][stats_ld] (sum, sumsq) or null
+  int stats_ld;
+  int group_rows;     // rows per ghost-BN group (tile never straddles a group)
+  int accumulate;     // out += result
+  float* slab;        // split-K workspace (set by the launcher's caller when splits > 1)
+};
+
+size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
+void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
+                  int bn, int splits, bool trans, hipStream_t st);
+
+struct WgradGeom {
+  int N, H, W, C;     // input x (C padded), NHWC
+  int P, Q, K;        // dy dims (K = output channels)
+  int R, S, stride, pad;
+  int Creal;          // unpadded input channels (layout of dW)
+};
+void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
+                  int splits, hipStream_t st);

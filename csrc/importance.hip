@@ -1,0 +1,257 @@
+// Importance-sampling data path on the GPU.
+//
+// pool_build  : the presample pool straight from the HBM-resident uint8 shard --
+//               epoch shuffle (Feistel permutation, drop_last), RandomCrop(32, pad 4),
+//               RandomHorizontalFlip, ToTensor, Normalize (`cifar10/data_loader.py:83-90`)
+//               -> NHWC bf16 with channels padded to 8.  Replaces 352 PIL-augmented
+//               images per step on the CPU.
+// is_sample   : the whole `update_samples` tail (`pytorch_collab.py:106-117`) in one
+//               workgroup: 10x EMA replay over the cumulative pool means (device-
+//               resident EMAverage), p = (l + alpha*ema)/sum, inverse-CDF draws with
+//               replacement (block-wide LDS prefix scan + binary search, Philox
+//               uniforms), importance weights N*p[idx].
+// gather      : the drawn samples' exact augmented views -> the next training batch.
+// table_*     : Groupwise_Sampler's global importance table kept in HBM: scatter of
+//               scored slices, and masked-normalise + weighted draws over the current
+//               group without a host round trip (`util.py:132-152`).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
+  const int slot = blockIdx.x;
+  const int j = slot / a.batch, t = slot - j * a.batch;
+  const int64_t pc = a.ctrl[0];
+  const int per_pool = a.P / a.batch;
+  const int nb = max(1, a.Ns / a.batch);
+  const int64_t gb = pc * per_pool + j;
+  const uint32_t epoch = (uint32_t)(gb / nb);
+  const int bi = (int)(gb % nb);
+  const uint32_t pos = (uint32_t)(bi * a.batch + t);
+  const uint32_t src = permute_index(pos, (uint32_t)a.Ns, a.seed, epoch);
+  int dy = a.pad, dx = a.pad, flip = 0;
+  if (a.augment) {
+    const u32x4 r = philox4x32(u32x4{(uint32_t)gb, (uint32_t)(gb >> 32), (uint32_t)t, 0x5eedu},
+                               a.seed, 0xA5A5A5A5u);
+    dy = r.x % (2 * a.pad + 1);
+    dx = r.y % (2 * a.pad + 1);
+    flip = a.flip ? (r.z & 1) : 0;
+  }
+  if (threadIdx.x == 0) {
+    a.pool_label[slot] = (int)a.labels[src];
+    a.pool_index[slot] = (int)src;
+  }
+  const uint8_t* img = a.shard + (size_t)src * a.H * a.W * 3;
+  bf16* out = a.pool + (size_t)slot * a.H * a.W * 8;
+  const int npx = a.H * a.W;
+  for (int px = threadIdx.x; px < npx; px += 256) {
+    const int h = px / a.W, w = px - h * a.W;
+    const int wc = flip ? (a.W - 1 - w) : w;
+    const int hs = h + dy - a.pad, ws = wc + dx - a.pad;
+    float v[3] = {0.f, 0.f, 0.f};
+    if (hs >= 0 && ws >= 0 && hs < a.H && ws < a.W) {
+      const uint8_t* p = img + ((size_t)hs * a.W + ws) * 3;
+      v[0] = p[0];
+      v[1] = p[1];
+      v[2] = p[2];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = f2bf((v[c] * (1.f / 255.f) - a.mean[c]) * a.inv_std[c]);
+#pragma unroll
+    for (int c = 3; c < 8; ++c) o[c] = f2bf(0.f);
+    *(bf16x8*)(out + (size_t)px * 8) = o;
+  }
+}
+
+constexpr int IS_T = 1024;
+
+__global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* p = lds;                   // [P] probabilities, then CDF
+  float* tsum = lds + a.P;          // [IS_T] per-thread segment sums (inclusive scan)
+  float* red = tsum + IS_T;         // [64]
+  const int tid = threadIdx.x;
+  const int G = a.P / a.group;
+  for (int i = tid; i < a.P; i += IS_T) p[i] = a.losses[i];
+  __syncthreads();
+  // group sums -> cumulative means -> EMA replay (10 updates for the reference pool)
+  if (tid == 0) {
+    float ema = a.ema[0];
+    bool init = a.ema[1] != 0.f;
+    double cs = 0.0;
+    for (int gi = 0; gi < G; ++gi) {
+      float s = 0.f;
+      for (int k = 0; k < a.group; ++k) s += p[gi * a.group + k];
+      cs += s;
+      const float m = (float)(cs / (double)((gi + 1) * a.group));
+      if (!init) {
+        ema = m;
+        init = true;
+      } else {
+        ema = a.ema_alpha * ema + (1.f - a.ema_alpha) * m;
+      }
+    }
+    a.ema[0] = ema;
+    a.ema[1] = 1.f;
+    red[32] = ema;
+    red[33] = (float)(cs / (double)a.P);
+    if (a.meters) {
+      a.meters[3] = red[33];
+      a.meters[4] = ema;
+    }
+  }
+  __syncthreads();
+  const float ema = red[32];
+  // shifted weights and per-thread contiguous segment sums
+  const int seg = (a.P + IS_T - 1) / IS_T;
+  const int s0 = min(a.P, tid * seg), s1 = min(a.P, s0 + seg);
+  float local = 0.f;
+  for (int i = s0; i < s1; ++i) {
+    const float v = a.importance ? (p[i] + a.alpha * ema) : 1.f;
+    p[i] = v;
+    local += v;
+  }
+  tsum[tid] = local;
+  __syncthreads();
+  for (int off = 1; off < IS_T; off <<= 1) {  // Hillis-Steele inclusive scan
+    const float add = tid >= off ? tsum[tid - off] : 0.f;
+    __syncthreads();
+    tsum[tid] += add;
+    __syncthreads();
+  }
+  const float total = tsum[IS_T - 1];
+  float run = tid > 0 ? tsum[tid - 1] : 0.f;
+  for (int i = s0; i < s1; ++i) {
+    run += p[i];
+    p[i] = run;  // unnormalised CDF
+  }
+  __syncthreads();
+  const int64_t dc = a.ctrl[1];
+  for (int d = tid; d < a.B; d += IS_T) {
+    const u32x4 r = philox4x32(u32x4{(uint32_t)dc, (uint32_t)(dc >> 32), (uint32_t)d, 0xd1a5u},
+                               a.seed, 0x3C6EF372u);
+    const float u = u01(r.x) * total;
+    int lo = 0, hi = a.P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (p[mid] > u) hi = mid;
+      else lo = mid + 1;
+    }
+    const float prev = lo > 0 ? p[lo - 1] : 0.f;
+    a.idx[d] = lo;
+    a.w[d] = a.importance ? (p[lo] - prev) / total * (float)a.P : 1.f;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    a.ctrl[0] += 1;
+    a.ctrl[1] += 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
+  const int b = blockIdx.y;
+  const int s = a.idx[b];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < a.chunks_per_img) {
+    const u32x4 v = ((const u32x4*)a.pool)[(size_t)s * a.chunks_per_img + i];
+    ((u32x4*)a.batch)[(size_t)b * a.chunks_per_img + i] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.batch_label[b] = a.pool_label[s];
+    if (a.batch_index) a.batch_index[b] = a.pool_index[s];
+  }
+}
+
+__global__ void table_write_kernel(float* imp, int64_t* grp, const float* losses, int start, int n,
+                                   int64_t gi) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    imp[start + i] = losses[i];
+    grp[start + i] = gi;
+  }
+}
+
+__global__ __launch_bounds__(1024) void table_sample_kernel(const float* imp, const int64_t* grp,
+                                                           int N, int64_t gi, int ndraw,
+                                                           uint32_t seed, uint64_t counter,
+                                                           int64_t* out) {
+  __shared__ float tsum[1024];
+  __shared__ float red[32];
+  const int tid = threadIdx.x;
+  const int seg = (N + 1023) / 1024;
+  const int s0 = min(N, tid * seg), s1 = min(N, s0 + seg);
+  float s = 0.f, cnt = 0.f;
+  for (int i = s0; i < s1; ++i)
+    if (grp[i] == gi) {
+      s += imp[i];
+      cnt += 1.f;
+    }
+  const float tot_imp = block_sum(s, red);
+  const float tot_cnt = block_sum(cnt, red);
+  const float mean = tot_cnt > 0.f ? tot_imp / tot_cnt : 0.f;
+  float local = 0.f;
+  for (int i = s0; i < s1; ++i)
+    if (grp[i] == gi) local += imp[i] + mean;  // w = imp + mean(imp), alpha = 1 (`util.py:146-148`)
+  tsum[tid] = local;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const float add = tid >= off ? tsum[tid - off] : 0.f;
+    __syncthreads();
+    tsum[tid] += add;
+    __syncthreads();
+  }
+  const float total = tsum[1023];
+  for (int d = tid; d < ndraw; d += 1024) {
+    const u32x4 r = philox4x32(u32x4{(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)d, 7u},
+                               seed, 0x1B873593u);
+    const float u = u01(r.x) * total;
+    int lo = 0, hi = 1023;  // thread segment whose inclusive sum exceeds u
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (tsum[mid] > u) hi = mid;
+      else lo = mid + 1;
+    }
+    float run = lo > 0 ? tsum[lo - 1] : 0.f;
+    const int a0 = min(N, lo * seg), a1 = min(N, a0 + seg);
+    int64_t pick = -1, last = -1;
+    for (int i = a0; i < a1; ++i) {
+      if (grp[i] != gi) continue;
+      last = i;
+      run += imp[i] + mean;
+      if (run > u) {
+        pick = i;
+        break;
+      }
+    }
+    out[d] = pick >= 0 ? pick : last;
+  }
+}
+}  // namespace
+
+void pool_build_launch(const PoolBuildArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(pool_build_kernel, dim3(a.P), dim3(256), 0, st, a);
+}
+
+void is_sample_launch(const IsSampleArgs& a, hipStream_t st) {
+  const size_t shm = (size_t)(a.P + IS_T + 64) * sizeof(float);
+  hipLaunchKernelGGL(is_sample_kernel, dim3(1), dim3(IS_T), shm, st, a);
+}
+
+void gather_launch(const GatherArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(gather_kernel, dim3((a.chunks_per_img + 255) / 256, a.B), dim3(256), 0, st, a);
+}
+
+void table_write_launch(float* importance, int64_t* group, const float* losses, int start, int n,
+                        int64_t group_index, hipStream_t st) {
+  hipLaunchKernelGGL(table_write_kernel, dim3((n + 255) / 256), dim3(256), 0, st, importance, group,
+                     losses, start, n, group_index);
+}
+
+void table_sample_launch(const float* importance, const int64_t* group, int N, int64_t group_index,
+                         int ndraw, uint32_t seed, uint64_t counter, int64_t* out,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(table_sample_kernel, dim3(1), dim3(1024), 0, st, importance, group, N,
+                     group_index, ndraw, seed, counter, out);
+}

@@ -1,0 +1,191 @@
+// Host-visible argument blocks + launchers for the non-GEMM kernels.
+// Every launcher is stream-ordered, allocation-free and graph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "igemm.h"
+
+// ------------------------------------------------------------------ batch norm
+struct BnApplyArgs {
+  const bf16* y;
+  const float* stats;            // [G][2][C]
+  const float* gamma;
+  const float* beta;
+  const float* rmean;            // eval mode
+  const float* rvar;
+  int use_running;
+  int res_mode;                  // 0 none, 1 identity (+res), 2 BN'd shortcut (+bn2(res))
+  const bf16* res;
+  const float* stats2;
+  const float* gamma2;
+  const float* beta2;
+  const float* rmean2;
+  const float* rvar2;
+  bf16* out;
+  int M, C, group_rows, act;     // act: 0 none, 1 relu, 2 relu6
+  float eps;
+};
+void bn_apply_launch(const BnApplyArgs& a, hipStream_t st);
+
+struct BnBwdArgs {
+  const bf16* dout;              // grad of the activation output
+  const bf16* out;               // activation output (mask)
+  const bf16* y;                 // conv output (pre-BN)
+  const float* stats;            // [2][C]
+  const float* gamma;
+  const bf16* y2;                // optional shortcut conv output sharing dz
+  const float* stats2;
+  const float* gamma2;
+  float* sums;                   // workspace [3][C]
+  bf16* dy;                      // grad wrt y
+  bf16* dy2;                     // grad wrt y2
+  bf16* dz;                      // optional: grad wrt pre-activation (identity residual)
+  float* dgamma;
+  float* dbeta;
+  float* dgamma2;
+  float* dbeta2;
+  int M, C, act;
+  float eps;
+};
+void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st);
+
+struct BnRunEntry {
+  float* rmean;
+  float* rvar;
+  const float* stats_train;      // [n_train][2][C]
+  const float* stats_score;      // [n_score][2][C]
+  long long* nbt;                // num_batches_tracked (int64) or null
+  int C, n_train, n_score;
+  float cnt_train, cnt_score;
+};
+void bn_running_launch(const BnRunEntry* tab, int nlayers, int maxC, float momentum,
+                       hipStream_t st);
+
+// ------------------------------------------------------------------ head (pool + fc + loss)
+struct HeadArgs {
+  const bf16* act;               // [B][HW][C] final activation
+  const float* w;                // fc weight [classes][C] (fp32 master)
+  const float* b;                // fc bias [classes]
+  const int* label;              // [B]
+  const float* isw;              // [B] importance weights N*p (train) or null (score / uniform)
+  float* pooled;                 // [B][C] workspace (saved for backward)
+  float* logits;                 // [B][classes] workspace
+  float* dlogits;                // [B][classes] (train) or null
+  float* losses;                 // [B] per-sample CE (score) or null
+  float* meters;                 // [0]+=sum(w-loss)*... see head.hip
+  int B, HW, C, classes, mode;   // mode 0 score, 1 train, 2 eval
+  int log_softmax_input;         // logits are already log-probs (VGG) -> NLL
+};
+void head_fwd_launch(const HeadArgs& a, hipStream_t st);
+
+struct HeadBwdArgs {
+  const float* pooled;           // [B][C]
+  const float* dlogits;          // [B][classes]
+  const float* w;                // [classes][C]
+  float* dw;                     // [classes][C] fp32 grad
+  float* db;                     // [classes]
+  bf16* dact;                    // [B][HW][C] grad of final activation
+  int B, HW, C, classes;
+};
+void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st);
+
+// ------------------------------------------------------------------ importance sampling
+struct PoolBuildArgs {
+  const uint8_t* shard;          // [Ns][H][W][3] uint8 HWC
+  const int64_t* labels;         // [Ns]
+  const int64_t* ctrl;           // [0] pool counter (pools built so far)
+  bf16* pool;                    // [P][H][W][8] bf16 normalised, channels 3..7 zero
+  int* pool_label;               // [P]
+  int* pool_index;               // [P] shard-local index (the dataset index the reference returns)
+  int Ns, H, W, P, batch, pad, flip, augment;
+  uint32_t seed;
+  float mean[3], inv_std[3];
+};
+void pool_build_launch(const PoolBuildArgs& a, hipStream_t st);
+
+struct IsSampleArgs {
+  const float* losses;           // [P]
+  float* ema;                    // [0] value, [1] initialised flag (device-resident EMAverage)
+  int64_t* ctrl;                 // [0] pool counter (incremented), [1] draw counter
+  int* idx;                      // [B] drawn pool slots
+  float* w;                      // [B] N * p[idx]
+  float* meters;                 // [3] pool mean out, [4] ema out
+  int P, B, group, importance;   // importance=0 -> uniform draws, w = 1
+  float alpha, ema_alpha;
+  uint32_t seed;
+};
+void is_sample_launch(const IsSampleArgs& a, hipStream_t st);
+
+struct GatherArgs {
+  const bf16* pool;              // [P][pix*8]
+  const int* pool_label;
+  const int* pool_index;
+  const int* idx;                // [B]
+  bf16* batch;                   // [B][pix*8]
+  int* batch_label;
+  int* batch_index;
+  int B, chunks_per_img;         // 16-byte chunks per image
+};
+void gather_launch(const GatherArgs& a, hipStream_t st);
+
+// global importance table (Groupwise sampler, K11)
+void table_write_launch(float* importance, int64_t* group, const float* losses, int start, int n,
+                        int64_t group_index, hipStream_t st);
+void table_sample_launch(const float* importance, const int64_t* group, int N, int64_t group_index,
+                         int ndraw, uint32_t seed, uint64_t counter, int64_t* out,
+                         hipStream_t st);
+
+// ------------------------------------------------------------------ optimizer
+struct OptSeg {
+  long long off;                 // element offset in the flat buffer (multiple of 4)
+  int numel;
+  int kind;                      // 0 plain, 1 conv weight (also write bf16 copies)
+  int K, R, S, C, Cpad;
+  bf16* w_krsc;                  // [K][R][S][Cpad] bf16 (forward / wgrad)
+  bf16* w_crsk;                  // [C][R][S][K] bf16 (dgrad) or null
+};
+struct OptArgs {
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  const OptSeg* segs;
+  int nsegs;
+  long long total;               // padded flat length
+  const float* hyper;            // device: [0] lr [1] beta1 [2] beta2 [3] eps [4] wd
+  const int64_t* step;           // device step counter (t, already incremented)
+  int algo;                      // 0 adam, 1 sgd(momentum)
+  int zero_grad;
+};
+void optimizer_launch(const OptArgs& a, hipStream_t st);
+void step_begin_launch(int64_t* ctrl, hipStream_t st);
+void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long long total,
+                         hipStream_t st);
+
+// ------------------------------------------------------------------ misc
+void quantize_launch(const float* x, float* out, float* absmax_ws, long long n, uint32_t seed,
+                     uint64_t counter, hipStream_t st);
+struct PoolArgs {                 // max-pool / avg-pool NHWC bf16
+  const bf16* x;
+  bf16* y;
+  int* argmax;                   // [N*P*Q*C] (max) for backward, or null
+  int N, H, W, C, P, Q, k, stride, pad, is_max;
+};
+void pool2d_fwd_launch(const PoolArgs& a, hipStream_t st);
+void maxpool2d_bwd_launch(const PoolArgs& geom, const bf16* dy, bf16* dx, hipStream_t st);
+struct DwArgs {                   // depthwise 3x3 conv NHWC bf16
+  const bf16* x;
+  const float* w;                // [C][3][3] fp32 master
+  bf16* y;
+  float* stats;                  // BN sums [G][2][C] or null
+  int N, H, W, C, P, Q, stride, pad, group_rows;
+};
+void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
+void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
+                         int P, int Q, int stride, int pad, hipStream_t st);
+void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
+                         int P, int Q, int stride, int pad, hipStream_t st);
+void nchw_to_nhwc8_launch(const float* x, bf16* y, int N, int C, int H, int W, int Cpad,
+                          hipStream_t st);

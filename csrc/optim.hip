@@ -1,0 +1,117 @@
+// Fused flat-buffer optimizer.
+//
+// One launch sweeps the whole flat fp32 parameter buffer (11.17M elements for
+// ResNet-18): Adam (torch.optim.Adam semantics, bias-corrected, L2 weight decay
+// folded into the gradient) or SGD with momentum, then -- in the same pass --
+// writes the bf16 operand copies the MFMA kernels consume:
+//   conv weight (master layout [K][R][S][C]) -> [K][R][S][Cpad] bf16 (fwd/wgrad B)
+//                                            -> [C][R][S][K]    bf16 (dgrad B)
+// and zeroes the gradient it consumed, so the next backward can accumulate with
+// atomics without a separate memset.  The reference does flatten -> all-reduce ->
+// divide -> unflatten -> per-tensor Adam -> (cuDNN re-reads fp32 weights); here
+// the all-reduce works in place on the same flat gradient and this is the only
+// optimizer pass.
+//
+// Segments are 4-element aligned in the flat buffer, so every thread handles one
+// float4 that never straddles two parameters.  Hyper-parameters (lr from the
+// cosine schedule) and the step counter live in device memory so the launch is
+// graph-capturable and replays with the current values.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int NT = 256;
+
+MA_DEV int find_seg(const OptSeg* s, int n, long long e) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s[mid].off <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+MA_DEV void write_copies(const OptSeg& sg, long long local, float v) {
+  if (sg.kind != 1 || local >= sg.numel) return;
+  const int rsc = sg.R * sg.S * sg.C;
+  const int k = (int)(local / rsc);
+  const int rem = (int)(local - (long long)k * rsc);
+  const int rs = rem / sg.C, c = rem - rs * sg.C;
+  const bf16 b = f2bf(v);
+  sg.w_krsc[((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c] = b;
+  if (sg.w_crsk) sg.w_crsk[((size_t)c * sg.R * sg.S + rs) * sg.K + k] = b;
+}
+
+__global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
+  const long long i4 = (long long)blockIdx.x * NT + threadIdx.x;
+  const long long e = i4 * 4;
+  if (e >= a.total) return;
+  const int si = find_seg(a.segs, a.nsegs, e);
+  const OptSeg sg = a.segs[si];
+  const float lr = a.hyper[0], b1 = a.hyper[1], b2 = a.hyper[2], eps = a.hyper[3], wd = a.hyper[4];
+  float4 p = *(const float4*)(a.p + e);
+  float4 g = *(const float4*)(a.g + e);
+  float4 m = *(const float4*)(a.m + e);
+  float pv[4] = {p.x, p.y, p.z, p.w}, gv[4] = {g.x, g.y, g.z, g.w}, mv[4] = {m.x, m.y, m.z, m.w};
+  if (a.algo == 0) {
+    float4 v = *(const float4*)(a.v + e);
+    float vv[4] = {v.x, v.y, v.z, v.w};
+    const float t = (float)(*a.step);
+    const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+    const float step_size = lr / bc1, rbc2 = rsqrtf(bc2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gv[k];
+      if (wd != 0.f) gk += wd * pv[k];
+      mv[k] = b1 * mv[k] + (1.f - b1) * gk;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
+      const float denom = sqrtf(vv[k]) * rbc2 + eps;
+      pv[k] -= step_size * mv[k] / denom;
+    }
+    *(float4*)(a.v + e) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+  } else {
+    const float mom = b1;
+    const bool first = *a.step <= 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gv[k];
+      if (wd != 0.f) gk += wd * pv[k];
+      mv[k] = first ? gk : mom * mv[k] + gk;
+      pv[k] -= lr * mv[k];
+    }
+  }
+  *(float4*)(a.p + e) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  *(float4*)(a.m + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+  if (a.zero_grad) *(float4*)(a.g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sg.kind == 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) write_copies(sg, e + k - sg.off, pv[k]);
+  }
+}
+
+__global__ __launch_bounds__(NT) void pack_kernel(const float* p, const OptSeg* segs, int nsegs,
+                                                  long long total) {
+  const long long e = (long long)blockIdx.x * NT + threadIdx.x;
+  if (e >= total) return;
+  const OptSeg sg = segs[find_seg(segs, nsegs, e)];
+  write_copies(sg, e - sg.off, p[e]);
+}
+
+__global__ void step_begin_kernel(int64_t* ctrl) { ctrl[2] += 1; }
+}  // namespace
+
+void optimizer_launch(const OptArgs& a, hipStream_t st) {
+  const long long n4 = (a.total + 3) / 4;
+  hipLaunchKernelGGL(optimizer_kernel, dim3((unsigned)((n4 + NT - 1) / NT)), dim3(NT), 0, st, a);
+}
+
+void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long long total,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, p, segs,
+                     nsegs, total);
+}
+
+void step_begin_launch(int64_t* ctrl, hipStream_t st) {
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, st, ctrl);
+}

@@ -1,0 +1,83 @@
+"""Python front-end for the CDNA4 HIP kernels in ``csrc/``.
+
+Each wrapper validates shapes / dtypes / devices / contiguity and then calls the
+raw launcher in ``mercury_amd._C`` on the *current* HIP stream (so every call
+is capturable into a HIP graph).  There is no silent fallback: on a machine
+with a GPU, a missing or stale extension raises; the pure-torch reference
+implementations live in ``mercury_amd.ops.reference`` and are used only by
+tests and by the CPU engine.
+
+Layout conventions: activations NHWC bf16 with channels padded to a multiple
+of 8; conv weights bf16 [K][R][S][Cpad] (forward) and [C][R][S][K] (dgrad);
+gradients and optimizer state fp32.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch
+
+_lib = None
+_err = None
+
+
+def lib():
+    """The loaded extension; builds it in-tree on first use if absent."""
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    try:
+        _lib = importlib.import_module('mercury_amd._C')
+    except ImportError as e:  # try an in-tree build (hipcc is in the image)
+        _err = e
+        if os.environ.get('MERCURY_NO_AUTOBUILD'):
+            raise
+        from .. import _build
+        _build.build(verbose=True)
+        _lib = importlib.import_module('mercury_amd._C')
+    return _lib
+
+
+def available():
+    try:
+        lib()
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t, dtype, name, numel=None):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError('%s must be a HIP device tensor' % name)
+    if t.dtype != dtype:
+        raise TypeError('%s: expected %s, got %s' % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError('%s must be contiguous' % name)
+    if numel is not None and t.numel() < numel:
+        raise ValueError('%s too small: %d < %d' % (name, t.numel(), numel))
+
+
+from .conv import (ConvSpec, conv_fwd, conv_dgrad, conv_wgrad, pick_tiles, pack_conv_weight,  # noqa: E402
+                   to_nhwc, from_nhwc)
+from .bn import bn_apply, bn_bwd, BnRunTable  # noqa: E402
+from .head import head_fwd, head_bwd  # noqa: E402
+from .importance import pool_build, is_sample, gather, table_write, table_sample  # noqa: E402
+from .optim import FlatOptimizer  # noqa: E402
+from .misc import quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad  # noqa: E402
+
+__all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_dgrad', 'conv_wgrad', 'pick_tiles',
+           'pack_conv_weight', 'to_nhwc', 'from_nhwc', 'bn_apply', 'bn_bwd', 'BnRunTable',
+           'head_fwd', 'head_bwd', 'pool_build', 'is_sample', 'gather', 'table_write',
+           'table_sample', 'FlatOptimizer', 'quantize', 'pool2d_fwd', 'maxpool2d_bwd',
+           'dwconv_fwd', 'dwconv_dgrad', 'dwconv_wgrad']

@@ -1,0 +1,194 @@
+"""Convolution front-end: geometry, tile selection and the three MFMA GEMMs.
+
+``ConvSpec`` describes one conv layer at one batch size.  Tile choice targets
+the MI355X's 256 CUs: a launch should have >= ~256 workgroups, so small-M
+layers (layer3/4 of ResNet-18 at batch 32: M = 2048 / 512 rows) get split-K
+(fp32 partial tiles reduced by a fused epilogue kernel) and big-M layers (the
+B=320 scoring pass) use 128-row tiles.  Ghost-BN statistics need a tile never
+to straddle a 32-image stat group; ``pick_tiles`` enforces that.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _chk, lib, ptr, stream_ptr
+
+CU = 256
+
+
+def cpad8(c):
+    return (c + 7) // 8 * 8
+
+
+@dataclass
+class ConvSpec:
+    N: int
+    H: int
+    W: int
+    C: int          # real input channels
+    K: int          # output channels
+    R: int
+    S: int
+    stride: int = 1
+    pad: int = 0
+    group_rows: int = 0   # rows per BN ghost group in the output (0 = whole batch)
+
+    @property
+    def Cp(self):
+        return cpad8(self.C)
+
+    @property
+    def P(self):
+        return (self.H + 2 * self.pad - self.R) // self.stride + 1
+
+    @property
+    def Q(self):
+        return (self.W + 2 * self.pad - self.S) // self.stride + 1
+
+    @property
+    def M(self):
+        return self.N * self.P * self.Q
+
+    def flops(self):
+        return 2.0 * self.M * self.K * self.R * self.S * self.C
+
+
+def pick_tiles(M, Ncols, kchunks, group_rows=0, min_blocks=CU):
+    """(bm, bn, splits) for the NT implicit GEMM."""
+    bn = 64 if Ncols <= 64 else 128
+    cands = [128, 64] if bn == 128 else [256, 128, 64]
+    grp = group_rows if group_rows and group_rows < M else 0
+    bm = None
+    for c in cands:
+        if grp and grp % c:
+            continue
+        bm = c
+        if math.ceil(M / c) * math.ceil(Ncols / bn) >= min_blocks:
+            break
+    if bm is None:
+        raise ValueError('no tile divides the BN ghost group (%d rows)' % group_rows)
+    blocks = math.ceil(M / bm) * math.ceil(Ncols / bn)
+    ktiles = math.ceil(kchunks / 8)
+    splits = 1
+    if blocks < min_blocks * 3 // 4 and ktiles >= 8:
+        splits = min(math.ceil(min_blocks / blocks), max(1, ktiles // 4), 16)
+    return bm, bn, splits
+
+
+def slab_bytes(M, Ncols, bm, bn, splits):
+    if splits <= 1:
+        return 0
+    return splits * math.ceil(M / bm) * math.ceil(Ncols / bn) * bm * bn * 4
+
+
+def fwd_plan(spec: ConvSpec):
+    kchunks = spec.R * spec.S * spec.Cp // 8
+    return pick_tiles(spec.M, spec.K, kchunks, spec.group_rows)
+
+
+def dgrad_plan(spec: ConvSpec):
+    kchunks = spec.R * spec.S * cpad8(spec.K) // 8
+    return pick_tiles(spec.N * spec.H * spec.W, spec.Cp, kchunks, 0)
+
+
+def wgrad_plan(spec: ConvSpec):
+    ncols = spec.R * spec.S * spec.Cp
+    bm = 64 if spec.K <= 64 else 128
+    bn = 64 if ncols <= 64 or spec.K > 256 and ncols < 1024 else 128
+    blocks = math.ceil(spec.K / bm) * math.ceil(ncols / bn)
+    ptiles = math.ceil(spec.M / 64)
+    splits = 1
+    if blocks < CU:
+        splits = max(1, min(math.ceil(2 * CU / blocks), ptiles // 4, 64))
+    return bm, bn, splits
+
+
+def _slab(slab, need, device):
+    if slab is not None and slab.numel() * slab.element_size() >= need:
+        return slab
+    if slab is None and not torch.cuda.is_current_stream_capturing():
+        return torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+    raise ValueError('split-K slab too small (%d < %d bytes)' % (
+        0 if slab is None else slab.numel() * slab.element_size(), need))
+
+
+def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=None,
+             accumulate=False):
+    """out[M][K] = conv(x NHWC, w [K][R][S][Cp]); optional BN-sum epilogue."""
+    Cp = spec.Cp
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
+    _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * Cp)
+    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    bm, bn, splits = plan or fwd_plan(spec)
+    if splits > 1:
+        slab = _slab(slab, slab_bytes(spec.M, spec.K, bm, bn, splits), x.device)
+    grp = spec.group_rows if spec.group_rows else spec.M
+    lib().igemm(ptr(x), ptr(w), ptr(out), spec.K, ptr(bias), ptr(stats), spec.K, grp,
+                int(accumulate), ptr(slab) if splits > 1 else 0,
+                spec.H, spec.W, Cp, spec.P, spec.Q, spec.R, spec.S, spec.stride, spec.pad,
+                spec.R * spec.S * Cp // 8, spec.K, spec.M, bm, bn, splits, False, stream_ptr())
+    return out
+
+
+def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False):
+    """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2."""
+    if spec.stride not in (1, 2):
+        raise ValueError('dgrad supports stride 1/2')
+    if spec.K % 8:
+        raise ValueError('dgrad needs K % 8 == 0')
+    Cp = spec.Cp
+    _chk(dy, torch.bfloat16, 'dy', spec.M * spec.K)
+    _chk(wt, torch.bfloat16, 'wt', Cp * spec.R * spec.S * spec.K)
+    _chk(dx, torch.bfloat16, 'dx', spec.N * spec.H * spec.W * Cp)
+    bm, bn, splits = plan or dgrad_plan(spec)
+    Mx = spec.N * spec.H * spec.W
+    if splits > 1:
+        slab = _slab(slab, slab_bytes(Mx, Cp, bm, bn, splits), dy.device)
+    lib().igemm(ptr(dy), ptr(wt), ptr(dx), Cp, 0, 0, Cp, Mx, int(accumulate),
+                ptr(slab) if splits > 1 else 0,
+                spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
+                spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, True, stream_ptr())
+    return dx
+
+
+def conv_wgrad(dy, x, dw, spec: ConvSpec, plan=None):
+    """dw[K][R][S][C] (fp32, channel padding dropped) += / = wgrad(dy, x)."""
+    _chk(dy, torch.bfloat16, 'dy', spec.M * spec.K)
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * spec.Cp)
+    _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
+    if spec.K % 8:
+        raise ValueError('wgrad needs K % 8 == 0')
+    bm, bn, splits = plan or wgrad_plan(spec)
+    lib().wgrad(ptr(dy), ptr(x), ptr(dw), spec.N, spec.H, spec.W, spec.Cp, spec.P, spec.Q,
+                spec.K, spec.R, spec.S, spec.stride, spec.pad, spec.C, bm, bn, splits,
+                stream_ptr())
+    return dw
+
+
+# ----------------------------------------------------------------------- layout helpers
+def to_nhwc(x, cpad=None):
+    """NCHW float -> NHWC bf16 with channels padded to ``cpad`` (default: next multiple of 8)."""
+    n, c, h, w = x.shape
+    cp = cpad or cpad8(c)
+    out = torch.zeros(n, h, w, cp, dtype=torch.bfloat16, device=x.device)
+    out[..., :c] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return out
+
+
+def from_nhwc(y, c=None):
+    """NHWC (padded) -> NCHW float32."""
+    c = c or y.shape[-1]
+    return y[..., :c].permute(0, 3, 1, 2).float()
+
+
+def pack_conv_weight(w_kcrs):
+    """fp32 torch conv weight [K][C][R][S] -> (bf16 [K][R][S][Cp], bf16 [C][R][S][K])."""
+    k, c, r, s = w_kcrs.shape
+    krsc = torch.zeros(k, r, s, cpad8(c), dtype=torch.bfloat16, device=w_kcrs.device)
+    krsc[..., :c] = w_kcrs.permute(0, 2, 3, 1).to(torch.bfloat16)
+    crsk = w_kcrs.permute(1, 2, 3, 0).contiguous().to(torch.bfloat16)
+    return krsc.contiguous(), crsk

@@ -1,0 +1,45 @@
+"""Importance-sampling kernels front-end (``csrc/importance.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from . import _chk, lib, ptr, stream_ptr
+from ..data.transforms import CIFAR_MEAN, CIFAR_STD
+
+
+def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed, pad=4,
+               flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD):
+    """Build a P-sample presample pool from the uint8 shard [Ns][H][W][3] on device."""
+    _chk(shard, torch.uint8, 'shard')
+    _chk(labels, torch.int64, 'labels')
+    Ns, H, W, _ = shard.shape
+    _chk(pool, torch.bfloat16, 'pool', P * H * W * 8)
+    lib().pool_build(ptr(shard), ptr(labels), ptr(ctrl), ptr(pool), ptr(pool_label),
+                     ptr(pool_index), Ns, H, W, P, batch, pad, int(flip), int(augment),
+                     int(seed) & 0xffffffff, list(mean), [1.0 / s for s in std], stream_ptr())
+
+
+def is_sample(losses, ema, ctrl, idx, w, P, B, group, alpha=0.5, ema_alpha=0.9, seed=0,
+              importance=True, meters=None):
+    _chk(losses, torch.float32, 'losses', P)
+    _chk(idx, torch.int32, 'idx', B)
+    lib().is_sample(ptr(losses), ptr(ema), ptr(ctrl), ptr(idx), ptr(w), ptr(meters), P, B, group,
+                    int(importance), alpha, ema_alpha, int(seed) & 0xffffffff, stream_ptr())
+
+
+def gather(pool, pool_label, pool_index, idx, batch, batch_label, batch_index, B):
+    per_img = pool[0].numel() * 2 // 16
+    lib().gather(ptr(pool), ptr(pool_label), ptr(pool_index), ptr(idx), ptr(batch),
+                 ptr(batch_label), ptr(batch_index), B, per_img, stream_ptr())
+
+
+def table_write(importance, group, losses, start, group_index):
+    n = losses.numel()
+    lib().table_write(ptr(importance), ptr(group), ptr(losses.float().contiguous()), start, n,
+                      int(group_index), stream_ptr())
+
+
+def table_sample(importance, group, group_index, ndraw, seed, counter, out):
+    lib().table_sample(ptr(importance), ptr(group), importance.numel(), int(group_index), ndraw,
+                       int(seed) & 0xffffffff, int(counter), ptr(out), stream_ptr())
+    return out

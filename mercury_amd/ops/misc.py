@@ -1,0 +1,38 @@
+"""Pooling, depthwise conv, quantisation front-ends (``csrc/misc.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from . import _chk, lib, ptr, stream_ptr
+
+
+def quantize(x, out=None, ws=None, seed=0, counter=0):
+    _chk(x, torch.float32, 'x')
+    out = torch.empty_like(x) if out is None else out
+    ws = torch.empty(1, dtype=torch.float32, device=x.device) if ws is None else ws
+    lib().quantize(ptr(x), ptr(out), ptr(ws), x.numel(), int(seed) & 0xffffffff, int(counter),
+                   stream_ptr())
+    return out
+
+
+def pool2d_fwd(x, y, N, H, W, C, P, Q, k, stride, pad, is_max=True, argmax=None):
+    lib().pool2d_fwd(ptr(x), ptr(y), ptr(argmax), N, H, W, C, P, Q, k, stride, pad, int(is_max),
+                     stream_ptr())
+
+
+def maxpool2d_bwd(dy, argmax, dx, N, H, W, C, P, Q, k, stride, pad):
+    lib().maxpool2d_bwd(ptr(dy), ptr(argmax), ptr(dx), N, H, W, C, P, Q, k, stride, pad,
+                        stream_ptr())
+
+
+def dwconv_fwd(x, w, y, N, H, W, C, P, Q, stride, pad, stats=None, group_rows=0):
+    lib().dwconv_fwd(ptr(x), ptr(w), ptr(y), ptr(stats), N, H, W, C, P, Q, stride, pad,
+                     group_rows or N * P * Q, stream_ptr())
+
+
+def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad):
+    lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr())
+
+
+def dwconv_wgrad(dy, x, dw, N, H, W, C, P, Q, stride, pad):
+    lib().dwconv_wgrad(ptr(dy), ptr(x), ptr(dw), N, H, W, C, P, Q, stride, pad, stream_ptr())

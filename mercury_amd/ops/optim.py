@@ -1,0 +1,56 @@
+"""Fused flat-buffer optimizer front-end (``csrc/optim.hip``).
+
+``FlatOptimizer`` owns fp32 ``p``/``g``/``m``/``v`` flat buffers (4-element
+aligned segments), a device segment table describing which segments are conv
+weights (and where their bf16 MFMA operand copies live), and a device
+hyper-parameter vector ``[lr, beta1, beta2, eps, weight_decay]``.  ``step``
+is one launch; ``set_lr`` is a 4-byte host->device copy done outside graphs
+(the cosine schedule changes lr once per epoch).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import lib, ptr, stream_ptr
+
+
+class FlatOptimizer(object):
+
+    def __init__(self, segments, total, device, algo='adam', lr=1e-3, betas=(0.9, 0.999),
+                 eps=1e-8, weight_decay=0.0, momentum=0.9):
+        self.device = torch.device(device)
+        self.total = int(total)
+        self.segments = segments
+        self.p = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.g = torch.zeros_like(self.p)
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p) if algo == 'adam' else torch.zeros(4, device=device)
+        self.algo = 0 if algo == 'adam' else 1
+        b1 = betas[0] if algo == 'adam' else momentum
+        self.hyper = torch.tensor([lr, b1, betas[1], eps, weight_decay, 0, 0, 0],
+                                  dtype=torch.float32, device=device)
+        rows = []
+        for s in segments:
+            rows.append([s['off'], s['numel'], s['kind'], s.get('K', 0), s.get('R', 1),
+                         s.get('S', 1), s.get('C', 1), s.get('Cpad', 1),
+                         ptr(s.get('w_krsc')), ptr(s.get('w_crsk'))])
+        packed = lib().pack_opt_segs(rows)
+        self.segbuf = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(device)
+        self.nsegs = len(rows)
+
+    @property
+    def lr(self):
+        return float(self.hyper[0].item())
+
+    def set_lr(self, lr):
+        self.hyper[0].fill_(float(lr))
+
+    def step(self, step_counter, zero_grad=True):
+        """``step_counter``: device int64 scalar tensor/view holding t (already incremented)."""
+        lib().optimizer(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), ptr(self.segbuf),
+                        self.nsegs, self.total, ptr(self.hyper), ptr(step_counter), self.algo,
+                        int(zero_grad), stream_ptr())
+
+    def pack_weights(self):
+        """Write the bf16 conv-weight copies from the fp32 master (after init / load)."""
+        lib().pack_weights(ptr(self.p), ptr(self.segbuf), self.nsegs, self.total, stream_ptr())

@@ -1,0 +1,425 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (SURVEY §4 layer 2).
+
+Inputs are rounded to bf16 first so the reference sees exactly what the kernel
+sees; tolerances then only cover bf16 output rounding / fp32 summation order.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _ops():
+    from mercury_amd import ops
+    ops.lib()
+    return ops
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, 'max err %g (scale %g)' % (err, scale)
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, S, stride, pad
+    (4, 32, 32, 3, 64, 3, 3, 1, 1),      # CIFAR stem (C padded to 8)
+    (4, 32, 32, 64, 64, 3, 3, 1, 1),
+    (4, 32, 32, 64, 128, 3, 3, 2, 1),
+    (4, 32, 32, 64, 128, 1, 1, 2, 0),    # shortcut
+    (8, 8, 8, 256, 512, 3, 3, 2, 1),     # small M -> split-K
+    (32, 4, 4, 512, 512, 3, 3, 1, 1),    # layer4 at batch 32
+    (2, 16, 16, 96, 24, 1, 1, 1, 0),     # MobileNet-style odd channels
+]
+
+
+def _mk(case, seed=0):
+    N, H, W, C, K, R, S, st, pd = case
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    x = bf(torch.randn(N, C, H, W, generator=g)).to(DEV)
+    w = bf(torch.randn(K, C, R, S, generator=g) / math.sqrt(C * R * S)).to(DEV)
+    return x, w
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv_fwd_and_stats(case):
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes
+    N, H, W, C, K, R, S, st, pd = case
+    x, w = _mk(case)
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    xn = ops.to_nhwc(x)
+    wk, _ = ops.pack_conv_weight(w)
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(2, K, device=DEV)
+    plan = fwd_plan(spec)
+    slab = torch.empty(max(1, slab_bytes(spec.M, K, *plan) // 4), device=DEV)
+    ops.conv_fwd(xn, wk, out, spec, stats=stats, slab=slab, plan=plan)
+    ref = F.conv2d(x, w, stride=st, padding=pd)
+    got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2)
+    close(got, ref)
+    yb = bf(ref)
+    close(stats[0], yb.sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+    close(stats[1], (yb * yb).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+
+
+@pytest.mark.parametrize('bm_bn_split', [(128, 128, 1), (64, 64, 3), (128, 64, 2), (64, 128, 1),
+                                         (256, 64, 1)])
+def test_conv_fwd_all_tiles(bm_bn_split):
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, slab_bytes
+    case = (4, 16, 16, 64, 128, 3, 3, 1, 1)
+    x, w = _mk(case, 3)
+    spec = ConvSpec(*case)
+    out = torch.empty(spec.M, 128, dtype=torch.bfloat16, device=DEV)
+    slab = torch.empty(max(1, slab_bytes(spec.M, 128, *bm_bn_split) // 4), device=DEV)
+    ops.conv_fwd(ops.to_nhwc(x), ops.pack_conv_weight(w)[0], out, spec, slab=slab,
+                 plan=bm_bn_split)
+    close(out.view(4, 16, 16, 128).permute(0, 3, 1, 2), F.conv2d(x, w, padding=1))
+
+
+def test_conv_ghost_group_stats():
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec
+    N = 64
+    case = (N, 8, 8, 64, 64, 3, 3, 1, 1)
+    x, w = _mk(case, 1)
+    spec = ConvSpec(*case, group_rows=32 * 64)
+    out = torch.empty(spec.M, 64, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(2, 2, 64, device=DEV)
+    ops.conv_fwd(ops.to_nhwc(x), ops.pack_conv_weight(w)[0], out, spec, stats=stats)
+    ref = bf(F.conv2d(x, w, padding=1))
+    for gi in range(2):
+        r = ref[gi * 32:(gi + 1) * 32]
+        close(stats[gi, 0], r.sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+
+
+@pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] % 8 == 0])
+def test_conv_dgrad(case):
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, dgrad_plan, slab_bytes
+    N, H, W, C, K, R, S, st, pd = case
+    x, w = _mk(case)
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    gy = bf(torch.randn(N, K, spec.P, spec.Q, device=DEV))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, stride=st, padding=pd).backward(gy)
+    _, wt = ops.pack_conv_weight(w)
+    dx = torch.empty(N * H * W, spec.Cp, dtype=torch.bfloat16, device=DEV)
+    plan = dgrad_plan(spec)
+    slab = torch.empty(max(1, slab_bytes(N * H * W, spec.Cp, *plan) // 4), device=DEV)
+    ops.conv_dgrad(ops.to_nhwc(gy), wt, dx, spec, slab=slab, plan=plan)
+    close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
+    # accumulate mode adds onto existing contents
+    dx2 = dx.clone()
+    ops.conv_dgrad(ops.to_nhwc(gy), wt, dx2, spec, slab=slab, plan=plan, accumulate=True)
+    close(ops.from_nhwc(dx2.view(N, H, W, spec.Cp), C), 2 * xr.grad, rtol=3e-2)
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv_wgrad(case):
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec
+    N, H, W, C, K, R, S, st, pd = case
+    if K % 8:
+        pytest.skip('K % 8')
+    x, w = _mk(case)
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    gy = bf(torch.randn(N, K, spec.P, spec.Q, device=DEV))
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(x, wr, stride=st, padding=pd).backward(gy)
+    dw = torch.zeros(K, R, S, C, device=DEV)
+    ops.conv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(x), dw, spec)
+    close(dw.permute(0, 3, 1, 2), wr.grad, rtol=2e-2, atol=1e-2)
+    for plan in [(64, 64, 1), (128, 128, 3), (64, 128, 2), (128, 64, 5)]:
+        dw2 = torch.zeros_like(dw)
+        ops.conv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(x), dw2, spec, plan=plan)
+        close(dw2, dw, rtol=1e-2, atol=1e-2)
+
+
+def _bn_ref(y, gamma, beta, eps=1e-5):
+    m = y.mean((0, 2, 3), keepdim=True)
+    v = y.var((0, 2, 3), unbiased=False, keepdim=True)
+    return (y - m) / torch.sqrt(v + eps) * gamma.view(1, -1, 1, 1) + beta.view(1, -1, 1, 1)
+
+
+def test_bn_apply_and_bwd_with_bn_shortcut():
+    ops = _ops()
+    N, C, H, W = 8, 64, 8, 8
+    M = N * H * W
+    torch.manual_seed(0)
+    y = bf(torch.randn(N, C, H, W, device=DEV) * 2 + 0.5)
+    y2 = bf(torch.randn(N, C, H, W, device=DEV))
+    g1, b1 = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    g2, b2 = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    yn, y2n = ops.to_nhwc(y).view(M, C), ops.to_nhwc(y2).view(M, C)
+    st1 = torch.stack([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3))])
+    st2 = torch.stack([y2.sum((0, 2, 3)), (y2 * y2).sum((0, 2, 3))])
+    out = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ops.bn_apply(yn, st1, g1, b1, out, M, C, act='relu', res=y2n, res_bn=(st2, g2, b2))
+    yr, y2r = y.clone().requires_grad_(True), y2.clone().requires_grad_(True)
+    g1r, b1r, g2r, b2r = [t.clone().requires_grad_(True) for t in (g1, b1, g2, b2)]
+    ref = F.relu(_bn_ref(yr, g1r, b1r) + _bn_ref(y2r, g2r, b2r))
+    close(ops.from_nhwc(out.view(N, H, W, C)), ref)
+    dout = bf(torch.randn_like(ref))
+    ref.backward(dout)
+    sums = torch.zeros(3, C, device=DEV)
+    dy = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    dy2 = torch.empty_like(dy)
+    dz = torch.empty_like(dy)
+    dg1, db1, dg2, db2 = [torch.zeros(C, device=DEV) for _ in range(4)]
+    ops.bn_bwd(ops.to_nhwc(dout).view(M, C), out, yn, st1, g1, sums, dy, M, C, act='relu',
+               y2=y2n, stats2=st2, gamma2=g2, dy2=dy2, dz=dz, dgamma=dg1, dbeta=db1,
+               dgamma2=dg2, dbeta2=db2)
+    close(ops.from_nhwc(dy.view(N, H, W, C)), yr.grad, rtol=3e-2, atol=3e-2)
+    close(ops.from_nhwc(dy2.view(N, H, W, C)), y2r.grad, rtol=3e-2, atol=3e-2)
+    close(dg1, g1r.grad, rtol=2e-2, atol=0.5)
+    close(db1, b1r.grad, rtol=2e-2, atol=0.5)
+    close(dg2, g2r.grad, rtol=2e-2, atol=0.5)
+    close(db2, b2r.grad, rtol=2e-2, atol=0.5)
+
+
+def test_bn_apply_ghost_groups_identity_residual_eval():
+    ops = _ops()
+    N, C, H, W = 64, 16, 4, 4
+    M = N * H * W
+    y = bf(torch.randn(N, C, H, W, device=DEV))
+    r = bf(torch.randn(N, C, H, W, device=DEV))
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    st = torch.zeros(2, 2, C, device=DEV)
+    for gi in range(2):
+        yy = y[gi * 32:(gi + 1) * 32]
+        st[gi, 0], st[gi, 1] = yy.sum((0, 2, 3)), (yy * yy).sum((0, 2, 3))
+    out = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ops.bn_apply(ops.to_nhwc(y).view(M, C), st, g, b, out, M, C, group_rows=32 * 16, act='relu',
+                 res=ops.to_nhwc(r).view(M, C))
+    ref = torch.cat([F.relu(_bn_ref(y[i * 32:(i + 1) * 32], g, b) + r[i * 32:(i + 1) * 32])
+                     for i in range(2)])
+    close(ops.from_nhwc(out.view(N, H, W, C)), ref)
+    rm, rv = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    ops.bn_apply(ops.to_nhwc(y).view(M, C), None, g, b, out, M, C, act='relu6', running=(rm, rv))
+    ref = F.relu6(F.batch_norm(y, rm, rv, g, b, False))
+    close(ops.from_nhwc(out.view(N, H, W, C)), ref)
+
+
+def test_bn_running_update_matches_torch():
+    ops = _ops()
+    C = 32
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    xs = [bf(torch.randn(32, C, 4, 4, device=DEV) * 3 + 1) for _ in range(11)]
+    for x in xs:
+        bn(x)  # train mode: 11 momentum updates (1 train + 10 scoring)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    st = [torch.stack([x.sum((0, 2, 3)), (x * x).sum((0, 2, 3))]) for x in xs]
+    st_train, st_score = st[0].contiguous(), torch.stack(st[1:]).contiguous()
+    tab = ops.BnRunTable([(rm, rv, st_train, st_score, nbt, C, 1, 10, 512.0, 512.0)], DEV)
+    tab.launch(0.1)
+    close(rm, bn.running_mean, rtol=1e-4, atol=1e-4)
+    close(rv, bn.running_var, rtol=1e-4, atol=1e-4)
+    assert int(nbt.item()) == 11
+
+
+def test_head_fwd_bwd_is_weighted():
+    ops = _ops()
+    B, HW, C, K = 32, 16, 512, 10
+    act = bf(torch.rand(B, HW, C, device=DEV))
+    w = torch.randn(K, C, device=DEV) * 0.05
+    b = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (B,), device=DEV)
+    isw = torch.rand(B, device=DEV) + 0.5
+    pooled = torch.empty(B, C, device=DEV)
+    dlog = torch.empty(B, K, device=DEV)
+    losses = torch.empty(B, device=DEV)
+    meters = torch.zeros(8, device=DEV)
+    ops.head_fwd(act.to(torch.bfloat16), w, b, lab.int(), B, HW, C, K, 'train', pooled=pooled,
+                 dlogits=dlog, losses=losses, isw=isw, meters=meters)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ar = act.clone().requires_grad_(True)
+    logits = ar.mean(1) @ wr.t() + br
+    l = F.cross_entropy(logits, lab, reduction='none')
+    close(losses, l, rtol=1e-4, atol=1e-4)
+    loss = (l / isw).mean()
+    loss.backward()
+    assert abs(meters[0].item() - loss.item() * B) < 1e-3 * B
+    assert meters[2].item() == (logits.argmax(1) == lab).sum().item()
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    dact = torch.empty(B, HW, C, dtype=torch.bfloat16, device=DEV)
+    ops.head_bwd(pooled, dlog, w, dw, db, dact, B, HW, C, K)
+    close(dw, wr.grad, rtol=1e-3, atol=1e-5)
+    close(db, br.grad, rtol=1e-3, atol=1e-5)
+    close(dact, ar.grad, rtol=2e-2, atol=1e-5)
+
+
+def test_pool_build_epoch_permutation_and_normalisation():
+    ops = _ops()
+    from mercury_amd.data.transforms import CIFAR_MEAN, CIFAR_STD
+    Ns, P, B = 100, 32, 16
+    shard = torch.randint(0, 256, (Ns, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labels = torch.arange(Ns, device=DEV) % 10
+    ctrl = torch.zeros(4, dtype=torch.int64, device=DEV)
+    pool = torch.empty(P, 32, 32, 8, dtype=torch.bfloat16, device=DEV)
+    pl, pi = torch.empty(P, dtype=torch.int32, device=DEV), torch.empty(P, dtype=torch.int32, device=DEV)
+    seen = []
+    for pc in range(3):  # 6 batches of 16 = 96 = one epoch of 6 batches (drop_last of 100)
+        ctrl[0] = pc
+        ops.pool_build(shard, labels, ctrl, pool, pl, pi, P, B, seed=7, augment=False)
+        seen += pi.tolist()
+        assert torch.equal(pl.long(), labels[pi.long()])
+    assert len(set(seen)) == 96  # no repeats inside an epoch
+    # normalisation of the un-augmented view
+    mean = torch.tensor(CIFAR_MEAN, device=DEV)
+    std = torch.tensor(CIFAR_STD, device=DEV)
+    ref = (shard[pi.long()].float() / 255 - mean) / std
+    close(pool[..., :3].float(), ref, rtol=1e-2, atol=2e-2)
+    assert pool[..., 3:].abs().max().item() == 0
+    # augmented: crop+flip keeps values from the same image's value set or the pad value
+    ops.pool_build(shard, labels, ctrl, pool, pl, pi, P, B, seed=7, augment=True)
+    assert torch.isfinite(pool.float()).all()
+
+
+def test_is_sample_ema_and_distribution():
+    ops = _ops()
+    from mercury_amd.utils import EMAverage
+    P, B = 320, 32
+    torch.manual_seed(0)
+    losses = torch.rand(P, device=DEV) * 3
+    ema = torch.zeros(2, device=DEV)
+    ctrl = torch.zeros(4, dtype=torch.int64, device=DEV)
+    idx = torch.empty(B, dtype=torch.int32, device=DEV)
+    w = torch.empty(B, device=DEV)
+    ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1)
+    ref = EMAverage()
+    for j in range(10):
+        ref.update(losses[:32 * (j + 1)].mean().item())
+    assert abs(ema[0].item() - ref.value) < 1e-5
+    p = (losses + 0.5 * ema[0]) / (losses + 0.5 * ema[0]).sum()
+    close(w, p[idx.long()] * P, rtol=1e-4, atol=1e-5)
+    assert int(ctrl[0].item()) == 1
+    counts = torch.zeros(P, device=DEV)
+    n = 0
+    for _ in range(600):
+        ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1)
+        counts.index_add_(0, idx.long(), torch.ones(B, device=DEV))
+        n += B
+    p = (losses + 0.5 * ema[0]) / (losses + 0.5 * ema[0]).sum()
+    chi2 = ((counts / n - p) ** 2 / p).sum().item() * n
+    assert chi2 < P + 6 * math.sqrt(2 * P), chi2
+
+
+def test_gather_and_table_sampler():
+    ops = _ops()
+    P, B = 64, 8
+    pool = torch.randn(P, 4, 4, 8, device=DEV).to(torch.bfloat16)
+    pl = torch.arange(P, dtype=torch.int32, device=DEV)
+    pi = pl * 3
+    idx = torch.randint(0, P, (B,), dtype=torch.int32, device=DEV)
+    batch = torch.empty(B, 4, 4, 8, dtype=torch.bfloat16, device=DEV)
+    bl, bi = torch.empty(B, dtype=torch.int32, device=DEV), torch.empty(B, dtype=torch.int32, device=DEV)
+    ops.gather(pool, pl, pi, idx, batch, bl, bi, B)
+    assert torch.equal(batch, pool[idx.long()]) and torch.equal(bl, idx) and torch.equal(bi, idx * 3)
+    N = 5000
+    imp = torch.ones(N, device=DEV)
+    grp = torch.zeros(N, dtype=torch.int64, device=DEV)
+    losses = torch.rand(1000, device=DEV) * 4
+    ops.table_write(imp, grp, losses, 2000, 3)
+    assert torch.equal(imp[2000:3000], losses) and int(grp[2500].item()) == 3
+    out = torch.empty(20000, dtype=torch.int64, device=DEV)
+    ops.table_sample(imp, grp, 3, 20000, seed=5, counter=0, out=out)
+    assert out.min().item() >= 2000 and out.max().item() < 3000
+    w = losses + losses.mean()
+    p = w / w.sum()
+    freq = torch.bincount(out - 2000, minlength=1000).float() / 20000
+    assert ((freq - p).abs().sum().item()) < 0.25
+
+
+def test_fused_adam_matches_torch_and_writes_bf16_copies():
+    ops = _ops()
+    torch.manual_seed(0)
+    conv = torch.randn(16, 8, 3, 3, device=DEV) * 0.1
+    vec = torch.randn(10, device=DEV)
+    k, c, r, s = conv.shape
+    off2 = (conv.numel() + 3) // 4 * 4
+    total = off2 + 12
+    krsc = torch.zeros(k, r, s, c, dtype=torch.bfloat16, device=DEV)
+    crsk = torch.zeros(c, r, s, k, dtype=torch.bfloat16, device=DEV)
+    segs = [dict(off=0, numel=conv.numel(), kind=1, K=k, R=r, S=s, C=c, Cpad=c, w_krsc=krsc,
+                 w_crsk=crsk),
+            dict(off=off2, numel=10, kind=0)]
+    opt = ops.FlatOptimizer(segs, total, DEV, 'adam', lr=1e-2, weight_decay=0.01)
+    opt.p[:conv.numel()] = conv.permute(0, 2, 3, 1).reshape(-1)
+    opt.p[off2:off2 + 10] = vec
+    ref = [conv.clone().requires_grad_(True), vec.clone().requires_grad_(True)]
+    topt = torch.optim.Adam(ref, lr=1e-2, weight_decay=0.01)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for t in range(5):
+        g1, g2 = torch.randn_like(conv), torch.randn_like(vec)
+        ref[0].grad, ref[1].grad = g1.clone(), g2.clone()
+        topt.step()
+        opt.g[:conv.numel()] = g1.permute(0, 2, 3, 1).reshape(-1)
+        opt.g[off2:off2 + 10] = g2
+        step += 1
+        opt.step(step)
+        assert opt.g.abs().max().item() == 0  # gradient consumed and zeroed
+    close(opt.p[:conv.numel()].view(k, r, s, c).permute(0, 3, 1, 2), ref[0].detach(), 1e-5, 1e-6)
+    close(opt.p[off2:off2 + 10], ref[1].detach(), 1e-5, 1e-6)
+    close(krsc.float(), ref[0].detach().permute(0, 2, 3, 1), 1e-2, 1e-3)
+    close(crsk.float(), ref[0].detach().permute(1, 2, 3, 0), 1e-2, 1e-3)
+
+
+def test_quantize_pool_dwconv():
+    ops = _ops()
+    x = torch.randn(100000, device=DEV)
+    q = ops.quantize(x, seed=3)
+    m = x.abs().max()
+    assert set(torch.unique(q.abs()).tolist()) <= {0.0, m.item()}
+    acc = torch.zeros_like(x)
+    for i in range(200):
+        acc += ops.quantize(x, seed=3, counter=i)
+    assert (acc / 200 - x).abs().mean().item() < 0.15
+    # max pool 2x2 (VGG) and 3x3/s2/p1 (ImageNet stem), fwd + bwd
+    for (k, st, pd) in [(2, 2, 0), (3, 2, 1)]:
+        N, C, H, W = 2, 16, 12, 12
+        xx = bf(torch.randn(N, C, H, W, device=DEV)).requires_grad_(True)
+        ref = F.max_pool2d(xx, k, st, pd)
+        P, Q = ref.shape[2:]
+        y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
+        am = torch.empty(N * P * Q * C, dtype=torch.int32, device=DEV)
+        ops.pool2d_fwd(ops.to_nhwc(xx.detach()), y, N, H, W, C, P, Q, k, st, pd, True, am)
+        close(ops.from_nhwc(y), ref, 1e-3, 1e-3)
+        gy = bf(torch.randn_like(ref))
+        ref.backward(gy)
+        dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+        ops.maxpool2d_bwd(ops.to_nhwc(gy), am, dx, N, H, W, C, P, Q, k, st, pd)
+        close(ops.from_nhwc(dx), xx.grad, 1e-2, 1e-2)
+    # depthwise 3x3, stride 1 and 2
+    for st in (1, 2):
+        N, C, H, W = 4, 24, 8, 8
+        xx = bf(torch.randn(N, C, H, W, device=DEV)).requires_grad_(True)
+        w = torch.randn(C, 1, 3, 3, device=DEV).requires_grad_(True)
+        ref = F.conv2d(xx, bf(w), stride=st, padding=1, groups=C)
+        P, Q = ref.shape[2:]
+        y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
+        stats = torch.zeros(2, C, device=DEV)
+        wf = bf(w.detach()).reshape(C, 9).contiguous()
+        ops.dwconv_fwd(ops.to_nhwc(xx.detach()), wf, y, N, H, W, C, P, Q, st, 1, stats=stats)
+        close(ops.from_nhwc(y), ref)
+        close(stats[0], bf(ref).sum((0, 2, 3)), 1e-2, 0.5)
+        gy = bf(torch.randn_like(ref))
+        ref.backward(gy)
+        dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+        ops.dwconv_dgrad(ops.to_nhwc(gy), wf, dx, N, H, W, C, P, Q, st, 1)
+        close(ops.from_nhwc(dx), xx.grad)
+        dw = torch.zeros(C, 9, device=DEV)
+        ops.dwconv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(xx.detach()), dw, N, H, W, C, P, Q, st, 1)
+        close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
