@@ -1,0 +1,134 @@
+"""Headline benchmark: importance-sampled ResNet-18 / CIFAR-10-shape DP training.
+
+BASELINE.json metric: "images/sec (whole node) + sampler overhead %, ResNet-18
+CIFAR-10 DP 1/2/4/8 GPU".  Each rank runs the reference's default step
+(`pytorch_collab.py:127-164`): score a 10x32 = 320-sample presample pool
+(forward, ghost-BN per 32), draw 32 samples with replacement proportional to
+loss + 0.5*EMA, IS-weighted fwd+bwd on them, gradient all-reduce (RCCL),
+Adam.  Per-GPU batch is fixed (weak scaling); ``value`` counts TRAINED images
+per second over the whole job (N x 32 x steps / time).  The sampler overhead
+is measured in a second timed loop with importance scoring switched off
+(uniform 32-sample batches, no pool forward): overhead % = 1 - t_uniform/t_IS.
+
+Data: synthetic CIFAR-10-shaped uint8 images (class-conditional templates +
+noise), Dirichlet(0.5) non-IID shards (seed 102) -- no network access for the
+real dataset.  Weights are random-init ResNet-18 (11,173,962 params).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REF_CPU_IMG_S = 41.0   # reference step, W=1, 39-43 trained img/s (CPU, only measured number)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--model', default='resnet18')
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--pool-batches', type=int, default=10)
+    ap.add_argument('--no-overhead', action='store_true')
+    ap.add_argument('--no-graphs', action='store_true')
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from mercury_amd.parallel import dist as pdist
+    rank, ws, device = pdist.init_from_env()
+    if ws != args.gpus and rank == 0:
+        print('[bench] warning: WORLD_SIZE=%d but --gpus=%d' % (ws, args.gpus), file=sys.stderr)
+
+    from mercury_amd.data.datasets import synthetic_arrays
+    from mercury_amd.data.partition import dirichlet_partition
+    from mercury_amd.engine.native import NativeEngine
+    from mercury_amd.models import build_model
+
+    x_all, y_all = synthetic_arrays(50000, 10, seed=8)
+    np.random.seed(102)
+    shards = dirichlet_partition(y_all, ws, 0.5, 10) if ws > 1 else {0: np.arange(50000)}
+    idx = np.asarray(shards[rank])
+    torch.manual_seed(1234)
+    net = build_model(args.model, 10).to(device)
+
+    def make(importance):
+        eng = NativeEngine(net, device, args.batch, args.pool_batches, optimizer='adam',
+                           lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
+                           use_graphs=not args.no_graphs)
+        eng.set_shard(x_all[idx], y_all[idx])
+        if ws > 1:
+            eng.broadcast_from(0)
+        return eng
+
+    def run(eng, steps, warmup, scoring=True):
+        eng.scoring = scoring
+        eng.prime()
+        eng.step()
+        if eng.use_graphs:
+            eng.build_graphs()
+        for _ in range(warmup):
+            eng.step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        if ws > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item())
+
+    eng = make(True)
+    t_is = run(eng, args.steps, args.warmup)
+    m = eng.read_meters()
+    ms = t_is * 1e3 / args.steps
+    value = ws * args.batch * args.steps / t_is
+    overhead = None
+    if not args.no_overhead:
+        del eng
+        torch.cuda.synchronize()
+        eng_u = make(False)
+        t_u = run(eng_u, args.steps, args.warmup, scoring=False)
+        overhead = 100.0 * max(0.0, 1.0 - t_u / t_is)
+    if rank == 0:
+        out = {
+            'metric': 'images/sec (whole node) + sampler overhead %, ResNet-18 CIFAR-10 DP 1/2/4/8 GPU',
+            'value': round(value, 2), 'unit': 'trained images/s', 'n_gpus': ws,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 4),
+            'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': round(value / REF_CPU_IMG_S, 2),
+            'baseline_note': 'reference publishes no numbers; BASELINE.md measured its step at '
+                             '39-43 trained img/s (W=1, CPU); vs_baseline uses 41',
+            'sampler_overhead_pct': None if overhead is None else round(overhead, 2),
+            'scored_images_per_sec': round(ws * args.batch * args.pool_batches * args.steps / t_is, 1),
+            'dtype': 'bf16', 'data': 'synthetic',
+            'config': {'model': args.model, 'dataset': 'cifar10-shape (32x32x3, 10 classes)',
+                       'global_batch': ws * args.batch, 'per_gpu_batch': args.batch,
+                       'presample_pool': args.batch * args.pool_batches, 'seq_len': None,
+                       'optimizer': 'adam', 'parallelism': 'dp%d' % ws,
+                       'sampler': 'importance (loss + 0.5*EMA), with replacement'},
+            'final_train_loss': round(m['loss_sum'] / max(m['count'], 1), 4),
+        }
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

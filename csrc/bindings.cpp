@@ -122,11 +122,11 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("pool_build", [](uintptr_t shard, uintptr_t labels, uintptr_t ctrl, uintptr_t pool,
                          uintptr_t pool_label, uintptr_t pool_index, int Ns, int H, int W, int Pn,
-                         int batch, int pad, int flip, int augment, uint32_t seed,
+                         int batch, int pad, int flip, int augment, int shuffle, uint32_t seed,
                          std::vector<float> mean, std::vector<float> inv_std, uintptr_t st) {
     PoolBuildArgs a{P<const uint8_t>(shard), P<const int64_t>(labels), P<const int64_t>(ctrl),
                     P<bf16>(pool), P<int>(pool_label), P<int>(pool_index), Ns, H, W, Pn, batch,
-                    pad, flip, augment, seed, {mean[0], mean[1], mean[2]},
+                    pad, flip, augment, shuffle, seed, {mean[0], mean[1], mean[2]},
                     {inv_std[0], inv_std[1], inv_std[2]}};
     pool_build_launch(a, S(st));
     check_launch("pool_build");
@@ -189,6 +189,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_weights", [](uintptr_t p, uintptr_t segs, int nsegs, long long total, uintptr_t st) {
     pack_weights_launch(P<const float>(p), P<const OptSeg>(segs), nsegs, total, S(st));
     check_launch("pack_weights");
+  });
+  m.def("transpose_weights", [](uintptr_t segs, uintptr_t jobs, int njobs, uintptr_t st) {
+    transpose_weights_launch(P<const OptSeg>(segs), P<const int>(jobs), njobs, S(st));
+    check_launch("transpose_weights");
   });
   m.def("step_begin", [](uintptr_t ctrl, uintptr_t st) {
     step_begin_launch(P<int64_t>(ctrl), S(st));

@@ -3,20 +3,21 @@
 // The forward conv epilogue (igemm.hip) already accumulates per-(ghost-group,
 // channel) sum / sum-of-squares, so BN forward here is a single streaming pass:
 //   out = act( y*scale + shift  [+ residual | + y2*scale2 + shift2] )
-// with scale/shift derived on the fly from the sums (train) or running stats
-// (eval).  Ghost groups reproduce the reference's scoring semantics exactly: the
-// reference scores 10 separate batches of 32 in train mode (`pytorch_collab.py:95-103`),
+// with scale/shift derived from the sums (train) or running stats (eval).  Ghost
+// groups reproduce the reference's scoring semantics exactly: the reference
+// scores 10 separate batches of 32 in train mode (`pytorch_collab.py:95-103`),
 // each normalised with its own batch statistics; here the 320-sample pool is one
-// launch whose rows are split into 10 stat groups.
+// launch whose rows are split into 10 stat groups (grid.y = group).
 //
 // Backward (train batch, one group) is two passes:
 //   reduce: sum(dz), sum(dz*xhat) [and sum(dz*xhat2) for a BN'd shortcut sharing dz]
 //   apply : dy = gamma*rstd*(dz - mean(dz) - xhat*mean(dz*xhat)); writes dgamma/dbeta
 // where dz = dout * act'(out) is recomputed from the saved block output.
 //
-// Thread mapping: every thread keeps ONE 8-channel chunk for its whole grid-stride
-// loop (the stride is a multiple of C/8), so per-channel constants are computed
-// once per thread and loads/stores are 16 bytes.
+// Thread mapping: every thread owns ONE 8-channel chunk for its whole loop (the
+// row stride is a multiple of C/8), so its per-channel constants are loaded once,
+// as 2 x float4 per array, all issued back to back -- never as conditional scalar
+// loads, which hipcc serialises behind one vmcnt(0) each (a ~15 us prologue).
 #include "common.h"
 #include "kernels.h"
 
@@ -35,62 +36,74 @@ MA_DEV float act_mask(float out, int act) {
   return 1.f;
 }
 
-MA_DEV void scale_shift(const float* stats, int ld, int g, int c, float inv_cnt, float eps,
-                        const float* gamma, const float* beta, const float* rm, const float* rv,
-                        int use_running, float& sc, float& sh) {
-  float mean, var;
-  if (use_running) {
-    mean = rm[c];
-    var = rv[c];
-  } else {
-    const float s = stats[(size_t)g * 2 * ld + c], ss = stats[(size_t)g * 2 * ld + ld + c];
-    mean = s * inv_cnt;
-    var = fmaxf(ss * inv_cnt - mean * mean, 0.f);
+MA_DEV void load8(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// scale/shift for 8 channels: from batch sums (sum, sumsq) or running (mean, var).
+MA_DEV void scale_shift8(const float* mean_or_sum, const float* var_or_sq, bool running,
+                         float inv_cnt, float eps, const float* gamma, const float* beta,
+                         float (&sc)[8], float (&sh)[8]) {
+  float a[8], b[8], g[8], be[8];
+  load8(mean_or_sum, a);
+  load8(var_or_sq, b);
+  load8(gamma, g);
+  load8(beta, be);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float mean, var;
+    if (running) {
+      mean = a[k];
+      var = b[k];
+    } else {
+      mean = a[k] * inv_cnt;
+      var = fmaxf(b[k] * inv_cnt - mean * mean, 0.f);
+    }
+    sc[k] = g[k] * rsqrtf(var + eps);
+    sh[k] = be[k] - mean * sc[k];
   }
-  const float rstd = rsqrtf(var + eps);
-  sc = (gamma ? gamma[c] : 1.f) * rstd;
-  sh = (beta ? beta[c] : 0.f) - mean * sc;
 }
 
-MA_DEV void mean_rstd(const float* stats, int ld, int c, float inv_cnt, float eps, float& mean,
-                      float& rstd) {
-  const float s = stats[c], ss = stats[ld + c];
-  mean = s * inv_cnt;
-  rstd = rsqrtf(fmaxf(ss * inv_cnt - mean * mean, 0.f) + eps);
+MA_DEV void mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, float (&mean)[8],
+                       float (&rstd)[8]) {
+  float s[8], ss[8];
+  load8(stats, s);
+  load8(stats + ld, ss);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = s[k] * inv_cnt;
+    rstd[k] = rsqrtf(fmaxf(ss[k] * inv_cnt - mean[k] * mean[k], 0.f) + eps);
+  }
 }
 
-MA_DEV void chunk_range(int C8, int& stride, int& start) {
-  const int T = gridDim.x * NT;
-  stride = T - T % C8;
-  start = blockIdx.x * NT + threadIdx.x;
-}
-
+// grid.x covers the rows of ONE stat group (grid.y = group), stride multiple of C/8
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
   const int C8 = a.C >> 3;
-  int stride, i0;
-  chunk_range(C8, stride, i0);
+  const int T = gridDim.x * NT;
+  const int stride = T - T % C8;
+  const int i0 = blockIdx.x * NT + threadIdx.x;
   if (i0 >= stride) return;
-  const int c8 = i0 % C8;
-  const size_t total = (size_t)a.M * C8;
+  const int c8 = i0 % C8, c = c8 * 8;
+  const int g = blockIdx.y;
+  const int row0 = g * a.group_rows, row1 = min(a.M, row0 + a.group_rows);
+  const float inv = 1.f / (float)(row1 - row0);
+  const bool run = a.use_running != 0;
   float sc[8], sh[8], sc2[8], sh2[8];
-  int gcur = -1;
-  for (size_t i = i0; i < total; i += stride) {
-    const int row = (int)(i / C8);
-    const int g = row / a.group_rows;
-    if (g != gcur) {
-      gcur = g;
-      const int cnt = min(a.group_rows, a.M - g * a.group_rows);
-      const float inv = 1.f / (float)cnt;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        scale_shift(a.stats, a.C, g, c8 * 8 + k, inv, a.eps, a.gamma, a.beta, a.rmean, a.rvar,
-                    a.use_running, sc[k], sh[k]);
-        if (a.res_mode == 2)
-          scale_shift(a.stats2, a.C, g, c8 * 8 + k, inv, a.eps, a.gamma2, a.beta2, a.rmean2,
-                      a.rvar2, a.use_running, sc2[k], sh2[k]);
-      }
-    }
-    const size_t off = i * 8;
+  {
+    const float* s0 = run ? a.rmean + c : a.stats + (size_t)g * 2 * a.C + c;
+    const float* s1 = run ? a.rvar + c : s0 + a.C;
+    scale_shift8(s0, s1, run, inv, a.eps, a.gamma + c, a.beta + c, sc, sh);
+  }
+  if (a.res_mode == 2) {
+    const float* s0 = run ? a.rmean2 + c : a.stats2 + (size_t)g * 2 * a.C + c;
+    const float* s1 = run ? a.rvar2 + c : s0 + a.C;
+    scale_shift8(s0, s1, run, inv, a.eps, a.gamma2 + c, a.beta2 + c, sc2, sh2);
+  }
+  const int rpi = stride / C8;
+  for (int row = row0 + i0 / C8; row < row1; row += rpi) {
+    const size_t off = (size_t)row * a.C + c;
     const bf16x8 y = *(const bf16x8*)(a.y + off);
     bf16x8 r;
     if (a.res_mode) r = *(const bf16x8*)(a.res + off);
@@ -109,108 +122,124 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   __shared__ float red[3 * 2048];
   const int C8 = a.C >> 3;
+  const bool two = a.y2 != nullptr;
   for (int i = threadIdx.x; i < 3 * a.C; i += NT) red[i] = 0.f;
   __syncthreads();
-  int stride, i0;
-  chunk_range(C8, stride, i0);
-  const int c8 = i0 % C8;
+  const int T = gridDim.x * NT;
+  const int stride = T - T % C8;
+  const int i0 = blockIdx.x * NT + threadIdx.x;
+  const int c8 = i0 % C8, c = c8 * 8;
   const float inv = 1.f / (float)a.M;
   float mean[8], rstd[8], mean2[8], rstd2[8];
   float sdz[8], sx[8], sx2[8];
+  mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
+  if (two) mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sdz[k] = sx[k] = sx2[k] = 0.f;
-    const int c = c8 * 8 + k;
-    mean_rstd(a.stats, a.C, c, inv, a.eps, mean[k], rstd[k]);
-    if (a.y2) mean_rstd(a.stats2, a.C, c, inv, a.eps, mean2[k], rstd2[k]);
-  }
+  for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = sx2[k] = 0.f;
   if (i0 < stride) {
-    const size_t total = (size_t)a.M * C8;
-    for (size_t i = i0; i < total; i += stride) {
-      const size_t off = i * 8;
-      const bf16x8 d = *(const bf16x8*)(a.dout + off);
-      const bf16x8 o = *(const bf16x8*)(a.out + off);
-      const bf16x8 y = *(const bf16x8*)(a.y + off);
-      bf16x8 y2;
-      if (a.y2) y2 = *(const bf16x8*)(a.y2 + off);
+    const int rpi = stride / C8;
+    // 4 rows per trip: all 12-16 loads of a trip are issued before the first use, so
+    // a thread exposes one memory latency per 4 rows instead of one per row
+    constexpr int U = 4;
+    for (int row = i0 / C8; row < a.M; row += U * rpi) {
+      bf16x8 d[U], o[U], y[U], y2[U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float dz = bf2f(d[k]) * act_mask(bf2f(o[k]), a.act);
-        sdz[k] += dz;
-        sx[k] += dz * (bf2f(y[k]) - mean[k]) * rstd[k];
-        if (a.y2) sx2[k] += dz * (bf2f(y2[k]) - mean2[k]) * rstd2[k];
+      for (int u = 0; u < U; ++u) {
+        const int r = min(row + u * rpi, a.M - 1);
+        const size_t off = (size_t)r * a.C + c;
+        d[u] = *(const bf16x8*)(a.dout + off);
+        o[u] = *(const bf16x8*)(a.out + off);
+        y[u] = *(const bf16x8*)(a.y + off);
+        if (two) y2[u] = *(const bf16x8*)(a.y2 + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (row + u * rpi >= a.M) break;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float dz = bf2f(d[u][k]) * act_mask(bf2f(o[u][k]), a.act);
+          sdz[k] += dz;
+          sx[k] += dz * (bf2f(y[u][k]) - mean[k]) * rstd[k];
+          if (two) sx2[k] += dz * (bf2f(y2[u][k]) - mean2[k]) * rstd2[k];
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c8 * 8 + k;
-      atomicAdd(&red[c], sdz[k]);
-      atomicAdd(&red[a.C + c], sx[k]);
-      if (a.y2) atomicAdd(&red[2 * a.C + c], sx2[k]);
+      atomicAdd(&red[c + k], sdz[k]);
+      atomicAdd(&red[a.C + c + k], sx[k]);
+      if (two) atomicAdd(&red[2 * a.C + c + k], sx2[k]);
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < a.C; c += NT) {
-    atomicAdd(&a.sums[c], red[c]);
-    atomicAdd(&a.sums[a.C + c], red[a.C + c]);
-    if (a.y2) atomicAdd(&a.sums[2 * a.C + c], red[2 * a.C + c]);
+  for (int j = threadIdx.x; j < a.C; j += NT) {
+    atomicAdd(&a.sums[j], red[j]);
+    atomicAdd(&a.sums[a.C + j], red[a.C + j]);
+    if (two) atomicAdd(&a.sums[2 * a.C + j], red[2 * a.C + j]);
   }
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const int C8 = a.C >> 3;
+  const bool two = a.y2 != nullptr;
   const float inv = 1.f / (float)a.M;
   if (blockIdx.x == 0) {  // parameter gradients
-    for (int c = threadIdx.x; c < a.C; c += NT) {
-      if (a.dgamma) a.dgamma[c] = a.sums[a.C + c];
-      if (a.dbeta) a.dbeta[c] = a.sums[c];
-      if (a.y2) {
-        if (a.dgamma2) a.dgamma2[c] = a.sums[2 * a.C + c];
-        if (a.dbeta2) a.dbeta2[c] = a.sums[c];
+    for (int j = threadIdx.x; j < a.C; j += NT) {
+      if (a.dgamma) a.dgamma[j] = a.sums[a.C + j];
+      if (a.dbeta) a.dbeta[j] = a.sums[j];
+      if (two) {
+        if (a.dgamma2) a.dgamma2[j] = a.sums[2 * a.C + j];
+        if (a.dbeta2) a.dbeta2[j] = a.sums[j];
       }
     }
   }
-  int stride, i0;
-  chunk_range(C8, stride, i0);
+  const int T = gridDim.x * NT;
+  const int stride = T - T % C8;
+  const int i0 = blockIdx.x * NT + threadIdx.x;
   if (i0 >= stride) return;
-  const int c8 = i0 % C8;
-  float k1[8], k2[8], mean[8], rstd[8], q1[8], q2[8], mean2[8], rstd2[8];
+  const int c8 = i0 % C8, c = c8 * 8;
+  float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
+  mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
+  load8(a.gamma + c, gm);
+  load8(a.sums + c, sdz);
+  load8(a.sums + a.C + c, sx);
+  if (two) {
+    mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
+    load8(a.gamma2 + c, gm2);
+    load8(a.sums + 2 * a.C + c, sx2);
+  }
+  float k1[8], k2[8], q1[8], k3[8], q2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = c8 * 8 + k;
-    mean_rstd(a.stats, a.C, c, inv, a.eps, mean[k], rstd[k]);
-    const float gm = a.gamma ? a.gamma[c] : 1.f;
-    k1[k] = gm * rstd[k];                  // gamma*rstd
-    k2[k] = a.sums[c] * inv;               // mean(dz)
-    q1[k] = a.sums[a.C + c] * inv;         // mean(dz*xhat)
-    if (a.y2) {
-      mean_rstd(a.stats2, a.C, c, inv, a.eps, mean2[k], rstd2[k]);
-      q2[k] = a.sums[2 * a.C + c] * inv;
+    k1[k] = gm[k] * rstd[k];      // gamma*rstd
+    k2[k] = sdz[k] * inv;         // mean(dz)
+    q1[k] = sx[k] * inv;          // mean(dz*xhat)
+    if (two) {
+      k3[k] = gm2[k] * rstd2[k];
+      q2[k] = sx2[k] * inv;
     }
   }
-  const size_t total = (size_t)a.M * C8;
-  for (size_t i = i0; i < total; i += stride) {
-    const size_t off = i * 8;
+  const int rpi = stride / C8;
+  for (int row = i0 / C8; row < a.M; row += rpi) {
+    const size_t off = (size_t)row * a.C + c;
     const bf16x8 d = *(const bf16x8*)(a.dout + off);
     const bf16x8 o = *(const bf16x8*)(a.out + off);
     const bf16x8 y = *(const bf16x8*)(a.y + off);
     bf16x8 y2, dy, dy2, dzo;
-    if (a.y2) y2 = *(const bf16x8*)(a.y2 + off);
+    if (two) y2 = *(const bf16x8*)(a.y2 + off);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float dz = bf2f(d[k]) * act_mask(bf2f(o[k]), a.act);
       const float xh = (bf2f(y[k]) - mean[k]) * rstd[k];
       dy[k] = f2bf(k1[k] * (dz - k2[k] - xh * q1[k]));
-      if (a.y2) {
-        const int c = c8 * 8 + k;
-        const float g2 = a.gamma2 ? a.gamma2[c] : 1.f;
+      if (two) {
         const float xh2 = (bf2f(y2[k]) - mean2[k]) * rstd2[k];
-        dy2[k] = f2bf(g2 * rstd2[k] * (dz - k2[k] - xh2 * q2[k]));
+        dy2[k] = f2bf(k3[k] * (dz - k2[k] - xh2 * q2[k]));
       }
       dzo[k] = f2bf(dz);
     }
     *(bf16x8*)(a.dy + off) = dy;
-    if (a.y2) *(bf16x8*)(a.dy2 + off) = dy2;
+    if (two) *(bf16x8*)(a.dy2 + off) = dy2;
     if (a.dz) *(bf16x8*)(a.dz + off) = dzo;
   }
 }
@@ -254,14 +283,16 @@ int grid_for(size_t chunks, int C8, int per_thread, int cap) {
 }  // namespace
 
 void bn_apply_launch(const BnApplyArgs& a, hipStream_t st) {
-  const size_t chunks = (size_t)a.M * (a.C / 8);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0, st, a);
+  const int G = (a.M + a.group_rows - 1) / a.group_rows;
+  const size_t chunks = (size_t)a.group_rows * (a.C / 8);
+  const int gx = grid_for(chunks, a.C / 8, 4, (2048 + G - 1) / G);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(gx, G), dim3(NT), 0, st, a);
 }
 
 void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
+  // a.sums must be zero on entry (the engine zeroes one arena per step)
   const size_t chunks = (size_t)a.M * (a.C / 8);
-  hipMemsetAsync(a.sums, 0, sizeof(float) * 3 * a.C, st);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 16, 128)), dim3(NT), 0,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 8, 256)), dim3(NT), 0,
                      st, a);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0,
                      st, a);

@@ -26,6 +26,7 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
   const float invhw = 1.f / (float)a.HW;
   for (int c = tid; c < a.C; c += NT) {
     float s = 0.f;
+#pragma unroll 8
     for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
     s *= invhw;
     pooled[c] = s;
@@ -35,6 +36,7 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
   for (int k = wv; k < a.classes; k += NT / 64) {
     const float* wr = a.w + (size_t)k * a.C;
     float d = 0.f;
+#pragma unroll 8
     for (int c = lane; c < a.C; c += 64) d += wr[c] * pooled[c];
     d = wave_sum(d);
     if (lane == 0) logit[k] = d + (a.b ? a.b[k] : 0.f);
@@ -90,30 +92,37 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
   }
 }
 
-// grid.x over channel blocks; each thread owns one channel c.
+// grid = (channel blocks, B + classes): block row y < B writes sample y's activation
+// gradient (d pooled / HW broadcast over the spatial positions); row B + k reduces
+// dW[k][:] (and db[k]) over the batch.  Every thread's loop is short and unrolled so
+// its loads are in flight together.
 __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadBwdArgs a) {
   const int c = blockIdx.x * NT + threadIdx.x;
-  if (blockIdx.x == 0) {
-    for (int k = threadIdx.x; k < a.classes; k += NT) {
+  const int b = blockIdx.y;
+  if (b >= a.B) {
+    const int k = b - a.B;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
       float s = 0.f;
-      for (int b = 0; b < a.B; ++b) s += a.dlogits[(size_t)b * a.classes + k];
-      a.db[k] = s;
+      for (int i = threadIdx.x; i < a.B; i += 64) s += a.dlogits[(size_t)i * a.classes + k];
+      s = wave_sum(s);
+      if (threadIdx.x == 0) a.db[k] = s;
     }
+    if (c >= a.C) return;
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < a.B; ++i)
+      s += a.dlogits[(size_t)i * a.classes + k] * a.pooled[(size_t)i * a.C + c];
+    a.dw[(size_t)k * a.C + c] = s;
+    return;
   }
   if (c >= a.C) return;
-  for (int k = 0; k < a.classes; ++k) {
-    float s = 0.f;
-    for (int b = 0; b < a.B; ++b) s += a.dlogits[(size_t)b * a.classes + k] * a.pooled[(size_t)b * a.C + c];
-    a.dw[(size_t)k * a.C + c] = s;
-  }
-  const float invhw = 1.f / (float)a.HW;
-  for (int b = 0; b < a.B; ++b) {
-    float s = 0.f;
-    for (int k = 0; k < a.classes; ++k) s += a.dlogits[(size_t)b * a.classes + k] * a.w[(size_t)k * a.C + c];
-    const bf16 v = f2bf(s * invhw);
-    bf16* dst = a.dact + (size_t)b * a.HW * a.C + c;
-    for (int hw = 0; hw < a.HW; ++hw) dst[(size_t)hw * a.C] = v;
-  }
+  float s = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < a.classes; ++k)
+    s += a.dlogits[(size_t)b * a.classes + k] * a.w[(size_t)k * a.C + c];
+  const bf16 v = f2bf(s / (float)a.HW);
+  bf16* dst = a.dact + (size_t)b * a.HW * a.C + c;
+  for (int hw = 0; hw < a.HW; ++hw) dst[(size_t)hw * a.C] = v;
 }
 }  // namespace
 
@@ -123,5 +132,6 @@ void head_fwd_launch(const HeadArgs& a, hipStream_t st) {
 }
 
 void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + NT - 1) / NT), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + NT - 1) / NT, a.B + a.classes), dim3(NT), 0, st,
+                     a);
 }

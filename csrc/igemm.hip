@@ -62,12 +62,24 @@ MA_DEV void epilogue_bf16(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiP
   if (stats) {
     for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
   }
+  // bias loads hoisted and issued together (a conditional load per column would be
+  // serialised behind its own vmcnt(0))
+  float biasv[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) biasv[tn] = 0.f;
+  if (e.bias) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int col = n0 + wn * (BN / 2) + tn * 16 + (lane & 15);
+      biasv[tn] = e.bias[col < N ? col : N - 1];
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int cl = wn * (BN / 2) + tn * 16 + (lane & 15);
     const int col = n0 + cl;
-    const float bias = (e.bias && col < N) ? e.bias[col] : 0.f;
+    const float bias = biasv[tn];
     float s = 0.f, ss = 0.f;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -169,11 +181,34 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
   }
 
   u32x4 ra[AR], rb[BR];
+  // k-chunk -> (r, s, c8).  When C/8 is a multiple of 8 a whole 64-deep stage lies in one
+  // filter tap, so (r, s, c8 base) advance incrementally without integer division.
+  const bool fastk = (C8 & 7) == 0;
+  int tr = 0, ts = 0, tc = 0;
+  if (fastk) {
+    const int k0c = kt0 * 8;
+    const int rs = k0c / C8;
+    tc = k0c - rs * C8;
+    tr = rs / g.S;
+    ts = rs - tr * g.S;
+  }
   auto load_stage = [&](int kt) {
     const int kc = kt * 8 + cc;
     const bool kval = kc < g.Kc;
     int r = 0, s = 0, c8 = 0;
-    if (kval) {
+    if (fastk) {
+      r = tr;
+      s = ts;
+      c8 = tc + cc;
+      tc += 8;  // advance the stage cursor for the next call
+      if (tc == C8) {
+        tc = 0;
+        if (++ts == g.S) {
+          ts = 0;
+          ++tr;
+        }
+      }
+    } else if (kval) {
       const int rs = kc / C8;
       c8 = kc - rs * C8;
       r = rs / g.S;

@@ -29,7 +29,8 @@ __global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
   const uint32_t epoch = (uint32_t)(gb / nb);
   const int bi = (int)(gb % nb);
   const uint32_t pos = (uint32_t)(bi * a.batch + t);
-  const uint32_t src = permute_index(pos, (uint32_t)a.Ns, a.seed, epoch);
+  const uint32_t src = a.shuffle ? permute_index(pos, (uint32_t)a.Ns, a.seed, epoch)
+                                 : (uint32_t)((gb * a.batch + t) % a.Ns);
   int dy = a.pad, dx = a.pad, flip = 0;
   if (a.augment) {
     const u32x4 r = philox4x32(u32x4{(uint32_t)gb, (uint32_t)(gb >> 32), (uint32_t)t, 0x5eedu},

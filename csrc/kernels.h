@@ -99,7 +99,7 @@ struct PoolBuildArgs {
   bf16* pool;                    // [P][H][W][8] bf16 normalised, channels 3..7 zero
   int* pool_label;               // [P]
   int* pool_index;               // [P] shard-local index (the dataset index the reference returns)
-  int Ns, H, W, P, batch, pad, flip, augment;
+  int Ns, H, W, P, batch, pad, flip, augment, shuffle;
   uint32_t seed;
   float mean[3], inv_std[3];
 };
@@ -161,6 +161,8 @@ struct OptArgs {
 };
 void optimizer_launch(const OptArgs& a, hipStream_t st);
 void step_begin_launch(int64_t* ctrl, hipStream_t st);
+// jobs: [njobs][4] = (segment index, r*S+s, k0, c0) -> one 64x64 tile each
+void transpose_weights_launch(const OptSeg* segs, const int* jobs, int njobs, hipStream_t st);
 void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long long total,
                          hipStream_t st);
 

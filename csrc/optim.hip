@@ -32,15 +32,37 @@ MA_DEV int find_seg(const OptSeg* s, int n, long long e) {
   return lo;
 }
 
+// bf16 [K][R][S][Cpad] forward copy.  The [C][R][S][K] dgrad copy is NOT written
+// here (a per-element scatter with stride K would turn every store into a partial
+// cache-line update); transpose_weights_kernel produces it tile-by-tile through LDS.
 MA_DEV void write_copies(const OptSeg& sg, long long local, float v) {
   if (sg.kind != 1 || local >= sg.numel) return;
   const int rsc = sg.R * sg.S * sg.C;
   const int k = (int)(local / rsc);
   const int rem = (int)(local - (long long)k * rsc);
   const int rs = rem / sg.C, c = rem - rs * sg.C;
-  const bf16 b = f2bf(v);
-  sg.w_krsc[((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c] = b;
-  if (sg.w_crsk) sg.w_crsk[((size_t)c * sg.R * sg.S + rs) * sg.K + k] = b;
+  sg.w_krsc[((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c] = f2bf(v);
+}
+
+// One 64(k) x 64(c) tile of one (segment, r*S+s) per workgroup: coalesced 2-byte reads
+// along c from the KRSC copy, LDS transpose, coalesced writes along k to CRSK.
+__global__ __launch_bounds__(256) void transpose_weights_kernel(const OptSeg* segs,
+                                                                const int* jobs) {
+  __shared__ bf16 tile[64][65];
+  const int* j = jobs + blockIdx.x * 4;
+  const OptSeg sg = segs[j[0]];
+  const int rs = j[1], k0 = j[2], c0 = j[3];
+  const int RS = sg.R * sg.S;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    tile[r][tx] = (k < sg.K && c < sg.C) ? sg.w_krsc[((size_t)k * RS + rs) * sg.Cpad + c] : f2bf(0.f);
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < sg.C && k < sg.K) sg.w_crsk[((size_t)c * RS + rs) * sg.K + k] = tile[tx][r];
+  }
 }
 
 __global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
@@ -85,8 +107,20 @@ __global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
   *(float4*)(a.m + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
   if (a.zero_grad) *(float4*)(a.g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
   if (sg.kind == 1) {
+    const long long local = e - sg.off;
+    if ((sg.C & 3) == 0 && local + 3 < sg.numel) {  // 4 consecutive channels: one 8-B store
+      const int rsc = sg.R * sg.S * sg.C;
+      const int k = (int)(local / rsc);
+      const int rem = (int)(local - (long long)k * rsc);
+      const int rs = rem / sg.C, c = rem - rs * sg.C;
+      bf16x4 b;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) write_copies(sg, e + k - sg.off, pv[k]);
+      for (int q = 0; q < 4; ++q) b[q] = f2bf(pv[q]);
+      *(bf16x4*)(sg.w_krsc + ((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c) = b;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) write_copies(sg, local + q, pv[q]);
+    }
   }
 }
 
@@ -110,6 +144,11 @@ void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long lon
                          hipStream_t st) {
   hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, p, segs,
                      nsegs, total);
+}
+
+void transpose_weights_launch(const OptSeg* segs, const int* jobs, int njobs, hipStream_t st) {
+  if (njobs > 0)
+    hipLaunchKernelGGL(transpose_weights_kernel, dim3(njobs), dim3(256), 0, st, segs, jobs);
 }
 
 void step_begin_launch(int64_t* ctrl, hipStream_t st) {

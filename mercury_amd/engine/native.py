@@ -1,0 +1,811 @@
+"""The MI355X-native training engine: fused HIP kernels + HIP graphs + RCCL.
+
+One importance-sampled step (reference `pytorch_collab.py:127-164`) runs as:
+
+    S1 (score stream)  : pool_build -> forward(B=320, ghost BN) -> CE scores
+                         -> is_sample (EMA replay, p, draws, weights)
+    S0 (main stream)   : forward(B=32) -> IS-weighted CE -> backward, segmented
+                         at gradient-bucket boundaries; after each segment the
+                         bucket's RCCL all-reduce (AVG) is issued on the NCCL
+                         stream while later segments and S1 keep computing
+    S0 after join      : BN running stats (train batch, then the 10 scoring
+                         groups, in reference order) -> fused Adam (+bf16
+                         weight packing, gradient zeroing) -> gather the drawn
+                         samples into the next training batch
+
+Scoring uses the same (pre-update) weights as training, exactly like the
+reference, so it overlaps the whole train fwd/bwd and the all-reduce instead
+of serialising after them (the reference's dead overlap code,
+`pytorch_collab.py:154-156`, made real without the race).  Each stream's work
+is captured once into HIP graphs (``torch.cuda.CUDAGraph``) and replayed, so
+a step costs a handful of host calls.  All buffers are allocated up front.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
+from ..parallel.buckets import default_bucket_bytes
+from ..trainer import Trainer
+from ..utils.meters import Accuracy, Average, EMAverage
+from .lower import lower, supports  # noqa: F401
+
+BN_EPS = 1e-5
+
+
+class _Mode(object):
+    """Per-batch-size buffers: activations, stats, plans, slabs."""
+
+    def __init__(self, name, N, group_imgs, train):
+        self.name = name
+        self.N = N
+        self.group_imgs = group_imgs   # images per BN stat group (0 = whole batch)
+        self.train = train
+        self.spec = {}
+        self.plan = {}
+        self.buf = {}
+        self.stats = {}
+        self.slab = None
+        self.G = 1 if not group_imgs else N // group_imgs
+
+
+class NativeEngine(object):
+
+    def __init__(self, net, device, batch_size=32, pool_batches=10, num_classes=None,
+                 image_hw=(32, 32), optimizer='adam', lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0, momentum=0.9, seed=0, alpha=0.5, ema_alpha=0.9,
+                 importance=True, world_size=1, bucket_bytes=None, use_graphs=True):
+        ops.lib()
+        self.net = net
+        self.device = torch.device(device)
+        self.lw = lower(net)
+        self.B = batch_size
+        self.P = batch_size * pool_batches
+        self.pool_batches = pool_batches
+        self.classes = self.lw.num_classes
+        self.H, self.W = image_hw
+        self.seed = seed
+        self.alpha, self.ema_alpha, self.importance = alpha, ema_alpha, importance
+        self.world_size = world_size
+        self.use_graphs = use_graphs
+        self._avg_op = None
+        if world_size > 1:
+            self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == 'nccl'
+                            else dist.ReduceOp.SUM)
+        self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
+        self.units = []
+        for blk in self.lw.blocks:
+            self.units += blk.units + ([blk.shortcut] if blk.shortcut else [])
+        for u in self.units:
+            if u.conv.bias is not None:
+                raise NotImplementedError('conv bias not supported by the native engine')
+        self._make_params(optimizer, lr, betas, eps, weight_decay, momentum)
+        self.modes = {}
+        self.ctrl = torch.zeros(8, dtype=torch.int64, device=self.device)
+        self.ema = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.meters = torch.zeros(8, dtype=torch.float32, device=self.device)
+        self.eval_meters = torch.zeros(8, dtype=torch.float32, device=self.device)
+        self.s_score = torch.cuda.Stream(self.device)
+        # Optional side stream for weight gradients.  Off by default: measured on MI355X
+        # (bench/host_overhead.py) a fork/join per conv inside a captured graph is spread
+        # over several hardware queues and each cross-queue edge costs ~15 us, which made
+        # the train graph 1.8 ms vs 1.5 ms single-stream.
+        self.s_wgrad = None
+        self.graphs = None
+        self.shard = None
+        self.scoring = True
+
+    # ------------------------------------------------------------------ parameters
+    def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
+        segs = []
+        self.w_krsc, self.w_crsk = {}, {}
+        for u in self.units:
+            if u.depthwise:
+                continue
+            K, C, R = u.K, u.C, u.R
+            self.w_krsc[u.name] = torch.zeros(K, R, R, cpad8(C), dtype=torch.bfloat16,
+                                              device=self.device)
+            if u.need_dgrad:
+                self.w_crsk[u.name] = torch.zeros(C, R, R, K, dtype=torch.bfloat16,
+                                                  device=self.device)
+        unit_by_w = {id(u.w_seg): u for u in self.units}
+        for s in self.lw.segs:
+            d = dict(off=s.off, numel=s.numel, kind=0)
+            u = unit_by_w.get(id(s))
+            if u is not None and not u.depthwise:
+                d.update(kind=1, K=u.K, R=u.R, S=u.R, C=u.C, Cpad=cpad8(u.C),
+                         w_krsc=self.w_krsc[u.name], w_crsk=self.w_crsk.get(u.name))
+            segs.append(d)
+        self.opt = ops.FlatOptimizer(segs, self.lw.total, self.device, optimizer, lr, betas, eps,
+                                     wd, momentum)
+        self.load_from_module()
+
+    def _pview(self, seg, grad=False):
+        buf = self.opt.g if grad else self.opt.p
+        return buf[seg.off:seg.off + seg.numel]
+
+    @torch.no_grad()
+    def load_from_module(self):
+        """Module parameters (torch layout) -> flat master (engine layout) + bf16 copies."""
+        for s in self.lw.segs:
+            p = s.param.detach().to(self.device, torch.float32)
+            if s.kind == 'conv':
+                p = p.permute(0, 2, 3, 1)
+            self.opt.p[s.off:s.off + s.numel].copy_(p.reshape(-1))
+        self.opt.pack_weights()
+
+    @torch.no_grad()
+    def sync_to_module(self):
+        """Flat master -> module parameters (torch layout).  BN buffers are shared already."""
+        for s in self.lw.segs:
+            v = self.opt.p[s.off:s.off + s.numel]
+            if s.kind == 'conv':
+                k, c, r, ss = s.param.shape
+                v = v.view(k, r, ss, c).permute(0, 3, 1, 2)
+            s.param.data.copy_(v.reshape(s.param.shape))
+
+    def _to_torch_layout(self, seg, flat):
+        v = flat[seg.off:seg.off + seg.numel]
+        if seg.kind == 'conv':
+            k, c, r, s = seg.param.shape
+            return v.view(k, r, s, c).permute(0, 3, 1, 2).contiguous()
+        return v.view(seg.param.shape).clone()
+
+    def _from_torch_layout(self, seg, flat, t):
+        t = t.to(self.device, torch.float32)
+        if seg.kind == 'conv':
+            t = t.permute(0, 2, 3, 1)
+        flat[seg.off:seg.off + seg.numel].copy_(t.reshape(-1))
+
+    # ------------------------------------------------------------------ buffers
+    def mode(self, name, N=None, group_imgs=0, train=False):
+        if name in self.modes:
+            return self.modes[name]
+        m = _Mode(name, N, group_imgs, train)
+        dev = self.device
+        H, W = self.H, self.W
+        C = cpad8(self.lw.in_channels)
+        slab = 0
+        nstats = 0
+        nsums = 0
+        bf = torch.bfloat16
+
+        def act(M, K):
+            return torch.empty(M * K, dtype=bf, device=dev)
+
+        for bi, blk in enumerate(self.lw.blocks):
+            h, w = H, W
+            main_hw = None
+            for u in blk.units + ([blk.shortcut] if blk.shortcut else []):
+                if u is blk.shortcut:
+                    main_hw = (h, w)
+                    h, w = H, W          # the shortcut reads the block input
+                sp = ConvSpec(N, h, w, u.C, u.K, u.R, u.R, u.stride, u.pad)
+                if group_imgs:
+                    sp.group_rows = group_imgs * sp.P * sp.Q
+                m.spec[u.name] = sp
+                if not u.depthwise:
+                    m.plan[u.name, 'fwd'] = p = fwd_plan(sp)
+                    slab = max(slab, slab_bytes(sp.M, sp.K, *p))
+                    if train:
+                        if u.need_dgrad:
+                            m.plan[u.name, 'dgrad'] = p = dgrad_plan(sp)
+                            slab = max(slab, slab_bytes(N * h * w, sp.Cp, *p))
+                        m.plan[u.name, 'wgrad'] = wgrad_plan(sp)
+                m.buf[u.name, 'y'] = act(sp.M, u.K)
+                m.stats[u.name] = nstats
+                nstats += m.G * 2 * u.K
+                if u is not blk.units[-1] and u is not blk.shortcut:
+                    m.buf[u.name, 'a'] = act(sp.M, u.K)
+                if train:
+                    m.buf[u.name, 'dy'] = act(sp.M, u.K)
+                    m.buf[u.name, 'sums'] = nsums
+                    nsums += 3 * u.K
+                    if u is not blk.units[-1] and u is not blk.shortcut:
+                        m.buf[u.name, 'da'] = act(sp.M, u.K)
+                if u is not blk.shortcut:
+                    h, w = sp.P, sp.Q
+            if main_hw is not None:
+                h, w = main_hw
+            last = blk.units[-1]
+            K = last.K
+            m.buf[bi, 'out'] = act(N * h * w, K)
+            if train:
+                m.buf[bi, 'dout'] = act(N * h * w, K)
+            if blk.pool is not None:
+                k, st, pd = blk.pool
+                P_ = (h + 2 * pd - k) // st + 1
+                Q_ = (w + 2 * pd - k) // st + 1
+                m.buf[bi, 'pre'] = m.buf[bi, 'out']
+                m.buf[bi, 'out'] = act(N * P_ * Q_, K)
+                m.buf[bi, 'pool_geom'] = (N, h, w, K, P_, Q_, k, st, pd)
+                if train:
+                    m.buf[bi, 'argmax'] = torch.empty(N * P_ * Q_ * K, dtype=torch.int32,
+                                                      device=dev)
+                    m.buf[bi, 'dpre'] = m.buf[bi, 'dout']
+                    m.buf[bi, 'dout'] = act(N * P_ * Q_, K)
+                h, w = P_, Q_
+            m.buf[bi, 'hw'] = (h, w)
+            H, W, C = h, w, K
+        m.stats_arena = torch.zeros(max(nstats, 1), device=dev)
+        m.sums_arena = torch.zeros(max(nsums, 1), device=dev)
+        for key, off in list(m.stats.items()):
+            u = next(x for x in self.units if x.name == key)
+            m.stats[key] = m.stats_arena[off:off + m.G * 2 * u.K]
+            if train:
+                so = m.buf[u.name, 'sums']
+                m.buf[u.name, 'sums'] = m.sums_arena[so:so + 3 * u.K]
+        m.final_hw = H * W
+        m.final_C = C
+        m.pooled = torch.zeros(N, C, device=dev)
+        m.losses = torch.zeros(N, device=dev)
+        if train:
+            m.dlogits = torch.zeros(N, self.classes, device=dev)
+        m.slab = torch.empty(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
+        m.input = torch.zeros(N, self.H, self.W, cpad8(self.lw.in_channels), dtype=bf, device=dev)
+        m.label = torch.zeros(N, dtype=torch.int32, device=dev)
+        m.index = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.modes[name] = m
+        return m
+
+    # ------------------------------------------------------------------ layer execution
+    def _gamma(self, u, grad=False):
+        return self._pview(u.g_seg, grad)
+
+    def _beta(self, u, grad=False):
+        return self._pview(u.beta_seg, grad)
+
+    def _conv_fwd(self, m, u, x, y, stats):
+        sp = m.spec[u.name]
+        if u.depthwise:
+            ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
+                           sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M)
+        else:
+            ops.conv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, slab=m.slab,
+                         plan=m.plan[u.name, 'fwd'])
+
+    def _bn_apply(self, m, u, y, out, act, res=None, res_unit=None):
+        sp = m.spec[u.name]
+        kw = {}
+        if m.train or m.group_imgs:
+            stats, running = m.stats[u.name], None
+        else:
+            stats, running = None, (u.bn.running_mean, u.bn.running_var)
+        if res_unit is not None:
+            r2 = None if stats is not None else (res_unit.bn.running_mean,
+                                                 res_unit.bn.running_var)
+            kw['res_bn'] = (m.stats[res_unit.name] if stats is not None else None,
+                            self._gamma(res_unit), self._beta(res_unit), r2)
+        ops.bn_apply(y, stats, self._gamma(u), self._beta(u), out, sp.M, u.K,
+                     group_rows=sp.group_rows or sp.M, act=act, eps=BN_EPS, running=running,
+                     res=res, **kw)
+
+    def forward(self, m, x=None):
+        """Forward through all blocks; returns the final activation buffer."""
+        x = m.input if x is None else x
+        stats_on = m.train or m.group_imgs
+        for bi, blk in enumerate(self.lw.blocks):
+            inp = x
+            nu = len(blk.units)
+            for i, u in enumerate(blk.units):
+                y = m.buf[u.name, 'y']
+                self._conv_fwd(m, u, inp, y, m.stats[u.name] if stats_on else None)
+                if i < nu - 1:
+                    a = m.buf[u.name, 'a']
+                    self._bn_apply(m, u, y, a, u.act)
+                    inp = a
+                else:
+                    out = m.buf[bi, 'pre'] if blk.pool else m.buf[bi, 'out']
+                    res, ru = None, None
+                    if blk.shortcut is not None:
+                        sc = blk.shortcut
+                        self._conv_fwd(m, sc, x, m.buf[sc.name, 'y'],
+                                       m.stats[sc.name] if stats_on else None)
+                        res, ru = m.buf[sc.name, 'y'], sc
+                    elif blk.identity:
+                        res = x
+                    self._bn_apply(m, u, y, out, blk.final_act, res=res, res_unit=ru)
+            if blk.pool:
+                N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
+                ops.pool2d_fwd(m.buf[bi, 'pre'], m.buf[bi, 'out'], N, h, w, K, P_, Q_, k, st, pd,
+                               True, m.buf.get((bi, 'argmax')))
+            x = m.buf[bi, 'out']
+        return x
+
+    def head(self, m, x, mode, isw=None, meters=None):
+        ops.head_fwd(x, self._pview(self.lw.fc_w), self._pview(self.lw.fc_b), m.label, m.N,
+                     m.final_hw, m.final_C, self.classes, mode, pooled=m.pooled,
+                     dlogits=getattr(m, 'dlogits', None) if mode == 'train' else None,
+                     losses=m.losses, isw=isw, meters=meters)
+
+    def _wgrad(self, m, u, dy, x):
+        sp = m.spec[u.name]
+        gw = self._pview(u.w_seg, grad=True)
+        if u.depthwise:
+            ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad)
+        else:
+            ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
+
+    def _conv_bwd(self, m, u, dy, x, dx, accumulate):
+        """Weight gradient on the side stream (off the critical path), data gradient here."""
+        sp = m.spec[u.name]
+        ws = self.s_wgrad
+        if ws is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            ws.wait_event(ev)
+            with torch.cuda.stream(ws):
+                self._wgrad(m, u, dy, x)
+        else:
+            self._wgrad(m, u, dy, x)
+        if u.depthwise:
+            if dx is not None:
+                assert not accumulate
+                ops.dwconv_dgrad(dy, self._pview(u.w_seg), dx, sp.N, sp.H, sp.W, sp.C, sp.P,
+                                 sp.Q, sp.stride, sp.pad)
+            return
+        if dx is not None:
+            ops.conv_dgrad(dy, self.w_crsk[u.name], dx, sp, slab=m.slab,
+                           plan=m.plan[u.name, 'dgrad'], accumulate=accumulate)
+
+    def _bn_bwd(self, m, u, dout, out, act, dy, unit2=None, dy2=None, dz=None):
+        sp = m.spec[u.name]
+        kw = {}
+        if unit2 is not None:
+            kw = dict(y2=m.buf[unit2.name, 'y'], stats2=m.stats[unit2.name],
+                      gamma2=self._gamma(unit2), dy2=dy2, dgamma2=self._gamma(unit2, True),
+                      dbeta2=self._beta(unit2, True))
+        ops.bn_bwd(dout, out, m.buf[u.name, 'y'], m.stats[u.name], self._gamma(u),
+                   m.buf[u.name, 'sums'], dy, sp.M, u.K, act=act, eps=BN_EPS, dz=dz,
+                   dgamma=self._gamma(u, True), dbeta=self._beta(u, True), zero_sums=False,
+                   **kw)
+
+    def backward_block(self, m, bi):
+        blk = self.lw.blocks[bi]
+        x = m.buf[bi - 1, 'out'] if bi > 0 else m.input
+        dx = m.buf[bi - 1, 'dout'] if (bi > 0 and blk.need_dx) else None
+        dout = m.buf[bi, 'dout']
+        out = m.buf[bi, 'out']
+        if blk.pool:
+            N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
+            ops.maxpool2d_bwd(dout, m.buf[bi, 'argmax'], m.buf[bi, 'dpre'], N, h, w, K, P_, Q_,
+                              k, st, pd)
+            dout, out = m.buf[bi, 'dpre'], m.buf[bi, 'pre']
+        units = blk.units
+        last = units[-1]
+        sc = blk.shortcut
+        dy_last = m.buf[last.name, 'dy']
+        dz = dx if (blk.identity and dx is not None) else None
+        self._bn_bwd(m, last, dout, out, blk.final_act, dy_last, unit2=sc,
+                     dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz)
+        if sc is not None:
+            self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
+        d = dy_last
+        for i in range(len(units) - 1, -1, -1):
+            u = units[i]
+            inp = x if i == 0 else m.buf[units[i - 1].name, 'a']
+            if i > 0:
+                prev = units[i - 1]
+                da = m.buf[prev.name, 'da']
+                self._conv_bwd(m, u, d, inp, da, accumulate=False)
+                dyp = m.buf[prev.name, 'dy']
+                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act, dyp)
+                d = dyp
+            else:
+                acc = blk.identity or sc is not None
+                self._conv_bwd(m, u, d, inp, dx if u.need_dgrad else None, accumulate=acc)
+
+    # ------------------------------------------------------------------ data
+    def set_shard(self, images_u8, labels):
+        """Keep this rank's training shard resident in HBM: uint8 [Ns][H][W][3]."""
+        x = torch.as_tensor(np.ascontiguousarray(images_u8)) if not torch.is_tensor(images_u8) \
+            else images_u8
+        self.shard = x.to(self.device, torch.uint8).contiguous()
+        self.shard_labels = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
+        self.train_mode = self.mode('train', self.B, 0, True)
+        self.score_mode = self.mode('score', self.P, self.B, False)
+        self.idx = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self._arange_b = torch.arange(self.B, dtype=torch.int32, device=self.device)
+        self.isw = torch.ones(self.B, dtype=torch.float32, device=self.device)
+        self._build_bn_table()
+
+    def _build_bn_table(self):
+        rows = []
+        tm, sm = self.train_mode, self.score_mode
+        for u in self.units:
+            sp_t, sp_s = tm.spec[u.name], sm.spec[u.name]
+            rows.append((u.bn.running_mean, u.bn.running_var, tm.stats[u.name], sm.stats[u.name],
+                         u.bn.num_batches_tracked, u.K, 1, sm.G, float(sp_t.M),
+                         float(sp_s.group_rows or sp_s.M)))
+        self.bn_table = ops.BnRunTable(rows, self.device)
+
+    # ------------------------------------------------------------------ step pieces
+    def score_branch(self):
+        sm = self.score_mode
+        if not self.scoring:
+            # uniform-sampling baseline: the next batch is the next 32 shard samples
+            # (epoch-shuffled, augmented), no pool forward, unit weights
+            ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label,
+                           sm.index, self.B, self.B, self.seed)
+            self.ctrl[0:1].add_(1)
+            self.idx.copy_(self._arange_b)
+            self.isw.fill_(1.0)
+            return
+        sm.stats_arena.zero_()
+        ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label, sm.index,
+                       self.P, self.B, self.seed)
+        x = self.forward(sm)
+        self.head(sm, x, 'score')
+        ops.is_sample(sm.losses, self.ema, self.ctrl, self.idx, self.isw, self.P, self.B, self.B,
+                      self.alpha, self.ema_alpha, self.seed, self.importance, self.meters)
+
+    def gather_batch(self):
+        sm, tm = self.score_mode, self.train_mode
+        ops.gather(sm.input, sm.label, sm.index, self.idx, tm.input, tm.label, tm.index, self.B)
+
+    def train_segments(self):
+        """Train fwd + backward as a list of callables; bucket all-reduces go between them."""
+        tm = self.train_mode
+        segs = []
+
+        def fwd_head():
+            ops.lib().step_begin(ops.ptr(self.ctrl), ops.stream_ptr())
+            tm.stats_arena.zero_()
+            tm.sums_arena.zero_()
+            x = self.forward(tm)
+            self.head(tm, x, 'train', isw=self.isw, meters=self.meters)
+            last = len(self.lw.blocks) - 1
+            ops.head_bwd(tm.pooled, tm.dlogits, self._pview(self.lw.fc_w),
+                         self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True),
+                         tm.buf[last, 'dout'], self.B, tm.final_hw, tm.final_C, self.classes)
+        def join_wgrad():
+            if self.s_wgrad is not None:
+                torch.cuda.current_stream().wait_stream(self.s_wgrad)
+
+        cuts = self.bucket_plan()
+        cur = [fwd_head]
+        for bi in range(len(self.lw.blocks) - 1, -1, -1):
+            cur.append(lambda bi=bi: self.backward_block(tm, bi))
+            if bi in cuts:
+                segs.append((cur + [join_wgrad], cuts[bi]))
+                cur = []
+        if cur:
+            segs.append((cur + [join_wgrad], None))
+        return segs
+
+    def bucket_plan(self):
+        """{block index: (flat_start, flat_end)} -- a bucket closes after that block's backward."""
+        if self.world_size == 1:
+            return {}
+        starts = []
+        for bi, blk in enumerate(self.lw.blocks):
+            us = blk.units + ([blk.shortcut] if blk.shortcut else [])
+            starts.append(min(min(s.off for s in (u.w_seg, u.g_seg, u.beta_seg)) for u in us))
+        cuts = {}
+        end = self.lw.total
+        for bi in range(len(self.lw.blocks) - 1, -1, -1):
+            if bi == 0 or (end - starts[bi]) * 4 >= self.bucket_bytes:
+                cuts[bi] = (0 if bi == 0 else starts[bi], end)
+                end = starts[bi]
+        return cuts
+
+    def tail(self):
+        self.bn_table.launch(0.1)
+        self.opt.step(self.ctrl[2:3])
+        self.gather_batch()
+
+    # ------------------------------------------------------------------ graphs
+    def _capture(self, fn, stream):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            fn()
+        return g
+
+    def build_graphs(self):
+        torch.cuda.synchronize(self.device)
+        cap = torch.cuda.Stream(self.device)
+        segs = self.train_segments()
+        self.graphs = {
+            'score': self._capture(self.score_branch, cap),
+            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b) for fs, b in segs],
+            'tail': self._capture(self.tail, cap),
+        }
+        torch.cuda.synchronize(self.device)
+
+    def prime(self):
+        """Score a first pool and gather the first training batch (reference `train()` entry)."""
+        s0 = torch.cuda.current_stream(self.device)
+        self.s_score.wait_stream(s0)
+        with torch.cuda.stream(self.s_score):
+            self.score_branch()
+        s0.wait_stream(self.s_score)
+        self.gather_batch()
+
+    def step(self):
+        """One importance-sampled DP step (all async; nothing syncs the host)."""
+        s0 = torch.cuda.current_stream(self.device)
+        ev_start = torch.cuda.Event()
+        ev_start.record(s0)
+        self.s_score.wait_event(ev_start)
+        graphs = self.graphs if self.use_graphs else None
+        with torch.cuda.stream(self.s_score):
+            if graphs:
+                graphs['score'].replay()
+            else:
+                self.score_branch()
+        ev_score = torch.cuda.Event()
+        ev_score.record(self.s_score)
+        works = []
+        segs = graphs['train'] if graphs else self.train_segments()
+        for g, bucket in segs:
+            if graphs:
+                g.replay()
+            else:
+                for f in g:
+                    f()
+            if bucket is not None and self.world_size > 1:
+                s, e = bucket
+                works.append((dist.all_reduce(self.opt.g[s:e], op=self._avg_op,
+                                              async_op=True), s, e))
+        for w, s, e in works:
+            w.wait()
+            if self._avg_op != dist.ReduceOp.AVG:   # gloo has no AVG
+                self.opt.g[s:e].mul_(1.0 / self.world_size)
+        s0.wait_event(ev_score)
+        if graphs:
+            graphs['tail'].replay()
+        else:
+            self.tail()
+
+    # ------------------------------------------------------------------ misc API
+    def reset_ema(self):
+        self.ema.zero_()
+
+    def broadcast_from(self, src=0):
+        dist.broadcast(self.opt.p, src)
+        for u in self.units:
+            dist.broadcast(u.bn.running_mean, src)
+            dist.broadcast(u.bn.running_var, src)
+        self.opt.pack_weights()
+
+    @torch.no_grad()
+    def evaluate_arrays(self, images_u8, labels, batch=500):
+        """Eval-mode (running-stats BN) loss / accuracy over uint8 HWC images on device."""
+        imgs = torch.as_tensor(np.ascontiguousarray(images_u8)).to(self.device)
+        labs = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
+        n = imgs.shape[0]
+        self.eval_meters.zero_()
+        ctrl = torch.zeros(8, dtype=torch.int64, device=self.device)
+        done = 0
+        while done < n:
+            b = min(batch, n - done)
+            m = self.mode('eval%d' % b, b, 0, False)
+            ops.pool_build(imgs[done:done + b], labs[done:done + b], ctrl, m.input, m.label,
+                           m.index, b, b, self.seed, augment=False, shuffle=False)
+            x = self.forward(m)
+            self.head(m, x, 'eval', meters=self.eval_meters)
+            done += b
+        r = self.eval_meters[:3].tolist()
+        return r[0] / max(r[1], 1), r[2] / max(r[1], 1), int(r[1])
+
+    def read_meters(self):
+        b = self.meters.tolist()
+        return {'loss_sum': b[0], 'count': b[1], 'correct': b[2], 'pool_mean': b[3], 'ema': b[4]}
+
+
+# ---------------------------------------------------------------------- trainer
+def _dataset_arrays(loader):
+    ds = getattr(loader, 'dataset', None)
+    x = getattr(ds, 'data', None)
+    y = getattr(ds, 'target', None)
+    if y is None:
+        y = getattr(ds, 'targets', None)
+    if x is None or y is None:
+        raise ValueError('native engine needs a dataset with uint8 HWC .data and .target')
+    return np.asarray(x), np.asarray(y)
+
+
+class NativeTrainer(Trainer):
+    """``Trainer`` whose step runs on the native engine (same public API)."""
+
+    def __init__(self, net, optimizer, train_loader, presam_loader, test_loader, device,
+                 config=None):
+        from ..config import Config
+        cfg = config or Config()
+        self.cfg = cfg
+        self.net = net
+        self.optimizer = optimizer
+        self.train_loader = train_loader
+        self.presam_loader = presam_loader
+        self.test_loader = test_loader
+        self.device = torch.device(device)
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world_size = dist.get_world_size() if dist.is_initialized() else 1
+        self.com_tensor = torch.ones(1)
+        self.epoch, self.step, self.writer, self.scheduler = 0, 1, None, None
+        self.next_batch_iter = None
+        self.computed_samples = {'index': [], 'prob': []}
+        self.should_compute_importance = True
+        self.batch_size = getattr(train_loader, 'batch_size', None) or cfg.batch_size
+        self.steps_per_epoch = len(train_loader) if train_loader is not None else 1
+        self.flat = None
+        self.bucketer = None
+        from ..utils.logging import PhaseTimer
+        self.timer = PhaseTimer(self.device)
+        g = optimizer.param_groups[0]
+        algo = 'adam' if isinstance(optimizer, torch.optim.Adam) else 'sgd'
+        x, y = _dataset_arrays(presam_loader)
+        self.engine = NativeEngine(
+            net, self.device, self.batch_size, cfg.presample_batches, image_hw=x.shape[1:3],
+            optimizer=algo, lr=g['lr'], betas=g.get('betas', (0.9, 0.999)),
+            eps=g.get('eps', 1e-8), weight_decay=g.get('weight_decay', 0.0),
+            momentum=g.get('momentum', 0.9), seed=cfg.seed * 1000 + self.rank, alpha=cfg.alpha,
+            ema_alpha=cfg.ema_alpha, importance=cfg.importance, world_size=self.world_size,
+            bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs)
+        self.engine.set_shard(x, y)
+
+    def average_model(self):
+        if self.world_size == 1:
+            return
+        if self.cfg.parity:
+            dist.all_reduce(self.engine.opt.p, op=dist.ReduceOp.SUM)
+            self.engine.opt.p /= float(self.world_size)
+            self.engine.opt.pack_weights()
+        else:
+            self.engine.broadcast_from(0)
+
+    def average_gradients(self):
+        pass  # bucketed inside engine.step()
+
+    def update_samples(self, ema_loss=None, alpha=None):
+        """API-compatible scoring call: returns (weights, data NCHW, label, index, pool_mean)."""
+        e = self.engine
+        e.prime()
+        sm = e.score_mode
+        idx = e.idx.long()
+        data = sm.input[idx][..., :3].permute(0, 3, 1, 2).float()
+        mean = e.meters[3].clone()
+        if ema_loss is not None:
+            ema_loss.first_update = False
+            ema_loss.value = float(e.ema[0].item())
+        return e.isw.clone(), data, sm.label[idx].long(), sm.index[idx].long(), mean
+
+    def _sync_lr(self):
+        self.engine.opt.set_lr(self.optimizer.param_groups[0]['lr'])
+
+    def train(self):
+        e = self.engine
+        running_train_loss = Average()
+        presam_ema_loss = EMAverage(self.cfg.ema_alpha)
+        runing_train_acc = Accuracy()
+        e.reset_ema()                      # reference: fresh EMAverage per epoch (`:121`)
+        e.meters[:3].zero_()
+        self._sync_lr()
+        e.prime()
+        if e.use_graphs and e.graphs is None:
+            e.step()                       # one eager step warms every kernel, then capture
+            self.step += 1
+            e.build_graphs()
+        t0 = time.perf_counter()
+        for _ in range(self.steps_per_epoch):
+            e.step()
+            if self.cfg.print_every and self.step % self.cfg.print_every == 0:
+                self._log(t0)
+                t0 = time.perf_counter()
+            if self.cfg.eval_every and self.step % self.cfg.eval_every == 0 and (
+                    self.rank == 0 or self.cfg.eval_all_ranks):
+                self._eval_log()
+            self.step += 1
+            if self._stop():
+                break
+        m = e.read_meters()
+        running_train_loss.update(m['loss_sum'] / max(m['count'], 1), max(int(m['count']), 1))
+        runing_train_acc.update_counts(m['correct'], int(m['count']))
+        presam_ema_loss.update(m['ema'])
+        return running_train_loss, runing_train_acc, presam_ema_loss
+
+    def _log(self, t0):
+        if self.rank != 0:
+            return
+        m = self.engine.read_meters()
+        cnt = max(m['count'], 1)
+        print('step:{}, running train loss: {:.6f}, running train acc: {:.2f}%, '
+              'presam_ema_loss: {:.6f}, pool_mean: {:.4f}, {:.3f} ms/step'.format(
+                  self.step, m['loss_sum'] / cnt, 100 * m['correct'] / cnt, m['ema'],
+                  m['pool_mean'], (time.perf_counter() - t0) * 1e3 / self.cfg.print_every),
+              flush=True)
+
+    def _eval_log(self):
+        train_loss, train_acc, test_loss, test_acc = self.evaluate()
+        if self.writer is not None:
+            self.writer.add_scalar('train/acc', train_acc.accuracy, self.step)
+            self.writer.add_scalar('test/acc', test_acc.accuracy, self.step)
+            self.writer.add_scalar('train/loss', train_loss.average, self.step)
+            self.writer.add_scalar('test/loss', test_loss.average, self.step)
+        if self.rank == 0:
+            print('(Eval) Step: {}, train loss: {}, train acc: {} test loss: {}, test acc: {}'
+                  .format(self.step, train_loss, train_acc, test_loss, test_acc), flush=True)
+
+    def evaluate(self, max_batches=None):
+        out = []
+        for loader in (self.train_loader, self.test_loader):
+            lm, am = Average(), Accuracy()
+            if loader is not None:
+                x, y = _dataset_arrays(loader)
+                bs = getattr(loader, 'batch_size', 32) or 32
+                n = (len(x) // bs) * bs       # drop_last, as the reference loaders
+                if max_batches is not None:
+                    n = min(n, max_batches * bs)
+                loss, acc, cnt = self.engine.evaluate_arrays(x[:n], y[:n])
+                lm.update(loss, cnt)
+                am.update_counts(acc * cnt, cnt)
+            out += [lm, am]
+        return out[0], out[1], out[2], out[3]
+
+    def state_dict(self):
+        e = self.engine
+        e.sync_to_module()
+        ost = self.optimizer.state_dict()
+        state = {}
+        t = int(e.ctrl[2].item())
+        for i, s in enumerate(e.lw.segs):
+            st = {'step': torch.tensor(float(t)), 'exp_avg': e._to_torch_layout(s, e.opt.m).cpu()}
+            if e.opt.algo == 0:
+                st['exp_avg_sq'] = e._to_torch_layout(s, e.opt.v).cpu()
+            else:
+                st = {'momentum_buffer': st['exp_avg']}
+            state[i] = st
+        ost['state'] = state
+        return {'model': {k: v.detach().cpu() for k, v in self.net.state_dict().items()},
+                'optimizer': ost,
+                'scheduler': self.scheduler.state_dict() if self.scheduler else None,
+                'step': self.step, 'epoch': self.epoch,
+                'engine': {'ctrl': e.ctrl.cpu(), 'ema': e.ema.cpu()}}
+
+    def load_state_dict(self, sd):
+        e = self.engine
+        self.net.load_state_dict(sd['model'])
+        e.load_from_module()
+        st = sd['optimizer'].get('state', {})
+        for i, s in enumerate(e.lw.segs):
+            if i in st:
+                if 'exp_avg' in st[i]:
+                    e._from_torch_layout(s, e.opt.m, st[i]['exp_avg'])
+                if 'exp_avg_sq' in st[i] and e.opt.algo == 0:
+                    e._from_torch_layout(s, e.opt.v, st[i]['exp_avg_sq'])
+                if 'momentum_buffer' in st[i]:
+                    e._from_torch_layout(s, e.opt.m, st[i]['momentum_buffer'])
+        if sd.get('scheduler') and self.scheduler is not None:
+            self.scheduler.load_state_dict(sd['scheduler'])
+        self.optimizer.param_groups[0]['lr'] = sd['optimizer']['param_groups'][0]['lr']
+        self.step, self.epoch = sd['step'], sd['epoch']
+        if 'engine' in sd:
+            e.ctrl.copy_(sd['engine']['ctrl'].to(e.device))
+            e.ema.copy_(sd['engine']['ema'].to(e.device))
+
+
+# ---------------------------------------------------------------------- smoke
+def smoke_step(device='cuda:0', steps=2):
+    """Tiny end-to-end check used by ``__graft_entry__.smoke``."""
+    from ..models import ResNet18
+    torch.manual_seed(0)
+    net = ResNet18(10).to(device)
+    eng = NativeEngine(net, device, batch_size=32, pool_batches=10, use_graphs=True)
+    rng = np.random.RandomState(0)
+    eng.set_shard(rng.randint(0, 256, (640, 32, 32, 3), dtype=np.uint8),
+                  rng.randint(0, 10, 640))
+    eng.prime()
+    eng.step()
+    eng.build_graphs()
+    for _ in range(steps):
+        eng.step()
+    torch.cuda.synchronize()
+    m = eng.read_meters()
+    assert math.isfinite(m['loss_sum']) and m['count'] == 32 * (steps + 1), m
+    return m

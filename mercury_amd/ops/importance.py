@@ -8,14 +8,14 @@ from ..data.transforms import CIFAR_MEAN, CIFAR_STD
 
 
 def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed, pad=4,
-               flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD):
+               flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD, shuffle=True):
     """Build a P-sample presample pool from the uint8 shard [Ns][H][W][3] on device."""
     _chk(shard, torch.uint8, 'shard')
     _chk(labels, torch.int64, 'labels')
     Ns, H, W, _ = shard.shape
     _chk(pool, torch.bfloat16, 'pool', P * H * W * 8)
     lib().pool_build(ptr(shard), ptr(labels), ptr(ctrl), ptr(pool), ptr(pool_label),
-                     ptr(pool_index), Ns, H, W, P, batch, pad, int(flip), int(augment),
+                     ptr(pool_index), Ns, H, W, P, batch, pad, int(flip), int(augment), int(shuffle),
                      int(seed) & 0xffffffff, list(mean), [1.0 / s for s in std], stream_ptr())
 
 

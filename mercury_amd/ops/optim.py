@@ -37,6 +37,21 @@ class FlatOptimizer(object):
         packed = lib().pack_opt_segs(rows)
         self.segbuf = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(device)
         self.nsegs = len(rows)
+        # 64x64 transpose tiles producing the dgrad ([C][R][S][K]) weight copies
+        jobs = []
+        for i, s in enumerate(segments):
+            if s['kind'] == 1 and s.get('w_crsk') is not None:
+                for rs in range(s['R'] * s['S']):
+                    for k0 in range(0, s['K'], 64):
+                        for c0 in range(0, s['C'], 64):
+                            jobs.append((i, rs, k0, c0))
+        self.njobs = len(jobs)
+        self.jobs = torch.tensor(jobs if jobs else [(0, 0, 0, 0)], dtype=torch.int32,
+                                 device=device).contiguous()
+
+    def _transpose(self):
+        if self.njobs:
+            lib().transpose_weights(ptr(self.segbuf), ptr(self.jobs), self.njobs, stream_ptr())
 
     @property
     def lr(self):
@@ -50,7 +65,9 @@ class FlatOptimizer(object):
         lib().optimizer(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), ptr(self.segbuf),
                         self.nsegs, self.total, ptr(self.hyper), ptr(step_counter), self.algo,
                         int(zero_grad), stream_ptr())
+        self._transpose()
 
     def pack_weights(self):
         """Write the bf16 conv-weight copies from the fp32 master (after init / load)."""
         lib().pack_weights(ptr(self.p), ptr(self.segbuf), self.nsegs, self.total, stream_ptr())
+        self._transpose()

@@ -1,0 +1,144 @@
+"""Native engine vs the PyTorch module: forward, IS-weighted backward, scoring, steps."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _cos(a, b):
+    a, b = a.flatten().double(), b.flatten().double()
+    return float((a @ b) / (a.norm() * b.norm() + 1e-30))
+
+
+def _engine(net, **kw):
+    from mercury_amd.engine.native import NativeEngine
+    eng = NativeEngine(net, DEV, batch_size=32, pool_batches=10, use_graphs=False, **kw)
+    rng = np.random.RandomState(0)
+    eng.set_shard(rng.randint(0, 256, (1000, 32, 32, 3), dtype=np.uint8), rng.randint(0, 10, 1000))
+    return eng
+
+
+@pytest.mark.parametrize('arch', ['resnet18', 'resnet50', 'mobilenetv2'])
+def test_train_forward_backward_matches_torch(arch):
+    from mercury_amd import ops
+    from mercury_amd.models import build_model
+    torch.manual_seed(0)
+    ncls = 100 if arch == 'mobilenetv2' else 10
+    net = build_model(arch, ncls).to(DEV)
+    eng = _engine(net)
+    tm = eng.train_mode
+    x = torch.randn(32, 3, 32, 32, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, ncls, (32,), device=DEV)
+    w = torch.rand(32, device=DEV) + 0.5
+    tm.input.copy_(ops.to_nhwc(x))
+    tm.label.copy_(y.int())
+    eng.isw.copy_(w)
+    tm.stats_arena.zero_()
+    out = eng.forward(tm)
+    eng.head(tm, out, 'train', isw=eng.isw, meters=eng.meters)
+    last = len(eng.lw.blocks) - 1
+    ops.head_bwd(tm.pooled, tm.dlogits, eng._pview(eng.lw.fc_w), eng._pview(eng.lw.fc_w, True),
+                 eng._pview(eng.lw.fc_b, True), tm.buf[last, 'dout'], 32, tm.final_hw,
+                 tm.final_C, eng.classes)
+    for bi in range(last, -1, -1):
+        eng.backward_block(tm, bi)
+    torch.cuda.synchronize()
+    # torch reference in train mode (batch-stat BN), same weights
+    net.train()
+    net.zero_grad()
+    logits = net(x)
+    loss = (F.cross_entropy(logits, y, reduction='none') / w).mean()
+    loss.backward()
+    got_loss = eng.meters[0].item() / 32
+    assert abs(got_loss - loss.item()) < 0.05 * abs(loss.item()) + 0.02, (got_loss, loss.item())
+    # what plain PyTorch reaches in bf16 on the same problem sets the tolerance:
+    # deep layers' gradients pass through ~20 bf16 BN/conv backward stages
+    import copy
+    nb = copy.deepcopy(net).to(torch.bfloat16)
+    nb.zero_grad()
+    lb = (F.cross_entropy(nb(x.to(torch.bfloat16)).float(), y, reduction='none') / w).mean()
+    lb.backward()
+    pb = dict(nb.named_parameters())
+    worst = 0.0
+    for s in eng.lw.segs:
+        g = eng._to_torch_layout(s, eng.opt.g)
+        ref = s.param.grad
+        if ref.norm() < 1e-8:
+            continue
+        gb = pb[s.name].grad.float()
+        err = float((g - ref).norm())
+        err_tb = float((gb - ref).norm())
+        # no worse than PyTorch's own bf16 run (some grads, e.g. the stem BN bias, are
+        # near-cancelling sums where even torch-bf16 keeps little of the fp32 direction)
+        worst = max(worst, err / max(err_tb, 1e-12))
+        assert err <= max(2.5 * err_tb, 0.05 * float(ref.norm())), (s.name, err, err_tb)
+    print(arch, 'worst grad error relative to torch-bf16', worst)
+
+
+def test_scoring_ghost_bn_matches_ten_separate_forwards():
+    from mercury_amd.models import ResNet18
+    torch.manual_seed(1)
+    net = ResNet18(10).to(DEV)
+    eng = _engine(net)
+    sm = eng.score_mode
+    sm.stats_arena.zero_()
+    from mercury_amd import ops
+    ops.pool_build(eng.shard, eng.shard_labels, eng.ctrl, sm.input, sm.label, sm.index, 320, 32,
+                   eng.seed)
+    x = eng.forward(sm)
+    eng.head(sm, x, 'score')
+    torch.cuda.synchronize()
+    data = sm.input[..., :3].permute(0, 3, 1, 2).float()
+    ref = []
+    net.train()
+    with torch.no_grad():
+        for j in range(10):  # the reference's 10 separate train-mode forwards
+            o = net(data[j * 32:(j + 1) * 32])
+            ref.append(F.cross_entropy(o, sm.label[j * 32:(j + 1) * 32].long(), reduction='none'))
+    ref = torch.cat(ref)
+    assert _cos(sm.losses, ref) > 0.995
+    assert (sm.losses - ref).abs().mean().item() < 0.05
+
+
+@pytest.mark.parametrize('graphs', [False, True])
+def test_steps_reduce_loss_and_graph_matches_eager(graphs):
+    from mercury_amd.data.datasets import synthetic_arrays
+    from mercury_amd.engine.native import NativeEngine
+    from mercury_amd.models import ResNet18
+    x, y = synthetic_arrays(4000, 10, seed=3)
+    torch.manual_seed(0)
+    net = ResNet18(10).to(DEV)
+    eng = NativeEngine(net, DEV, 32, 10, lr=1e-3, use_graphs=graphs)
+    eng.set_shard(x, y)
+    eng.prime()
+    eng.step()
+    if graphs:
+        eng.build_graphs()
+    losses = []
+    for i in range(60):
+        eng.meters[:3].zero_()
+        eng.step()
+        m = eng.read_meters()
+        losses.append(m['loss_sum'] / m['count'])
+    assert all(math.isfinite(v) for v in losses)
+    assert np.mean(losses[-10:]) < np.mean(losses[:10]), losses
+    assert int(eng.ctrl[2].item()) == 61
+    # BN running stats moved (train + 10 scoring updates per step)
+    u = eng.units[0]
+    assert int(u.bn.num_batches_tracked.item()) == 61 * 11
+    eng.sync_to_module()
+    net.eval()
+    loss, acc, n = eng.evaluate_arrays(x[:1000], y[:1000])
+    with torch.no_grad():
+        from mercury_amd import ops
+        xx = torch.as_tensor(x[:1000]).to(DEV).permute(0, 3, 1, 2).float() / 255
+        mean = torch.tensor([0.49139968, 0.48215827, 0.44653124], device=DEV).view(1, 3, 1, 1)
+        std = torch.tensor([0.24703233, 0.24348505, 0.26158768], device=DEV).view(1, 3, 1, 1)
+        lo = net(((xx - mean) / std).to(torch.bfloat16).float())
+        ref_loss = F.cross_entropy(lo, torch.as_tensor(y[:1000]).to(DEV)).item()
+    assert n == 1000 and abs(loss - ref_loss) < 0.05 * ref_loss + 0.05, (loss, ref_loss)
