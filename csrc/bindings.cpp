@@ -30,11 +30,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("igemm", [](uintptr_t src, uintptr_t wt, uintptr_t out, int ldo, uintptr_t bias,
                     uintptr_t stats, int stats_ld, int group_rows, int accumulate, uintptr_t slab,
                     int SH, int SW, int SC, int RP, int RQ, int R, int Sk, int stride, int pad, int Kc,
-                    int Ncols, int M, int bm, int bn, int splits, bool trans, uintptr_t st) {
+                    int Ncols, int M, int bm, int bn, int splits, bool trans, uintptr_t st,
+                    int pipe) {
     ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
     EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows,
                 accumulate, P<float>(slab)};
-    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
+    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
     check_launch("igemm");
   });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {

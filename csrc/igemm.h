@@ -29,8 +29,9 @@ struct EpiParams {
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
+// pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
-                  int bn, int splits, bool trans, hipStream_t st);
+                  int bn, int splits, bool trans, hipStream_t st, int pipe = 0);
 
 struct WgradGeom {
   int N, H, W, C;     // input x (C padded), NHWC

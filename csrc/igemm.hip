@@ -15,18 +15,25 @@
 // one 16-byte load = one (pixel, 8-channel) chunk = exactly the 8 bf16 a lane
 // feeds to v_mfma_f32_16x16x32_bf16 (lane l: row l&15, k = 8*(l>>4)..+7).
 //
-// Structure: 256 threads = 4 waves (2x2), BMxBN output tile, BK = 64 per stage,
-// register-staged double-buffered LDS (global loads of stage t+1 are issued before
-// the MFMAs of stage t and written to the other LDS buffer after them: one barrier
-// per stage), XOR-swizzled LDS rows (16-B chunk c of row r lives at c ^ (r&7)) so
-// the ds_read_b128 fragment reads are spread over the banks.  Split-K writes fp32
-// partial tiles in MFMA fragment order (fully coalesced 16 B/lane) and a reducer
-// with the same epilogue finishes them.
+// The MFMA is issued with the operands SWAPPED (weights as the "A" input, pixels
+// as "B"), so the accumulator comes out transposed: lane l holds output pixel
+// l&15 and FOUR CONSECUTIVE CHANNELS 4*(l>>4)..+3 -- 8 contiguous bytes of the
+// NHWC output.  The epilogue therefore stores straight from registers (no LDS
+// staging pass), and BN statistics reduce across the 16 pixel lanes with four
+// DPP row operations (cdna_hip_programming.md §3: choose the product orientation
+// so later consumers see the layout they want).
 //
-// Epilogue (fused): optional per-channel bias, bf16 rounding, per-(ghost-group,
-// channel) BatchNorm sum/sum-of-squares from the rounded values (LDS pre-reduce,
-// one atomic per column per block), optional accumulate-into-existing (dgrad of a
-// residual), coalesced 16-B stores through an LDS-staged tile.
+// Main loop (two variants, same LDS image and fragment reads):
+//   pipe 0 : 256 threads = 4 waves (2x2), BK = 64 per stage, register-staged double
+//            buffer (stage t+1 loads issued before stage t's MFMAs, one barrier/stage)
+//   pipe 3/4: LDS-DMA ring (`global_load_lds_dwordx4`) of that many stages, counted
+//            `s_waitcnt vmcnt(N)` + raw `s_barrier` so tiles stay in flight across
+//            barriers; the XOR swizzle moves to the source address (lane l fetches
+//            logical chunk (l&7)^(l>>3) of its row, landing at physical chunk l&7).
+// LDS rows are XOR-swizzled (chunk c of row r lives at c ^ (r&7)).  All address math
+// is 32-bit (per-row base offsets + one uniform per-tap offset), padding chunks read
+// a zero page.  Split-K writes fp32 partial tiles in fragment order (16 B per lane,
+// fully coalesced) and a reducer runs the same epilogue.
 #include "common.h"
 #include "igemm.h"
 
@@ -35,74 +42,87 @@ namespace {
 constexpr int BK = 64;          // k elements per stage (8 chunks of 8)
 constexpr int NT = 256;         // threads
 
+__device__ __attribute__((aligned(16))) bf16 g_zero_page[64];
+
 MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
 template <int BM, int BN>
 struct Smem {
-  static constexpr int A_ELEMS = BM * BK;
-  static constexpr int B_ELEMS = BN * BK;
-  static constexpr int STAGE = A_ELEMS + B_ELEMS;
-  static constexpr int LOOP_BYTES = 2 * STAGE * 2;
-  static constexpr int EPI_BYTES = BM * (BN + 8) * 2 + 2 * BN * 4 * 2;
-  static constexpr int BYTES = LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES;
+  static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
+  static constexpr int RED_BYTES = 2 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
+  static constexpr int bytes(int stages) {
+    return stages * STAGE * 2 > RED_BYTES ? stages * STAGE * 2 : RED_BYTES;
+  }
 };
 
+// DPP sum over the 16 lanes of a row (quad xor1, quad xor2, half-mirror, mirror)
+MA_DEV float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 // ---------------------------------------------------------------- epilogue
-// acc[tm][tn][j] holds OUT[row0 + tm*16 + (lane>>4)*4 + j][col0 + tn*16 + (lane&15)]
-// with row0 = m0 + wm*(BM/2), col0 = n0 + wn*(BN/2).
+// acc[tm][tn][j] = OUT[m0 + wm*(BM/2) + tm*16 + (lane&15)][n0 + wn*(BN/2) + tn*16 + 4*(lane>>4) + j]
 template <int BM, int BN>
-MA_DEV void epilogue_bf16(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e,
-                          int M, int N, int m0, int n0) {
+MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
+                     int m0, int n0) {
   constexpr int TM = BM / 32, TN = BN / 32, LDT = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  bf16* tile = (bf16*)smem;
-  float* red = (float*)(smem + BM * LDT * 2);  // [2][BN] sum, sumsq
   const bool stats = e.stats != nullptr;
+  float* red = (float*)smem;                       // [2][BN] sum, sumsq
+  bf16* tile = (bf16*)(smem + 2 * BN * 4);         // [BM][LDT] staged output
   if (stats) {
     for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
   }
-  // bias loads hoisted and issued together (a conditional load per column would be
-  // serialised behind its own vmcnt(0))
-  float biasv[TN];
+  float4 bias[TN];
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn) biasv[tn] = 0.f;
+  for (int tn = 0; tn < TN; ++tn) bias[tn] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e.bias) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const int col = n0 + wn * (BN / 2) + tn * 16 + (lane & 15);
-      biasv[tn] = e.bias[col < N ? col : N - 1];
+      const int nb = n0 + wn * (BN / 2) + tn * 16 + 4 * (lane >> 4);
+      bias[tn] = *(const float4*)(e.bias + (nb < N ? nb : N - 4));
     }
   }
   __syncthreads();
+  const int mrow = m0 + wm * (BM / 2) + (lane & 15);
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
-    const int cl = wn * (BN / 2) + tn * 16 + (lane & 15);
-    const int col = n0 + cl;
-    const float bias = biasv[tn];
-    float s = 0.f, ss = 0.f;
+    const int nl = wn * (BN / 2) + tn * 16 + 4 * (lane >> 4);
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+    const float bb[4] = {bias[tn].x, bias[tn].y, bias[tn].z, bias[tn].w};
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
+      const int ml = wm * (BM / 2) + tm * 16 + (lane & 15);
+      bf16x4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int rl = wm * (BM / 2) + tm * 16 + (lane >> 4) * 4 + j;
-        const bf16 v = f2bf(acc[tm][tn][j] + bias);
-        tile[rl * LDT + cl] = v;
-        if (stats && (m0 + rl) < M) {
-          const float fv = bf2f(v);
-          s += fv;
-          ss += fv * fv;
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j] + bb[j]);
+      *(bf16x4*)(tile + ml * LDT + nl) = o;   // one 8-byte LDS write per lane
+      if (stats && mrow + tm * 16 < M) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = bf2f(o[j]);
+          s[j] += f;
+          ss[j] += f * f;
         }
       }
     }
     if (stats) {
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      ss += __shfl_xor(ss, 16, 64);
-      ss += __shfl_xor(ss, 32, 64);
-      if (lane < 16) {
-        atomicAdd(&red[cl], s);
-        atomicAdd(&red[BN + cl], ss);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] = row16_sum(s[j]);
+        ss[j] = row16_sum(ss[j]);
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(&red[nl + j], s[j]);
+          atomicAdd(&red[BN + nl + j], ss[j]);
+        }
       }
     }
   }
@@ -118,8 +138,8 @@ MA_DEV void epilogue_bf16(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiP
       }
     }
   }
-  // coalesced 16-byte stores
-  constexpr int CPR = BN / 8;  // chunks per row
+  // coalesced 16-byte row stores from the staged tile
+  constexpr int CPR = BN / 8;
   for (int i = tid; i < BM * CPR; i += NT) {
     const int rl = i / CPR, ch = i - rl * CPR;
     const int row = m0 + rl, col = n0 + ch * 8;
@@ -135,6 +155,139 @@ MA_DEV void epilogue_bf16(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiP
   }
 }
 
+// ---------------------------------------------------------------- A-row gather helpers
+// (plain scalars per row -- a struct holding the per-row arrays was demoted to scratch
+// by hipcc, which turned every gather into a scratch load + vmcnt(0))
+template <bool TRANS>
+MA_DEV void row_init(const ConvGeom& g, int m, int& off, int& h, int& w) {
+  if (m < g.M) {
+    const int pq = g.RP * g.RQ;
+    const int n = m / pq, rem = m - n * pq;
+    const int p = rem / g.RQ, q = rem - p * g.RQ;
+    off = n * g.SH * g.SW;
+    h = TRANS ? p + g.pad : p * g.stride - g.pad;
+    w = TRANS ? q + g.pad : q * g.stride - g.pad;
+  } else {
+    off = -1;
+    h = w = 0;
+  }
+}
+
+// element offset of (row, tap r/s, channel chunk c8) or -1 for a zero chunk
+template <bool TRANS>
+MA_DEV int row_at(const ConvGeom& g, int off, int h, int w, int r, int s, int c8) {
+  if (off < 0) return -1;
+  int hh, ww;
+  if (TRANS) {
+    const int hp = h - r, wp = w - s;
+    if (hp < 0 || wp < 0) return -1;
+    if (g.stride == 2) {
+      if ((hp | wp) & 1) return -1;
+      hh = hp >> 1;
+      ww = wp >> 1;
+    } else {
+      hh = hp;
+      ww = wp;
+    }
+    if (hh >= g.SH || ww >= g.SW) return -1;
+  } else {
+    hh = h + r;
+    ww = w + s;
+    if (hh < 0 || ww < 0 || hh >= g.SH || ww >= g.SW) return -1;
+  }
+  return (off + hh * g.SW + ww) * g.SC + c8 * 8;
+}
+
+// k-chunk -> (r, s, c8) cursor.  When C/8 is a multiple of 8 a 64-deep stage lies in one
+// filter tap, so the tap advances incrementally (no division in the loop).
+struct KCursor {
+  int tr, ts, tc;
+  bool fast;
+  MA_DEV void init(const ConvGeom& g, int kt0) {
+    const int C8 = g.SC >> 3;
+    fast = (C8 & 7) == 0;
+    tr = ts = tc = 0;
+    if (fast) {
+      const int k0c = kt0 * 8;
+      const int rs = k0c / C8;
+      tc = k0c - rs * C8;
+      tr = rs / g.S;
+      ts = rs - tr * g.S;
+    }
+  }
+  // decode the chunk `lcc` (0..7) of stage kt and advance after the last use
+  MA_DEV void decode(const ConvGeom& g, int kt, int lcc, int& r, int& s, int& c8, bool& kval) const {
+    const int kc = kt * 8 + lcc;
+    kval = kc < g.Kc;
+    if (fast) {
+      r = tr;
+      s = ts;
+      c8 = tc + lcc;
+    } else {
+      const int C8 = g.SC >> 3;
+      const int rs = kc / C8;
+      c8 = kc - rs * C8;
+      r = rs / g.S;
+      s = rs - r * g.S;
+    }
+  }
+  MA_DEV void advance(const ConvGeom& g) {
+    if (!fast) return;
+    tc += 8;
+    if (tc == (g.SC >> 3)) {
+      tc = 0;
+      if (++ts == g.S) {
+        ts = 0;
+        ++tr;
+      }
+    }
+  }
+};
+
+template <int BM, int BN>
+MA_DEV void mma_stage(const bf16* a, const bf16* b, f32x4 (&acc)[BM / 32][BN / 32], int lane,
+                      int wm, int wn) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int chunk = kk * 4 + (lane >> 4);
+    bf16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int row = wm * (BM / 2) + tm * 16 + (lane & 15);
+      fa[tm] = *(const bf16x8*)(a + row * BK + swz(row, chunk) * 8);
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int row = wn * (BN / 2) + tn * 16 + (lane & 15);
+      fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
+    }
+    // swapped operands: weights as the MFMA "A", pixels as "B" -> transposed accumulator
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
+  }
+}
+
+template <int BM, int BN>
+MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
+                   int m0, int n0) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  if (e.slab) {  // split-K partial in fragment order: [split][tile][TM*TN][256 threads] float4
+    const size_t ntiles = (size_t)gridDim.x;
+    f32x4* dst = (f32x4*)e.slab + ((size_t)blockIdx.y * ntiles + blockIdx.x) * (TM * TN) * NT;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) dst[(tm * TN + tn) * NT + threadIdx.x] = acc[tm][tn];
+    return;
+  }
+  epilogue<BM, BN>(acc, smem, e, M, N, m0, n0);
+}
+
+// ---------------------------------------------------------------- register-staged loop
 template <int BM, int BN, bool TRANS>
 __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict__ src,
                                                           const bf16* __restrict__ wt,
@@ -142,7 +295,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
                                                           int ktiles_per_split) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;  // rows per thread for A / B staging
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
   bf16* sA = (bf16*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -153,100 +306,42 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
   const int ktiles = (g.Kc + 7) / 8;
   const int kt0 = blockIdx.y * ktiles_per_split;
   const int kt1 = min(ktiles, kt0 + ktiles_per_split);
-  const int C8 = g.SC >> 3;
   const int Kelems = g.Kc * 8;
-
-  // per-thread A rows: decode pixel once
   const int cc = tid & 7;
-  int a_base[AR], a_h[AR], a_w[AR];
+
+  int aoff[AR], ah[AR], aw[AR];
 #pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
-    if (m < g.M) {
-      const int pq = g.RP * g.RQ;
-      const int n = m / pq, rem = m - n * pq;
-      const int p = rem / g.RQ, q = rem - p * g.RQ;
-      a_base[i] = n * g.SH * g.SW;
-      if (TRANS) {
-        a_h[i] = p + g.pad;
-        a_w[i] = q + g.pad;
-      } else {
-        a_h[i] = p * g.stride - g.pad;
-        a_w[i] = q * g.stride - g.pad;
-      }
-    } else {
-      a_base[i] = -1;
-      a_h[i] = a_w[i] = 0;
-    }
+  for (int i = 0; i < AR; ++i) row_init<TRANS>(g, m0 + (tid >> 3) + 32 * i, aoff[i], ah[i], aw[i]);
+  int boff[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    boff[i] = n < g.Ncols ? n * Kelems : -1;
   }
+  KCursor kc;
+  kc.init(g, kt0);
+  const bf16* zp = g_zero_page;
 
   u32x4 ra[AR], rb[BR];
-  // k-chunk -> (r, s, c8).  When C/8 is a multiple of 8 a whole 64-deep stage lies in one
-  // filter tap, so (r, s, c8 base) advance incrementally without integer division.
-  const bool fastk = (C8 & 7) == 0;
-  int tr = 0, ts = 0, tc = 0;
-  if (fastk) {
-    const int k0c = kt0 * 8;
-    const int rs = k0c / C8;
-    tc = k0c - rs * C8;
-    tr = rs / g.S;
-    ts = rs - tr * g.S;
-  }
   auto load_stage = [&](int kt) {
-    const int kc = kt * 8 + cc;
-    const bool kval = kc < g.Kc;
-    int r = 0, s = 0, c8 = 0;
-    if (fastk) {
-      r = tr;
-      s = ts;
-      c8 = tc + cc;
-      tc += 8;  // advance the stage cursor for the next call
-      if (tc == C8) {
-        tc = 0;
-        if (++ts == g.S) {
-          ts = 0;
-          ++tr;
-        }
-      }
-    } else if (kval) {
-      const int rs = kc / C8;
-      c8 = kc - rs * C8;
-      r = rs / g.S;
-      s = rs - r * g.S;
-    }
+    int r, s, c8;
+    bool kval;
+    kc.decode(g, kt, cc, r, s, c8, kval);
+    kc.advance(g);
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (kval && a_base[i] >= 0) {
-        int h, ww;
-        bool ok;
-        if (TRANS) {
-          const int hp = a_h[i] - r, wp = a_w[i] - s;
-          ok = hp >= 0 && wp >= 0;
-          if (g.stride == 2) ok = ok && !((hp | wp) & 1);
-          h = g.stride == 2 ? (hp >> 1) : hp;
-          ww = g.stride == 2 ? (wp >> 1) : wp;
-          ok = ok && h < g.SH && ww < g.SW;
-        } else {
-          h = a_h[i] + r;
-          ww = a_w[i] + s;
-          ok = h >= 0 && ww >= 0 && h < g.SH && ww < g.SW;
-        }
-        if (ok) v = *(const u32x4*)(src + (size_t)(a_base[i] + h * g.SW + ww) * g.SC + c8 * 8);
-      }
-      ra[i] = v;
+      const int o = kval ? row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8) : -1;
+      ra[i] = *(const u32x4*)(o >= 0 ? src + o : zp);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (kval && n < g.Ncols) v = *(const u32x4*)(wt + (size_t)n * Kelems + kc * 8);
-      rb[i] = v;
+      const bool ok = kval && boff[i] >= 0;
+      rb[i] = *(const u32x4*)(ok ? wt + boff[i] + (kt * 8 + cc) * 8 : zp);
     }
   };
   auto store_stage = [&](int buf) {
     bf16* a = sA + buf * Smem<BM, BN>::STAGE;
-    bf16* b = a + Smem<BM, BN>::A_ELEMS;
+    bf16* b = a + BM * BK;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = (tid >> 3) + 32 * i;
@@ -274,50 +369,113 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
       const bool more = kt + 1 < kt1;
       if (more) load_stage(kt + 1);
       const bf16* a = sA + buf * Smem<BM, BN>::STAGE;
-      const bf16* b = a + Smem<BM, BN>::A_ELEMS;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + (lane >> 4);
-        bf16x8 fa[TM], fb[TN];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          const int row = wm * (BM / 2) + tm * 16 + (lane & 15);
-          fa[tm] = *(const bf16x8*)(a + row * BK + swz(row, chunk) * 8);
-        }
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          const int row = wn * (BN / 2) + tn * 16 + (lane & 15);
-          fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
-        }
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
-      }
+      mma_stage<BM, BN>(a, a + BM * BK, acc, lane, wm, wn);
       if (more) store_stage(buf ^ 1);
       __syncthreads();
       buf ^= 1;
     }
   }
+  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
+}
 
-  if (e.slab) {
-    // split-K partial in fragment order: [split][tile][TM*TN][256 threads] float4
-    const size_t ntiles = (size_t)gridDim.x;
-    f32x4* dst = (f32x4*)e.slab + ((size_t)blockIdx.y * ntiles + blockIdx.x) * (TM * TN) * NT;
+// ---------------------------------------------------------------- LDS-DMA ring loop
+template <int N>
+MA_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+MA_DEV void glds16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int BM, int BN, int STAGES, bool TRANS>
+__global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restrict__ src,
+                                                            const bf16* __restrict__ wt,
+                                                            ConvGeom g, EpiParams e,
+                                                            int ktiles_per_split) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int AI = BM / 32, BI = BN / 32;  // LDS-DMA instructions per wave per stage
+  constexpr int G = AI + BI;
+  constexpr int STAGE = Smem<BM, BN>::STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(STAGES)];
+  bf16* sbase = (bf16*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.Ncols + BN - 1) / BN;
+  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (g.Kc + 7) / 8;
+  const int kt0 = blockIdx.y * ktiles_per_split;
+  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
+  const int Kelems = g.Kc * 8;
+  const int lrow = lane >> 3;                  // row inside an 8-row DMA instruction
+  const int lc = (lane & 7) ^ lrow;            // logical chunk this lane fetches
+
+  int aoff[AI], ah[AI], aw[AI];
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+  for (int i = 0; i < AI; ++i)
+    row_init<TRANS>(g, m0 + w * (BM / 4) + i * 8 + lrow, aoff[i], ah[i], aw[i]);
+  int boff[BI];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) dst[(tm * TN + tn) * NT + tid] = acc[tm][tn];
-    return;
+  for (int i = 0; i < BI; ++i) {
+    const int n = n0 + w * (BN / 4) + i * 8 + lrow;
+    boff[i] = n < g.Ncols ? n * Kelems : -1;
   }
-  epilogue_bf16<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
+  KCursor kc;
+  kc.init(g, kt0);
+  const bf16* zp = g_zero_page;
+
+  auto issue = [&](int kt, int slot) {
+    bf16* a_st = sbase + slot * STAGE;
+    bf16* b_st = a_st + BM * BK;
+    int r, s, c8;
+    bool kval;
+    kc.decode(g, kt, lc, r, s, c8, kval);
+    kc.advance(g);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int o = kval ? row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8) : -1;
+      glds16(o >= 0 ? (const void*)(src + o) : (const void*)zp, a_st + (w * (BM / 4) + i * 8) * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bool ok = kval && boff[i] >= 0;
+      glds16(ok ? (const void*)(wt + boff[i] + (kt * 8 + lc) * 8) : (const void*)zp,
+             b_st + (w * (BN / 4) + i * 8) * BK);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kt1 - kt0;
+#pragma unroll
+  for (int j = 0; j < STAGES - 1; ++j)
+    if (j < nk) issue(kt0 + j, j);
+  for (int it = 0; it < nk; ++it) {
+    const int ahead = min(STAGES - 2, nk - 1 - it);  // tiles issued after this one
+    if (ahead >= 2) wait_vmcnt<2 * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (it + STAGES - 1 < nk) issue(kt0 + it + STAGES - 1, (it + STAGES - 1) % STAGES);
+    const bf16* a = sbase + (it % STAGES) * STAGE;
+    mma_stage<BM, BN>(a, a + BM * BK, acc, lane, wm, wn);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
 }
 
 template <int BM, int BN>
 __global__ __launch_bounds__(NT) void splitk_reduce_kernel(ConvGeom g, EpiParams e, int splits) {
   constexpr int TM = BM / 32, TN = BN / 32;
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::EPI_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::RED_BYTES];
   const int tid = threadIdx.x;
   const int ntn = (g.Ncols + BN - 1) / BN;
   const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
@@ -334,12 +492,25 @@ __global__ __launch_bounds__(NT) void splitk_reduce_kernel(ConvGeom g, EpiParams
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) acc[tm][tn] += src[(tm * TN + tn) * NT + tid];
   }
-  epilogue_bf16<BM, BN>(acc, smem, e, g.M, g.Ncols, mt * BM, nt * BN);
+  epilogue<BM, BN>(acc, smem, e, g.M, g.Ncols, mt * BM, nt * BN);
+}
+
+template <int BM, int BN, bool TRANS>
+void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int per,
+                 dim3 grid, int pipe, hipStream_t st) {
+  if (pipe >= 4)
+    hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, (BM + BN > 256 ? 3 : 4), TRANS>), grid, dim3(NT),
+                       0, st, src, wt, g, e, per);
+  else if (pipe == 3)
+    hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, 3, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e,
+                       per);
+  else
+    hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
 }
 
 template <int BM, int BN, bool TRANS>
 void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
-                hipStream_t st) {
+                int pipe, hipStream_t st) {
   const int mtiles = (g.M + BM - 1) / BM, ntiles = (g.Ncols + BN - 1) / BN;
   const int ktiles = (g.Kc + 7) / 8;
   splits = splits < 1 ? 1 : (splits > ktiles ? ktiles : splits);
@@ -348,10 +519,9 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
   dim3 grid(mtiles * ntiles, splits);
   if (splits == 1) {
     e.slab = nullptr;
-    hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
+    launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);
   } else {
-    EpiParams ep = e;  // the GEMM writes slabs; the reducer runs the real epilogue
-    hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, ep, per);
+    launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);  // writes slabs
     hipLaunchKernelGGL((splitk_reduce_kernel<BM, BN>), dim3(mtiles * ntiles), dim3(NT), 0, st, g, e,
                        splits);
   }
@@ -365,12 +535,12 @@ size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
 }
 
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e,
-                  int bm, int bn, int splits, bool trans, hipStream_t st) {
-#define MA_CASE(BM_, BN_)                                                \
-  if (bm == BM_ && bn == BN_) {                                          \
-    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, st);    \
-    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, st);         \
-    return;                                                              \
+                  int bm, int bn, int splits, bool trans, hipStream_t st, int pipe) {
+#define MA_CASE(BM_, BN_)                                                      \
+  if (bm == BM_ && bn == BN_) {                                                \
+    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, pipe, st);    \
+    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, pipe, st);         \
+    return;                                                                    \
   }
   MA_CASE(128, 128)
   MA_CASE(128, 64)

@@ -14,9 +14,13 @@ from dataclasses import dataclass
 
 import torch
 
+import os
+
 from . import _chk, lib, ptr, stream_ptr
 
 CU = 256
+# NT implicit-GEMM main loop: 0 = register-staged double buffer, 3/4 = LDS-DMA ring
+PIPE = int(os.environ.get('MERCURY_IGEMM_PIPE', '0'))
 
 
 def cpad8(c):
@@ -116,7 +120,7 @@ def _slab(slab, need, device):
 
 
 def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=None,
-             accumulate=False):
+             accumulate=False, pipe=None):
     """out[M][K] = conv(x NHWC, w [K][R][S][Cp]); optional BN-sum epilogue."""
     Cp = spec.Cp
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
@@ -130,11 +134,12 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     lib().igemm(ptr(x), ptr(w), ptr(out), spec.K, ptr(bias), ptr(stats), spec.K, grp,
                 int(accumulate), ptr(slab) if splits > 1 else 0,
                 spec.H, spec.W, Cp, spec.P, spec.Q, spec.R, spec.S, spec.stride, spec.pad,
-                spec.R * spec.S * Cp // 8, spec.K, spec.M, bm, bn, splits, False, stream_ptr())
+                spec.R * spec.S * Cp // 8, spec.K, spec.M, bm, bn, splits, False, stream_ptr(),
+                PIPE if pipe is None else pipe)
     return out
 
 
-def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False):
+def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, pipe=None):
     """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2."""
     if spec.stride not in (1, 2):
         raise ValueError('dgrad supports stride 1/2')
@@ -151,7 +156,8 @@ def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=Fals
     lib().igemm(ptr(dy), ptr(wt), ptr(dx), Cp, 0, 0, Cp, Mx, int(accumulate),
                 ptr(slab) if splits > 1 else 0,
                 spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
-                spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, True, stream_ptr())
+                spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, True, stream_ptr(),
+                PIPE if pipe is None else pipe)
     return dx
 
 
