@@ -134,9 +134,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("is_sample", [](uintptr_t losses, uintptr_t ema, uintptr_t ctrl, uintptr_t idx, uintptr_t w,
                         uintptr_t meters, int Pn, int B, int group, int importance, float alpha,
-                        float ema_alpha, uint32_t seed, uintptr_t st) {
+                        float ema_alpha, uint32_t seed, uintptr_t st, int alias) {
     IsSampleArgs a{P<const float>(losses), P<float>(ema), P<int64_t>(ctrl), P<int>(idx), P<float>(w),
-                   P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed};
+                   P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed, alias};
     is_sample_launch(a, S(st));
     check_launch("is_sample");
   });

@@ -123,13 +123,57 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
     __syncthreads();
   }
   const float total = tsum[IS_T - 1];
+  const int64_t dc = a.ctrl[1];
+  if (a.alias) {
+    // Walker/Vose alias table in LDS (prob in q[], alias[]), then O(1) draws.
+    float* q = tsum + IS_T + 64;                 // [P]
+    int* al = (int*)(q + a.P);                   // [P]
+    int* small = al + a.P;                       // [P]
+    int* large = small + a.P;                    // [P]
+    const float scale = (float)a.P / total;
+    for (int i = tid; i < a.P; i += IS_T) {
+      q[i] = p[i] * scale;
+      al[i] = i;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int ns = 0, nl = 0;
+      for (int i = 0; i < a.P; ++i) {
+        if (q[i] < 1.f) small[ns++] = i;
+        else large[nl++] = i;
+      }
+      while (ns > 0 && nl > 0) {
+        const int s = small[--ns], l = large[--nl];
+        al[s] = l;                               // q[s] stays as prob[s]
+        q[l] = (q[l] + q[s]) - 1.f;
+        if (q[l] < 1.f) small[ns++] = l;
+        else large[nl++] = l;
+      }
+      while (nl > 0) q[large[--nl]] = 1.f;
+      while (ns > 0) q[small[--ns]] = 1.f;       // numerical leftovers
+    }
+    __syncthreads();
+    for (int d = tid; d < a.B; d += IS_T) {
+      const u32x4 r = philox4x32(u32x4{(uint32_t)dc, (uint32_t)(dc >> 32), (uint32_t)d, 0xa11au},
+                                 a.seed, 0x3C6EF372u);
+      const int bin = min((int)(u01(r.x) * (float)a.P), a.P - 1);
+      const int pick = u01(r.y) < q[bin] ? bin : al[bin];
+      a.idx[d] = pick;
+      a.w[d] = a.importance ? p[pick] / total * (float)a.P : 1.f;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      a.ctrl[0] += 1;
+      a.ctrl[1] += 1;
+    }
+    return;
+  }
   float run = tid > 0 ? tsum[tid - 1] : 0.f;
   for (int i = s0; i < s1; ++i) {
     run += p[i];
     p[i] = run;  // unnormalised CDF
   }
   __syncthreads();
-  const int64_t dc = a.ctrl[1];
   for (int d = tid; d < a.B; d += IS_T) {
     const u32x4 r = philox4x32(u32x4{(uint32_t)dc, (uint32_t)(dc >> 32), (uint32_t)d, 0xd1a5u},
                                a.seed, 0x3C6EF372u);
@@ -236,7 +280,7 @@ void pool_build_launch(const PoolBuildArgs& a, hipStream_t st) {
 }
 
 void is_sample_launch(const IsSampleArgs& a, hipStream_t st) {
-  const size_t shm = (size_t)(a.P + IS_T + 64) * sizeof(float);
+  const size_t shm = (size_t)(a.P + IS_T + 64) * sizeof(float) + (a.alias ? 4 * (size_t)a.P * 4 : 0);
   hipLaunchKernelGGL(is_sample_kernel, dim3(1), dim3(IS_T), shm, st, a);
 }
 

@@ -115,6 +115,7 @@ struct IsSampleArgs {
   int P, B, group, importance;   // importance=0 -> uniform draws, w = 1
   float alpha, ema_alpha;
   uint32_t seed;
+  int alias;                     // 1: Walker alias table in LDS + O(1) draws; 0: inverse CDF
 };
 void is_sample_launch(const IsSampleArgs& a, hipStream_t st);
 

@@ -22,6 +22,8 @@ class Config:
     presample_batches: int = 10     # pool = presample_batches * batch_size
     importance: bool = True         # False -> uniform sampling baseline
     global_ema: bool = False        # share the EMA normaliser across ranks (score all-gather)
+    exchange_scores: bool = False   # all-gather pool scores every step (global importance view)
+    sampler: str = 'alias'          # draw kernel: 'alias' (Walker table) | 'cdf' (inverse CDF)
     # data
     dataset: str = 'cifar10'
     data_dir: str = './data/cifar10'

@@ -60,7 +60,8 @@ class NativeEngine(object):
     def __init__(self, net, device, batch_size=32, pool_batches=10, num_classes=None,
                  image_hw=(32, 32), optimizer='adam', lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
                  weight_decay=0.0, momentum=0.9, seed=0, alpha=0.5, ema_alpha=0.9,
-                 importance=True, world_size=1, bucket_bytes=None, use_graphs=True):
+                 importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
+                 sampler='alias', exchange_scores=False):
         ops.lib()
         self.net = net
         self.device = torch.device(device)
@@ -100,6 +101,11 @@ class NativeEngine(object):
         self.graphs = None
         self.shard = None
         self.scoring = True
+        self.sampler = sampler
+        self.score_exchange = None
+        if world_size > 1 and exchange_scores:
+            from ..parallel.scores import ScoreExchange
+            self.score_exchange = ScoreExchange(self.P, self.device)
 
     # ------------------------------------------------------------------ parameters
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
@@ -443,7 +449,8 @@ class NativeEngine(object):
         x = self.forward(sm)
         self.head(sm, x, 'score')
         ops.is_sample(sm.losses, self.ema, self.ctrl, self.idx, self.isw, self.P, self.B, self.B,
-                      self.alpha, self.ema_alpha, self.seed, self.importance, self.meters)
+                      self.alpha, self.ema_alpha, self.seed, self.importance, self.meters,
+                      alias=self.sampler == 'alias')
 
     def gather_batch(self):
         sm, tm = self.score_mode, self.train_mode
@@ -539,6 +546,10 @@ class NativeEngine(object):
                 graphs['score'].replay()
             else:
                 self.score_branch()
+            if self.score_exchange is not None and self.scoring:
+                # cross-worker importance-score all-gather: issued on the score
+                # stream right after scoring, RCCL runs it beside the train backward
+                self.score_exchange.start(self.score_mode.losses)
         ev_score = torch.cuda.Event()
         ev_score.record(self.s_score)
         works = []
@@ -594,6 +605,12 @@ class NativeEngine(object):
         r = self.eval_meters[:3].tolist()
         return r[0] / max(r[1], 1), r[2] / max(r[1], 1), int(r[1])
 
+    def global_share(self):
+        """Each rank's fraction of total pool importance (needs ``exchange_scores``)."""
+        if self.score_exchange is None:
+            return torch.ones(1, device=self.device)
+        return self.score_exchange.global_share()
+
     def read_meters(self):
         b = self.meters.tolist()
         return {'loss_sum': b[0], 'count': b[1], 'correct': b[2], 'pool_mean': b[3], 'ema': b[4]}
@@ -647,7 +664,8 @@ class NativeTrainer(Trainer):
             eps=g.get('eps', 1e-8), weight_decay=g.get('weight_decay', 0.0),
             momentum=g.get('momentum', 0.9), seed=cfg.seed * 1000 + self.rank, alpha=cfg.alpha,
             ema_alpha=cfg.ema_alpha, importance=cfg.importance, world_size=self.world_size,
-            bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs)
+            bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs,
+            sampler=cfg.sampler, exchange_scores=cfg.exchange_scores or cfg.global_ema)
         self.engine.set_shard(x, y)
 
     def average_model(self):

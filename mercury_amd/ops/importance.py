@@ -20,11 +20,14 @@ def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed
 
 
 def is_sample(losses, ema, ctrl, idx, w, P, B, group, alpha=0.5, ema_alpha=0.9, seed=0,
-              importance=True, meters=None):
+              importance=True, meters=None, alias=True):
+    """EMA replay + probabilities + B draws with replacement.  ``alias=True``: Walker alias
+    table built in LDS and O(1) draws; ``alias=False``: inverse-CDF (prefix scan + search)."""
     _chk(losses, torch.float32, 'losses', P)
     _chk(idx, torch.int32, 'idx', B)
     lib().is_sample(ptr(losses), ptr(ema), ptr(ctrl), ptr(idx), ptr(w), ptr(meters), P, B, group,
-                    int(importance), alpha, ema_alpha, int(seed) & 0xffffffff, stream_ptr())
+                    int(importance), alpha, ema_alpha, int(seed) & 0xffffffff, stream_ptr(),
+                    int(alias))
 
 
 def gather(pool, pool_label, pool_index, idx, batch, batch_label, batch_index, B):

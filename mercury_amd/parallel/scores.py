@@ -29,6 +29,9 @@ class ScoreExchange(object):
         self._h = None
 
     def start(self, scores):
+        # order the previous exchange before ``local`` is overwritten (stream-side wait on
+        # nccl, so the host does not block)
+        self.wait()
         self.local.copy_(scores.reshape(-1))
         if self.ws == 1:
             self.gathered[0].copy_(self.local)

@@ -43,13 +43,17 @@ def _bucketed(rank, ws):
     torch.manual_seed(0)
     m = Small()
     flat = FlatParams(m)
-    br = BucketedAllReduce(flat, bucket_bytes=4096).attach()
-    assert len(br.buckets) > 1
     torch.manual_seed(100 + rank)
     x = torch.randn(8, 16)
+    # local gradient first, without hooks: once attached, a bucket's async all-reduce may
+    # already be rewriting flat.grad in place while backward is still running
     flat.zero_grad()
     m(x).pow(2).mean().backward()
     local = flat.grad.clone()
+    br = BucketedAllReduce(flat, bucket_bytes=4096).attach()
+    assert len(br.buckets) > 1
+    flat.zero_grad()
+    m(x).pow(2).mean().backward()
     br.finish()
     ref = local.clone()
     dist.all_reduce(ref)

@@ -288,17 +288,19 @@ def test_pool_build_epoch_permutation_and_normalisation():
     assert torch.isfinite(pool.float()).all()
 
 
-def test_is_sample_ema_and_distribution():
+@pytest.mark.parametrize('alias', [True, False])
+def test_is_sample_ema_and_distribution(alias):
     ops = _ops()
     from mercury_amd.utils import EMAverage
     P, B = 320, 32
     torch.manual_seed(0)
-    losses = torch.rand(P, device=DEV) * 3
+    losses = torch.rand(P, device=DEV) ** 3 * 3      # skewed: many light, few heavy bins
     ema = torch.zeros(2, device=DEV)
     ctrl = torch.zeros(4, dtype=torch.int64, device=DEV)
     idx = torch.empty(B, dtype=torch.int32, device=DEV)
     w = torch.empty(B, device=DEV)
-    ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1)
+    ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1,
+                  alias=alias)
     ref = EMAverage()
     for j in range(10):
         ref.update(losses[:32 * (j + 1)].mean().item())
@@ -309,7 +311,8 @@ def test_is_sample_ema_and_distribution():
     counts = torch.zeros(P, device=DEV)
     n = 0
     for _ in range(600):
-        ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1)
+        ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1,
+                      alias=alias)
         counts.index_add_(0, idx.long(), torch.ones(B, device=DEV))
         n += B
     p = (losses + 0.5 * ema[0]) / (losses + 0.5 * ema[0]).sum()

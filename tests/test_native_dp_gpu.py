@@ -27,7 +27,8 @@ def _dp_worker(rank, ws):
     shard = dirichlet_partition(y, ws, 0.5, 10)[rank]
     torch.manual_seed(100 + rank)             # different init per rank
     net = ResNet18(10).cuda()
-    eng = NativeEngine(net, 'cuda', 32, 10, world_size=ws, bucket_bytes=4 << 20, seed=rank)
+    eng = NativeEngine(net, 'cuda', 32, 10, world_size=ws, bucket_bytes=4 << 20, seed=rank,
+                       exchange_scores=True)
     assert len(eng.bucket_plan()) > 1
     eng.set_shard(x[shard], y[shard])
     eng.broadcast_from(0)
@@ -43,6 +44,12 @@ def _dp_worker(rank, ws):
     assert torch.equal(gathered[0], gathered[1]), float((gathered[0] - gathered[1]).abs().max())
     m = eng.read_meters()
     assert np.isfinite(m['loss_sum'])
+    # cross-worker score exchange: row r of the gathered matrix is rank r's pool scores
+    g = eng.score_exchange.wait()
+    torch.cuda.synchronize()
+    assert torch.equal(g[rank], eng.score_mode.losses.reshape(-1))
+    share = eng.global_share()
+    assert abs(float(share.sum()) - 1.0) < 1e-5
 
 
 def test_native_dp_two_ranks_gloo_same_gpu():
