@@ -106,10 +106,11 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("head_fwd", [](uintptr_t act, uintptr_t w, uintptr_t b, uintptr_t label, uintptr_t isw,
                        uintptr_t pooled, uintptr_t logits, uintptr_t dlogits, uintptr_t losses,
-                       uintptr_t meters, int B, int HW, int C, int classes, int mode, uintptr_t st) {
+                       uintptr_t meters, int B, int HW, int C, int classes, int mode, uintptr_t st,
+                       int score_kind) {
     HeadArgs a{P<const bf16>(act), P<const float>(w), P<const float>(b), P<const int>(label),
                P<const float>(isw), P<float>(pooled), P<float>(logits), P<float>(dlogits),
-               P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0};
+               P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0, score_kind};
     head_fwd_launch(a, S(st));
     check_launch("head_fwd");
   });
@@ -134,9 +135,13 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("is_sample", [](uintptr_t losses, uintptr_t ema, uintptr_t ctrl, uintptr_t idx, uintptr_t w,
                         uintptr_t meters, int Pn, int B, int group, int importance, float alpha,
-                        float ema_alpha, uint32_t seed, uintptr_t st, int alias) {
+                        float ema_alpha, uint32_t seed, uintptr_t st, int alias, uintptr_t gl,
+                        int W) {
+    if (group <= 0 || Pn % group || Pn / group > 256)
+      throw std::runtime_error("is_sample: pool must be 1..256 groups of `group` samples");
     IsSampleArgs a{P<const float>(losses), P<float>(ema), P<int64_t>(ctrl), P<int>(idx), P<float>(w),
-                   P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed, alias};
+                   P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed, alias,
+                   P<const float>(gl), W};
     is_sample_launch(a, S(st));
     check_launch("is_sample");
   });
@@ -149,15 +154,22 @@ PYBIND11_MODULE(_C, m) {
     gather_launch(a, S(st));
     check_launch("gather");
   });
-  m.def("table_write", [](uintptr_t imp, uintptr_t grp, uintptr_t losses, int start, int n,
-                          int64_t gi, uintptr_t st) {
-    table_write_launch(P<float>(imp), P<int64_t>(grp), P<const float>(losses), start, n, gi, S(st));
-    check_launch("table_write");
+  m.def("table_num_segments", &table_num_segments);
+  m.def("table_scalars_bytes", []() { return (int)sizeof(TableScalars); });
+  m.def("table_scatter", [](uintptr_t imp, uintptr_t grp, uintptr_t losses, uintptr_t index,
+                            uintptr_t stamp, int start, int n, int N, int gi, uintptr_t st) {
+    TableScatterArgs a{P<float>(imp), P<int>(grp), P<const float>(losses), P<const int>(index),
+                       P<const int64_t>(stamp), start, n, N, gi};
+    table_scatter_launch(a, S(st));
+    check_launch("table_scatter");
   });
-  m.def("table_sample", [](uintptr_t imp, uintptr_t grp, int N, int64_t gi, int ndraw, uint32_t seed,
-                           uint64_t counter, uintptr_t out, uintptr_t st) {
-    table_sample_launch(P<const float>(imp), P<const int64_t>(grp), N, gi, ndraw, seed, counter,
-                        P<int64_t>(out), S(st));
+  m.def("table_sample", [](uintptr_t imp, uintptr_t grp, int N, int gi, uintptr_t gi_dev,
+                           uintptr_t part, uintptr_t prefix, uintptr_t sc, uintptr_t counter,
+                           int ndraw, uint32_t seed, uintptr_t out, uintptr_t out32, uintptr_t st) {
+    TableSampleArgs a{P<const float>(imp), P<const int>(grp), N, gi, P<const int64_t>(gi_dev),
+                      P<float2>(part), P<double>(prefix), P<TableScalars>(sc), P<int64_t>(counter),
+                      ndraw, seed, P<int64_t>(out), P<int>(out32)};
+    table_sample_launch(a, S(st));
     check_launch("table_sample");
   });
 

@@ -67,8 +67,20 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
     const float lse = mx + __logf(se);
     const int y = a.label[b];
     const float loss = lse - logit[y];
+    float score = loss;
+    if (a.score_kind == 1) {
+      // exact per-sample gradient norm of the classifier layer: d(loss)/d[W|b] is the outer
+      // product of dz = softmax - onehot with [h, 1], so its Frobenius norm factorises
+      float g2 = 0.f, h2 = 0.f;
+      for (int k = lane; k < a.classes; k += 64) {
+        const float d = __expf(logit[k] - lse) - (k == y ? 1.f : 0.f);
+        g2 += d * d;
+      }
+      for (int c = lane; c < a.C; c += 64) h2 += pooled[c] * pooled[c];
+      score = sqrtf(wave_sum(g2) * (wave_sum(h2) + 1.f));
+    }
     if (lane == 0) {
-      if (a.losses) a.losses[b] = loss;
+      if (a.losses) a.losses[b] = score;
       red[0] = lse;
       const float wi = a.isw ? a.isw[b] : 1.f;
       if (a.mode == 1 || a.mode == 2) {

@@ -11,9 +11,7 @@
 //               replacement (block-wide LDS prefix scan + binary search, Philox
 //               uniforms), importance weights N*p[idx].
 // gather      : the drawn samples' exact augmented views -> the next training batch.
-// table_*     : Groupwise_Sampler's global importance table kept in HBM: scatter of
-//               scored slices, and masked-normalise + weighted draws over the current
-//               group without a host round trip (`util.py:132-152`).
+// (the global importance table of Groupwise_Sampler lives in table.hip)
 #include "common.h"
 #include "kernels.h"
 
@@ -67,6 +65,7 @@ __global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
 }
 
 constexpr int IS_T = 1024;
+constexpr int MAX_GROUPS = 256;   // pool batches per pool
 
 __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -77,16 +76,29 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
   const int G = a.P / a.group;
   for (int i = tid; i < a.P; i += IS_T) p[i] = a.losses[i];
   __syncthreads();
-  // group sums -> cumulative means -> EMA replay (10 updates for the reference pool)
+  // group sums (over this rank's pool, or over every rank's pool when the gathered W x P
+  // score matrix is given -- the global-EMA mode) -> cumulative means -> EMA replay
+  // (10 updates for the reference pool)
+  __shared__ float gsum[MAX_GROUPS];
+  const float* src = a.gl ? a.gl : a.losses;
+  const int rows = a.gl ? a.W : 1;
+  for (int i = tid; i < G; i += IS_T) gsum[i] = 0.f;
+  __syncthreads();
+  for (int pr = tid; pr < rows * G; pr += IS_T) {
+    const int r = pr / G, gi = pr - r * G;
+    const float* q = src + (size_t)r * a.P + gi * a.group;
+    float s = 0.f;
+    for (int k = 0; k < a.group; ++k) s += q[k];
+    atomicAdd(&gsum[gi], s);
+  }
+  __syncthreads();
   if (tid == 0) {
     float ema = a.ema[0];
     bool init = a.ema[1] != 0.f;
     double cs = 0.0;
     for (int gi = 0; gi < G; ++gi) {
-      float s = 0.f;
-      for (int k = 0; k < a.group; ++k) s += p[gi * a.group + k];
-      cs += s;
-      const float m = (float)(cs / (double)((gi + 1) * a.group));
+      cs += gsum[gi];
+      const float m = (float)(cs / (double)((gi + 1) * a.group * rows));
       if (!init) {
         ema = m;
         init = true;
@@ -97,7 +109,7 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
     a.ema[0] = ema;
     a.ema[1] = 1.f;
     red[32] = ema;
-    red[33] = (float)(cs / (double)a.P);
+    red[33] = (float)(cs / (double)(a.P * rows));
     if (a.meters) {
       a.meters[3] = red[33];
       a.meters[4] = ema;
@@ -209,70 +221,6 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
   }
 }
 
-__global__ void table_write_kernel(float* imp, int64_t* grp, const float* losses, int start, int n,
-                                   int64_t gi) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    imp[start + i] = losses[i];
-    grp[start + i] = gi;
-  }
-}
-
-__global__ __launch_bounds__(1024) void table_sample_kernel(const float* imp, const int64_t* grp,
-                                                           int N, int64_t gi, int ndraw,
-                                                           uint32_t seed, uint64_t counter,
-                                                           int64_t* out) {
-  __shared__ float tsum[1024];
-  __shared__ float red[32];
-  const int tid = threadIdx.x;
-  const int seg = (N + 1023) / 1024;
-  const int s0 = min(N, tid * seg), s1 = min(N, s0 + seg);
-  float s = 0.f, cnt = 0.f;
-  for (int i = s0; i < s1; ++i)
-    if (grp[i] == gi) {
-      s += imp[i];
-      cnt += 1.f;
-    }
-  const float tot_imp = block_sum(s, red);
-  const float tot_cnt = block_sum(cnt, red);
-  const float mean = tot_cnt > 0.f ? tot_imp / tot_cnt : 0.f;
-  float local = 0.f;
-  for (int i = s0; i < s1; ++i)
-    if (grp[i] == gi) local += imp[i] + mean;  // w = imp + mean(imp), alpha = 1 (`util.py:146-148`)
-  tsum[tid] = local;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const float add = tid >= off ? tsum[tid - off] : 0.f;
-    __syncthreads();
-    tsum[tid] += add;
-    __syncthreads();
-  }
-  const float total = tsum[1023];
-  for (int d = tid; d < ndraw; d += 1024) {
-    const u32x4 r = philox4x32(u32x4{(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)d, 7u},
-                               seed, 0x1B873593u);
-    const float u = u01(r.x) * total;
-    int lo = 0, hi = 1023;  // thread segment whose inclusive sum exceeds u
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (tsum[mid] > u) hi = mid;
-      else lo = mid + 1;
-    }
-    float run = lo > 0 ? tsum[lo - 1] : 0.f;
-    const int a0 = min(N, lo * seg), a1 = min(N, a0 + seg);
-    int64_t pick = -1, last = -1;
-    for (int i = a0; i < a1; ++i) {
-      if (grp[i] != gi) continue;
-      last = i;
-      run += imp[i] + mean;
-      if (run > u) {
-        pick = i;
-        break;
-      }
-    }
-    out[d] = pick >= 0 ? pick : last;
-  }
-}
 }  // namespace
 
 void pool_build_launch(const PoolBuildArgs& a, hipStream_t st) {
@@ -286,17 +234,4 @@ void is_sample_launch(const IsSampleArgs& a, hipStream_t st) {
 
 void gather_launch(const GatherArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(gather_kernel, dim3((a.chunks_per_img + 255) / 256, a.B), dim3(256), 0, st, a);
-}
-
-void table_write_launch(float* importance, int64_t* group, const float* losses, int start, int n,
-                        int64_t group_index, hipStream_t st) {
-  hipLaunchKernelGGL(table_write_kernel, dim3((n + 255) / 256), dim3(256), 0, st, importance, group,
-                     losses, start, n, group_index);
-}
-
-void table_sample_launch(const float* importance, const int64_t* group, int N, int64_t group_index,
-                         int ndraw, uint32_t seed, uint64_t counter, int64_t* out,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(table_sample_kernel, dim3(1), dim3(1024), 0, st, importance, group, N,
-                     group_index, ndraw, seed, counter, out);
 }

@@ -77,6 +77,7 @@ struct HeadArgs {
   float* meters;                 // [0]+=sum(w-loss)*... see head.hip
   int B, HW, C, classes, mode;   // mode 0 score, 1 train, 2 eval
   int log_softmax_input;         // logits are already log-probs (VGG) -> NLL
+  int score_kind;                // losses[] holds 0: CE loss, 1: classifier-layer grad norm
 };
 void head_fwd_launch(const HeadArgs& a, hipStream_t st);
 
@@ -116,6 +117,8 @@ struct IsSampleArgs {
   float alpha, ema_alpha;
   uint32_t seed;
   int alias;                     // 1: Walker alias table in LDS + O(1) draws; 0: inverse CDF
+  const float* gl;               // [W][P] all ranks' pool scores (global EMA) or null
+  int W;
 };
 void is_sample_launch(const IsSampleArgs& a, hipStream_t st);
 
@@ -131,12 +134,38 @@ struct GatherArgs {
 };
 void gather_launch(const GatherArgs& a, hipStream_t st);
 
-// global importance table (Groupwise sampler, K11)
-void table_write_launch(float* importance, int64_t* group, const float* losses, int start, int n,
-                        int64_t group_index, hipStream_t st);
-void table_sample_launch(const float* importance, const int64_t* group, int N, int64_t group_index,
-                         int ndraw, uint32_t seed, uint64_t counter, int64_t* out,
-                         hipStream_t st);
+// global importance table in HBM (Groupwise sampler, K2/K11) -- csrc/table.hip
+struct TableScatterArgs {
+  float* imp;                    // [N] importance
+  int* grp;                      // [N] group stamp
+  const float* losses;           // [n]
+  const int* index;              // [n] table positions, or null -> start + i
+  const int64_t* stamp;          // device group id (graph-replay safe) or null -> gi
+  int start, n, N, gi;
+};
+void table_scatter_launch(const TableScatterArgs& a, hipStream_t st);
+
+struct TableScalars {
+  float mean, count;             // group mean importance, member count
+  double total;                  // sum of w = imp + mean over members
+  int64_t counter;               // draw-counter snapshot used by this batch of draws
+};
+struct TableSampleArgs {
+  const float* imp;
+  const int* grp;
+  int N, gi;
+  const int64_t* gi_dev;         // device group id or null -> gi
+  float2* part;                  // workspace [table_num_segments(N)]
+  double* prefix;                // workspace [table_num_segments(N) + 1]
+  TableScalars* sc;              // workspace / result scalars
+  int64_t* counter;              // device draw counter (bumped once per launch) or null
+  int ndraw;
+  uint32_t seed;
+  int64_t* out;                  // [ndraw] drawn table positions (int64) or null
+  int* out32;                    // [ndraw] same as int32 or null
+};
+int table_num_segments(int N);
+void table_sample_launch(const TableSampleArgs& a, hipStream_t st);
 
 // ------------------------------------------------------------------ optimizer
 struct OptSeg {

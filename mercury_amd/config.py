@@ -23,6 +23,8 @@ class Config:
     importance: bool = True         # False -> uniform sampling baseline
     global_ema: bool = False        # share the EMA normaliser across ranks (score all-gather)
     exchange_scores: bool = False   # all-gather pool scores every step (global importance view)
+    score: str = 'loss'             # importance score: 'loss' (reference) | 'gradnorm' (per-sample
+                                    # classifier-layer gradient norm)
     sampler: str = 'alias'          # draw kernel: 'alias' (Walker table) | 'cdf' (inverse CDF)
     # data
     dataset: str = 'cifar10'

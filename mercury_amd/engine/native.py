@@ -61,7 +61,8 @@ class NativeEngine(object):
                  image_hw=(32, 32), optimizer='adam', lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
                  weight_decay=0.0, momentum=0.9, seed=0, alpha=0.5, ema_alpha=0.9,
                  importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
-                 sampler='alias', exchange_scores=False):
+                 sampler='alias', exchange_scores=False, global_table=True, score='loss',
+                 global_ema=False):
         ops.lib()
         self.net = net
         self.device = torch.device(device)
@@ -102,8 +103,14 @@ class NativeEngine(object):
         self.shard = None
         self.scoring = True
         self.sampler = sampler
+        if score not in ('loss', 'gradnorm'):
+            raise ValueError('score must be loss or gradnorm')
+        self.score = score
+        self.global_table = global_table
+        self.table = None
         self.score_exchange = None
-        if world_size > 1 and exchange_scores:
+        self.global_ema = global_ema
+        if world_size > 1 and (exchange_scores or global_ema):
             from ..parallel.scores import ScoreExchange
             self.score_exchange = ScoreExchange(self.P, self.device)
 
@@ -328,7 +335,8 @@ class NativeEngine(object):
         ops.head_fwd(x, self._pview(self.lw.fc_w), self._pview(self.lw.fc_b), m.label, m.N,
                      m.final_hw, m.final_C, self.classes, mode, pooled=m.pooled,
                      dlogits=getattr(m, 'dlogits', None) if mode == 'train' else None,
-                     losses=m.losses, isw=isw, meters=meters)
+                     losses=m.losses, isw=isw, meters=meters,
+                     score=self.score if mode == 'score' else 'loss')
 
     def _wgrad(self, m, u, dy, x):
         sp = m.spec[u.name]
@@ -419,6 +427,10 @@ class NativeEngine(object):
         self.idx = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._arange_b = torch.arange(self.B, dtype=torch.int32, device=self.device)
         self.isw = torch.ones(self.B, dtype=torch.float32, device=self.device)
+        if self.global_table:
+            # shard-wide importance table resident in HBM: every scored pool sample's latest
+            # loss, stamped with the optimizer step that scored it
+            self.table = ops.ImportanceTable(self.shard.shape[0], self.device)
         self._build_bn_table()
 
     def _build_bn_table(self):
@@ -433,6 +445,11 @@ class NativeEngine(object):
 
     # ------------------------------------------------------------------ step pieces
     def score_branch(self):
+        self.score_forward()
+        if not self._split_score:
+            self.score_sample()
+
+    def score_forward(self):
         sm = self.score_mode
         if not self.scoring:
             # uniform-sampling baseline: the next batch is the next 32 shard samples
@@ -448,9 +465,40 @@ class NativeEngine(object):
                        self.P, self.B, self.seed)
         x = self.forward(sm)
         self.head(sm, x, 'score')
+        if self.table is not None:
+            self.table.scatter(sm.index, sm.losses, stamp=self.ctrl[2:3])
+
+    def score_sample(self):
+        if not self.scoring:
+            return
+        sm = self.score_mode
+        gathered = self.score_exchange.gathered if self._split_score else None
         ops.is_sample(sm.losses, self.ema, self.ctrl, self.idx, self.isw, self.P, self.B, self.B,
                       self.alpha, self.ema_alpha, self.seed, self.importance, self.meters,
-                      alias=self.sampler == 'alias')
+                      alias=self.sampler == 'alias', gathered=gathered)
+
+    @property
+    def _split_score(self):
+        # global EMA: the all-gather of every rank's pool scores sits between the scoring
+        # forward and the draw, so the score stream runs as two graphs around the collective
+        return self.global_ema and self.score_exchange is not None and self.scoring
+
+    def _score_stream_work(self, graphs):
+        """Everything on the score stream for one step (caller sets the stream)."""
+        if graphs:
+            graphs['score'].replay()
+        else:
+            self.score_forward() if self._split_score else self.score_branch()
+        if self.score_exchange is not None and self.scoring:
+            # cross-worker importance-score all-gather (SURVEY X6), issued on the score stream
+            # right after scoring; RCCL runs it beside the train backward
+            self.score_exchange.start(self.score_mode.losses)
+        if self._split_score:
+            self.score_exchange.wait()          # stream-side wait on RCCL
+            if graphs:
+                graphs['score_sample'].replay()
+            else:
+                self.score_sample()
 
     def gather_batch(self):
         sm, tm = self.score_mode, self.train_mode
@@ -519,10 +567,13 @@ class NativeEngine(object):
         cap = torch.cuda.Stream(self.device)
         segs = self.train_segments()
         self.graphs = {
-            'score': self._capture(self.score_branch, cap),
+            'score': self._capture(self.score_forward if self._split_score else self.score_branch,
+                                   cap),
             'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b) for fs, b in segs],
             'tail': self._capture(self.tail, cap),
         }
+        if self._split_score:
+            self.graphs['score_sample'] = self._capture(self.score_sample, cap)
         torch.cuda.synchronize(self.device)
 
     def prime(self):
@@ -530,7 +581,7 @@ class NativeEngine(object):
         s0 = torch.cuda.current_stream(self.device)
         self.s_score.wait_stream(s0)
         with torch.cuda.stream(self.s_score):
-            self.score_branch()
+            self._score_stream_work(None)
         s0.wait_stream(self.s_score)
         self.gather_batch()
 
@@ -542,14 +593,7 @@ class NativeEngine(object):
         self.s_score.wait_event(ev_start)
         graphs = self.graphs if self.use_graphs else None
         with torch.cuda.stream(self.s_score):
-            if graphs:
-                graphs['score'].replay()
-            else:
-                self.score_branch()
-            if self.score_exchange is not None and self.scoring:
-                # cross-worker importance-score all-gather: issued on the score
-                # stream right after scoring, RCCL runs it beside the train backward
-                self.score_exchange.start(self.score_mode.losses)
+            self._score_stream_work(graphs)
         ev_score = torch.cuda.Event()
         ev_score.record(self.s_score)
         works = []
@@ -655,6 +699,9 @@ class NativeTrainer(Trainer):
         self.bucketer = None
         from ..utils.logging import PhaseTimer
         self.timer = PhaseTimer(self.device)
+        # the engine's fused kernel performs the optimizer step; tell the LR scheduler so it
+        # does not warn that optimizer.step() was never called
+        optimizer._opt_called = True
         g = optimizer.param_groups[0]
         algo = 'adam' if isinstance(optimizer, torch.optim.Adam) else 'sgd'
         x, y = _dataset_arrays(presam_loader)
@@ -665,7 +712,8 @@ class NativeTrainer(Trainer):
             momentum=g.get('momentum', 0.9), seed=cfg.seed * 1000 + self.rank, alpha=cfg.alpha,
             ema_alpha=cfg.ema_alpha, importance=cfg.importance, world_size=self.world_size,
             bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs,
-            sampler=cfg.sampler, exchange_scores=cfg.exchange_scores or cfg.global_ema)
+            sampler=cfg.sampler, exchange_scores=cfg.exchange_scores,
+            score=cfg.score, global_ema=cfg.global_ema)
         self.engine.set_shard(x, y)
 
     def average_model(self):
@@ -784,7 +832,16 @@ class NativeTrainer(Trainer):
                 'optimizer': ost,
                 'scheduler': self.scheduler.state_dict() if self.scheduler else None,
                 'step': self.step, 'epoch': self.epoch,
-                'engine': {'ctrl': e.ctrl.cpu(), 'ema': e.ema.cpu()}}
+                'engine': self._engine_state()}
+
+    def _engine_state(self):
+        e = self.engine
+        out = {'ctrl': e.ctrl.cpu(), 'ema': e.ema.cpu()}
+        if e.table is not None:
+            # shard importance table with the Groupwise_Sampler field names (`util.py:106-107`)
+            out['importance'] = e.table.importance.cpu()
+            out['group_indicator'] = e.table.group.cpu().to(torch.int64)
+        return out
 
     def load_state_dict(self, sd):
         e = self.engine
@@ -806,6 +863,9 @@ class NativeTrainer(Trainer):
         if 'engine' in sd:
             e.ctrl.copy_(sd['engine']['ctrl'].to(e.device))
             e.ema.copy_(sd['engine']['ema'].to(e.device))
+            if e.table is not None and 'importance' in sd['engine']:
+                e.table.importance.copy_(sd['engine']['importance'].to(e.device))
+                e.table.group.copy_(sd['engine']['group_indicator'].to(e.device, torch.int32))
 
 
 # ---------------------------------------------------------------------- smoke

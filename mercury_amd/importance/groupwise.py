@@ -13,9 +13,12 @@ per-group weight is ``imp + mean(imp)`` (alpha = 1 smoothing).
 
 Fixes: ``__len__`` works (reference references an undefined ``num_samples``),
 scoring runs under ``no_grad``, and the table can live on the GPU
-(``device='cuda'``) where the MI355X path keeps it resident in HBM and the
-per-draw work (masked normalise + weighted draw) runs as one fused HIP
-kernel (``mercury_amd.ops.table_sample``) instead of a numpy round trip.
+(``device='cuda'``) where the MI355X path keeps it resident in HBM
+(``mercury_amd.ops.ImportanceTable``, ``csrc/table.hip``): writes are a scatter
+kernel and a batch of draws is three launches (segment partials, fp64 segment
+scan, one wave per draw) instead of an O(N) numpy normalise per draw.  On the
+GPU ``__iter__`` draws ``prefetch`` indices per launch; ``prefetch=1`` keeps the
+reference's "updates apply to the very next draw" semantics.
 """
 from __future__ import annotations
 
@@ -27,13 +30,22 @@ from torch.utils.data import Sampler
 
 class Groupwise_Sampler(Sampler):
 
-    def __init__(self, dataset, replacement=True, num_samples=None, device='cpu'):
+    def __init__(self, dataset, replacement=True, num_samples=None, device='cpu', seed=0,
+                 prefetch=1):
         self.dataset = dataset
         self.replacement = replacement
         self.device = torch.device(device)
+        self.seed = int(seed)
+        self.prefetch = max(1, int(prefetch))
         n = len(dataset)
-        self.group_indicator = torch.zeros(n, dtype=torch.int64, device=self.device)
-        self.importance = torch.ones(n, dtype=torch.float32, device=self.device)
+        self.table = None
+        if self.device.type == 'cuda':
+            from ..ops.table import ImportanceTable
+            self.table = ImportanceTable(n, self.device)
+            self.importance, self.group_indicator = self.table.importance, self.table.group
+        else:
+            self.group_indicator = torch.zeros(n, dtype=torch.int64, device=self.device)
+            self.importance = torch.ones(n, dtype=torch.float32, device=self.device)
         self.cur_sample_index = 0
         self.group_index = 0
         self.last_update_iteration = -1
@@ -61,6 +73,9 @@ class Groupwise_Sampler(Sampler):
         return start, end
 
     def write_scores(self, start, end, losses):
+        if self.table is not None:
+            self.table.write(start, torch.as_tensor(losses)[:end - start], self.group_index)
+            return
         self.importance[start:end] = torch.as_tensor(losses).detach().to(
             self.importance.device, torch.float32).reshape(-1)[:end - start]
         self.group_indicator[start:end] = self.group_index
@@ -75,9 +90,23 @@ class Groupwise_Sampler(Sampler):
         w = imp + imp.mean()
         return members, w / w.sum()
 
+    def sample(self, n):
+        """``n`` draws at once from the current group (device tensor on the GPU path)."""
+        if self.table is not None:
+            return self.table.sample(n, self.group_index, self.seed)
+        members, p = self.group_distribution()
+        return members[torch.multinomial(p.cpu(), n, True)]
+
     def __iter__(self):
         counter = 0
         n = self.num_samples
+        if self.table is not None:
+            while counter < n:
+                k = min(self.prefetch, n - counter)
+                for j in self.table.sample(k, self.group_index, self.seed).tolist():
+                    yield int(j)
+                counter += k
+            return
         while True:
             members, p = self.group_distribution()
             j = torch.multinomial(p.cpu(), 1, self.replacement).item()
@@ -98,10 +127,14 @@ class Groupwise_Sampler(Sampler):
                 'last_update_iteration': self.last_update_iteration}
 
     def load_state_dict(self, sd):
-        self.importance = torch.as_tensor(np.asarray(sd['importance']), dtype=torch.float32,
-                                          device=self.device)
-        self.group_indicator = torch.as_tensor(np.asarray(sd['group_indicator']),
-                                               dtype=torch.int64, device=self.device)
+        imp = torch.as_tensor(np.asarray(sd['importance']), dtype=torch.float32)
+        grp = torch.as_tensor(np.asarray(sd['group_indicator'])).to(torch.int64)
+        if self.table is not None:
+            self.table.importance.copy_(imp)
+            self.table.group.copy_(grp.to(torch.int32))
+        else:
+            self.importance = imp.to(self.device)
+            self.group_indicator = grp.to(self.device)
         self.cur_sample_index = int(sd['cur_sample_index'])
         self.group_index = int(sd['group_index'])
         self.last_update_iteration = int(sd['last_update_iteration'])

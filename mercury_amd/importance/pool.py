@@ -32,6 +32,27 @@ def cumulative_means(losses, group):
     return (csum[ends - 1] / ends.double()).to(losses.dtype)
 
 
+def global_cumulative_means(gathered, group):
+    """Cumulative pool means over every rank's pool: ``gathered`` is [W][P] (the score
+    all-gather); the mean after batch ``j`` covers the first ``group*(j+1)`` samples of
+    all W pools (the global-EMA mode; the fused kernel does the same on device)."""
+    W, n = gathered.shape
+    gs = gathered.double().reshape(W, n // group, group).sum((0, 2))
+    ends = torch.arange(1, n // group + 1, device=gathered.device, dtype=torch.float64)
+    return (torch.cumsum(gs, 0) / (ends * group * W)).to(gathered.dtype)
+
+
+def classifier_gradnorm(logits, labels, feats):
+    """Exact per-sample gradient norm of the classifier layer ``z = W h + b`` under CE:
+    ``||softmax(z) - onehot(y)|| * sqrt(||h||^2 + 1)`` (an importance score that upper-bounds
+    the full gradient norm up to a constant; Katharopoulos & Fleuret 2018).  Works for
+    log-softmax outputs too (softmax is shift invariant)."""
+    d = torch.softmax(logits.float(), 1)
+    d[torch.arange(d.shape[0], device=d.device), labels] -= 1.0
+    h2 = feats.float().reshape(feats.shape[0], -1).pow(2).sum(1)
+    return d.norm(dim=1) * torch.sqrt(h2 + 1.0)
+
+
 def ema_replay(ema, means):
     """Apply ``EMAverage.update`` for each cumulative mean in order (`util.py:207-213`).
 

@@ -20,29 +20,19 @@ def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed
 
 
 def is_sample(losses, ema, ctrl, idx, w, P, B, group, alpha=0.5, ema_alpha=0.9, seed=0,
-              importance=True, meters=None, alias=True):
+              importance=True, meters=None, alias=True, gathered=None):
     """EMA replay + probabilities + B draws with replacement.  ``alias=True``: Walker alias
-    table built in LDS and O(1) draws; ``alias=False``: inverse-CDF (prefix scan + search)."""
+    table built in LDS and O(1) draws; ``alias=False``: inverse-CDF (prefix scan + search).
+    ``gathered`` ([W][P] every rank's scores): the EMA is replayed over the global pool means
+    (shared normaliser across ranks) while the draw still uses this rank's ``losses``."""
     _chk(losses, torch.float32, 'losses', P)
     _chk(idx, torch.int32, 'idx', B)
     lib().is_sample(ptr(losses), ptr(ema), ptr(ctrl), ptr(idx), ptr(w), ptr(meters), P, B, group,
                     int(importance), alpha, ema_alpha, int(seed) & 0xffffffff, stream_ptr(),
-                    int(alias))
+                    int(alias), ptr(gathered), gathered.shape[0] if gathered is not None else 1)
 
 
 def gather(pool, pool_label, pool_index, idx, batch, batch_label, batch_index, B):
     per_img = pool[0].numel() * 2 // 16
     lib().gather(ptr(pool), ptr(pool_label), ptr(pool_index), ptr(idx), ptr(batch),
                  ptr(batch_label), ptr(batch_index), B, per_img, stream_ptr())
-
-
-def table_write(importance, group, losses, start, group_index):
-    n = losses.numel()
-    lib().table_write(ptr(importance), ptr(group), ptr(losses.float().contiguous()), start, n,
-                      int(group_index), stream_ptr())
-
-
-def table_sample(importance, group, group_index, ndraw, seed, counter, out):
-    lib().table_sample(ptr(importance), ptr(group), importance.numel(), int(group_index), ndraw,
-                       int(seed) & 0xffffffff, int(counter), ptr(out), stream_ptr())
-    return out

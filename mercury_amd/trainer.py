@@ -67,6 +67,25 @@ class Trainer(object):
         self.flat = None
         self.bucketer = None
         self._setup_flat()
+        self._fc_in = None
+        if self.cfg.score == 'gradnorm':
+            fcs = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+            if not fcs:
+                raise ValueError("score='gradnorm' needs a final nn.Linear classifier")
+            fcs[-1].register_forward_pre_hook(self._keep_fc_input)
+        self.score_exchange = None
+        if self.world_size > 1 and (self.cfg.global_ema or self.cfg.exchange_scores):
+            from .parallel.scores import ScoreExchange
+            self.score_exchange = ScoreExchange(self.cfg.pool_size(), self.device)
+
+    def _keep_fc_input(self, _mod, inp):
+        self._fc_in = inp[0].detach()
+
+    def _score(self, output, label):
+        """Per-sample importance score of a scored batch (`pytorch_collab.py:102`)."""
+        if self.cfg.score == 'gradnorm':
+            return ispool.classifier_gradnorm(output, label, self._fc_in)
+        return F.cross_entropy(output.float(), label, reduction='none')
 
     # ------------------------------------------------------------------ DP plumbing
     def _setup_flat(self):
@@ -129,14 +148,22 @@ class Trainer(object):
                 data = data.to(self.device, non_blocking=True)
                 label = torch.as_tensor(label).to(self.device, non_blocking=True)
                 output = self.net(data)  # train mode: BN batch stats, as the reference
-                losses.append(F.cross_entropy(output.float(), label, reduction='none'))
+                losses.append(self._score(output, label))
                 labels.append(label)
                 datas.append(data)
                 index.append(torch.as_tensor(idx))
-                # EMA updated with the running pool mean after each batch
-                ema_loss.update(torch.cat(losses).mean())
+                if not self._global_ema():
+                    # EMA updated with the running pool mean after each batch
+                    ema_loss.update(torch.cat(losses).mean())
         pool_losses = torch.cat(losses)
         pool_mean = pool_losses.mean()
+        if self.score_exchange is not None and cnt == self.cfg.presample_batches:
+            self.score_exchange.start(pool_losses.float())
+            if self._global_ema():
+                # one normaliser for every rank: the replay runs over the global pool means
+                g = self.score_exchange.wait()
+                ispool.ema_replay(ema_loss, ispool.global_cumulative_means(g, self.batch_size))
+                pool_mean = g.mean()
         if self.cfg.importance:
             probs = ispool.importance_probs(pool_losses, ema_loss.value, alpha)
         else:
@@ -145,6 +172,9 @@ class Trainer(object):
         weights = ispool.is_weights(probs, important_idx)
         return (weights, torch.cat(datas)[important_idx], torch.cat(labels)[important_idx],
                 torch.cat(index)[important_idx.cpu()], pool_mean)
+
+    def _global_ema(self):
+        return self.cfg.global_ema and self.score_exchange is not None
 
     # ------------------------------------------------------------------ loop
     def train_step(self, probs, i_data, i_label, ema, running_loss, running_acc):

@@ -89,3 +89,27 @@ def _trainer_dp(rank, ws):
 
 def test_trainer_dp_replicas_identical():
     spawn(_trainer_dp, 2)
+
+
+def _global_ema(rank, ws):
+    from mercury_amd.config import Config
+    from mercury_amd.trainer import Trainer
+    from mercury_amd.utils import EMAverage
+    from test_importance import FakeLoader, TinyNet
+    torch.manual_seed(0)
+    net = TinyNet()
+    cfg = Config(print_every=0, eval_every=0, global_ema=True, score='gradnorm')
+    t = Trainer(net, torch.optim.Adam(net.parameters(), lr=1e-3), FakeLoader(n=4),
+                FakeLoader(n=12, seed=rank), None, 'cpu', cfg)
+    ema = EMAverage()
+    w, d, lab, idx, pm = t.update_samples(ema)
+    assert w.shape == (32,) and torch.isfinite(w).all()
+    vals = [torch.zeros(1) for _ in range(ws)]
+    dist.all_gather(vals, torch.tensor([float(ema.value)]))
+    assert vals[0].item() == vals[1].item(), 'global EMA must agree across ranks'
+    g = t.score_exchange.wait()
+    assert g.shape == (ws, 320) and abs(float(pm) - float(g.mean())) < 1e-6
+
+
+def test_trainer_global_ema_gradnorm_two_ranks():
+    spawn(_global_ema, 2)

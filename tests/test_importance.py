@@ -140,3 +140,24 @@ def test_groupwise_lifecycle_matches_reference():
     assert set(draws) <= set(members.tolist())
     assert len(ours) == 100
     assert len(list(iter(Groupwise_Sampler(ds)))) == 100  # stops after len(dataset) yields
+
+
+def test_global_cumulative_means_and_gradnorm():
+    from mercury_amd.importance.pool import (classifier_gradnorm, cumulative_means,
+                                             global_cumulative_means)
+    torch.manual_seed(0)
+    x = torch.rand(320)
+    assert torch.allclose(global_cumulative_means(x[None], 32), cumulative_means(x, 32))
+    g = torch.rand(3, 320)
+    gm = global_cumulative_means(g, 32)
+    assert torch.allclose(gm[4], g[:, :160].mean())
+    # gradnorm == per-sample autograd norm of the classifier's (W, b) gradient
+    fc = nn.Linear(20, 7)
+    h = torch.randn(5, 20)
+    y = torch.randint(0, 7, (5,))
+    gn = classifier_gradnorm(fc(h), y, h)
+    for i in range(5):
+        fc.zero_grad()
+        F.cross_entropy(fc(h[i:i + 1]), y[i:i + 1]).backward()
+        ref = torch.sqrt(fc.weight.grad.pow(2).sum() + fc.bias.grad.pow(2).sum())
+        assert torch.allclose(gn[i], ref, atol=1e-5)

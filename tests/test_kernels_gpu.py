@@ -261,6 +261,54 @@ def test_head_fwd_bwd_is_weighted():
     close(dact, ar.grad, rtol=2e-2, atol=1e-5)
 
 
+def test_head_gradnorm_score_matches_autograd():
+    """score='gradnorm': per-sample classifier-layer gradient norm vs torch autograd."""
+    ops = _ops()
+    from mercury_amd.importance.pool import classifier_gradnorm
+    B, HW, C, K = 16, 16, 512, 10
+    act = bf(torch.rand(B, HW, C, device=DEV))
+    w = torch.randn(K, C, device=DEV) * 0.05
+    b = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (B,), device=DEV)
+    losses = torch.empty(B, device=DEV)
+    ops.head_fwd(act.to(torch.bfloat16), w, b, lab.int(), B, HW, C, K, 'score',
+                 pooled=torch.empty(B, C, device=DEV), losses=losses, score='gradnorm')
+    h = act.mean(1)
+    ref = []
+    for i in range(B):
+        wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        F.cross_entropy((h[i:i + 1] @ wr.t() + br), lab[i:i + 1]).backward()
+        ref.append(torch.sqrt(wr.grad.pow(2).sum() + br.grad.pow(2).sum()))
+    ref = torch.stack(ref)
+    close(losses, ref, rtol=1e-4, atol=1e-5)
+    close(classifier_gradnorm(h @ w.t() + b, lab, h), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_is_sample_global_ema_over_gathered_scores():
+    """Global-EMA mode: the replay runs over all ranks' cumulative pool means."""
+    ops = _ops()
+    from mercury_amd.importance.pool import global_cumulative_means
+    from mercury_amd.utils import EMAverage
+    P, B, W = 320, 32, 4
+    g = torch.rand(W, P, device=DEV) * 3
+    ema = torch.zeros(2, device=DEV)
+    ctrl = torch.zeros(4, dtype=torch.int64, device=DEV)
+    idx = torch.empty(B, dtype=torch.int32, device=DEV)
+    w = torch.empty(B, device=DEV)
+    meters = torch.zeros(8, device=DEV)
+    ops.is_sample(g[1].contiguous(), ema, ctrl, idx, w, P, B, 32, seed=3, meters=meters,
+                  gathered=g)
+    ref = EMAverage()
+    for j in range(10):
+        ref.update(g[:, :32 * (j + 1)].mean().item())
+    assert abs(ema[0].item() - ref.value) < 1e-5
+    gm = global_cumulative_means(g, 32)
+    assert abs(gm[-1].item() - g.mean().item()) < 1e-5
+    assert abs(meters[3].item() - g.mean().item()) < 1e-5
+    p = (g[1] + 0.5 * ema[0]) / (g[1] + 0.5 * ema[0]).sum()
+    close(w, p[idx.long()] * P, rtol=1e-4, atol=1e-5)
+
+
 def test_pool_build_epoch_permutation_and_normalisation():
     ops = _ops()
     from mercury_amd.data.transforms import CIFAR_MEAN, CIFAR_STD
@@ -331,19 +379,66 @@ def test_gather_and_table_sampler():
     bl, bi = torch.empty(B, dtype=torch.int32, device=DEV), torch.empty(B, dtype=torch.int32, device=DEV)
     ops.gather(pool, pl, pi, idx, batch, bl, bi, B)
     assert torch.equal(batch, pool[idx.long()]) and torch.equal(bl, idx) and torch.equal(bi, idx * 3)
-    N = 5000
-    imp = torch.ones(N, device=DEV)
-    grp = torch.zeros(N, dtype=torch.int64, device=DEV)
-    losses = torch.rand(1000, device=DEV) * 4
-    ops.table_write(imp, grp, losses, 2000, 3)
-    assert torch.equal(imp[2000:3000], losses) and int(grp[2500].item()) == 3
-    out = torch.empty(20000, dtype=torch.int64, device=DEV)
-    ops.table_sample(imp, grp, 3, 20000, seed=5, counter=0, out=out)
-    assert out.min().item() >= 2000 and out.max().item() < 3000
-    w = losses + losses.mean()
-    p = w / w.sum()
-    freq = torch.bincount(out - 2000, minlength=1000).float() / 20000
-    assert ((freq - p).abs().sum().item()) < 0.25
+
+
+@pytest.mark.parametrize('N', [5000, 1_281_167])
+def test_global_importance_table(N):
+    """HBM table: contiguous write, index scatter with a device stamp, and the two-level
+    inverse-CDF draw vs the exact distribution p ~ imp + mean(imp) over the group (chi^2)."""
+    ops = _ops()
+    torch.manual_seed(0)
+    t = ops.ImportanceTable(N, DEV)
+    lo, n = N // 3, 1000
+    losses = torch.rand(n, device=DEV) * 4
+    t.write(lo, losses, 3)
+    assert torch.equal(t.importance[lo:lo + n], losses) and int(t.group[lo + 500]) == 3
+    # scattered members far apart (other segments) stamped from a device scalar
+    sidx = torch.randperm(N, device=DEV)[:200].to(torch.int32)
+    sidx = sidx[(sidx < lo) | (sidx >= lo + n)]
+    sl = torch.rand(sidx.numel(), device=DEV) * 2
+    stamp = torch.full((1,), 3, dtype=torch.int64, device=DEV)
+    t.scatter(sidx, sl, stamp=stamp)
+    members = torch.cat([torch.arange(lo, lo + n, device=DEV), sidx.long()])
+    imp = torch.cat([losses, sl])
+    w = imp + imp.mean()
+    p = (w / w.sum()).double()
+    nd = 200_000
+    out = t.sample(nd, 3, seed=5)
+    mean, cnt, total = t.group_stats()
+    assert cnt == members.numel() and abs(mean - imp.mean().item()) < 1e-4
+    assert abs(total - w.sum().item()) / total < 1e-4
+    lut = torch.full((N,), -1, dtype=torch.int64, device=DEV)
+    lut[members] = torch.arange(members.numel(), device=DEV)
+    pos = lut[out]
+    assert int(pos.min()) >= 0, 'drew a non-member'
+    counts = torch.bincount(pos, minlength=members.numel()).double()
+    k = members.numel()
+    chi2 = (((counts - nd * p) ** 2) / (nd * p)).sum().item()
+    assert chi2 < k + 6 * math.sqrt(2 * k), chi2
+    # the device draw counter advances -> a second batch differs
+    out2 = t.sample(nd, 3, seed=5)
+    assert not torch.equal(out, out2)
+    # empty group -> -1
+    assert int(t.sample(4, 99)[0]) == -1
+
+
+def test_groupwise_sampler_gpu_lifecycle():
+    from mercury_amd.importance.groupwise import Groupwise_Sampler
+
+    class DS(object):
+        def __len__(self):
+            return 3000
+
+    s = Groupwise_Sampler(DS(), device=DEV, seed=1, prefetch=64)
+    s.update_importance(1, 1000, None, losses=torch.rand(1000) + 1)
+    s.update_importance(1, 500, None, losses=torch.rand(500) + 1)   # same iteration -> same group
+    draws = torch.as_tensor(list(iter(s)))
+    assert draws.numel() == len(s) == 3000
+    assert int(draws.min()) >= 0 and int(draws.max()) < 1500
+    sd = s.state_dict()
+    s2 = Groupwise_Sampler(DS(), device=DEV)
+    s2.load_state_dict(sd)
+    assert torch.equal(s2.importance, s.importance) and s2.group_index == 1
 
 
 def test_fused_adam_matches_torch_and_writes_bf16_copies():

@@ -28,7 +28,7 @@ def _dp_worker(rank, ws):
     torch.manual_seed(100 + rank)             # different init per rank
     net = ResNet18(10).cuda()
     eng = NativeEngine(net, 'cuda', 32, 10, world_size=ws, bucket_bytes=4 << 20, seed=rank,
-                       exchange_scores=True)
+                       exchange_scores=True, global_ema=True)
     assert len(eng.bucket_plan()) > 1
     eng.set_shard(x[shard], y[shard])
     eng.broadcast_from(0)
@@ -48,6 +48,10 @@ def _dp_worker(rank, ws):
     g = eng.score_exchange.wait()
     torch.cuda.synchronize()
     assert torch.equal(g[rank], eng.score_mode.losses.reshape(-1))
+    # global EMA: one normaliser shared by every rank
+    emas = [torch.zeros(2, device='cuda') for _ in range(ws)]
+    dist.all_gather(emas, eng.ema.clone())
+    assert torch.equal(emas[0], emas[1])
     share = eng.global_share()
     assert abs(float(share.sum()) - 1.0) < 1e-5
 
@@ -93,3 +97,8 @@ def test_native_trainer_api_checkpoint(tmp_path):
     load_checkpoint(tr2, path)
     assert torch.equal(tr2.engine.opt.p, tr.engine.opt.p)
     assert torch.equal(tr2.engine.opt.v, tr.engine.opt.v)
+    # HBM importance table: scored samples carry their latest loss and scoring step
+    tab = tr.engine.table
+    scored = tab.group > 0
+    assert int(scored.sum()) > 0 and bool((tab.importance[scored] > 0).all())
+    assert torch.equal(tr2.engine.table.importance, tab.importance)
