@@ -30,18 +30,36 @@ sys.path.insert(0, ROOT)
 
 REF_CPU_IMG_S = 41.0   # reference step, W=1, 39-43 trained img/s (CPU, only measured number)
 
+HEADLINE = 'images/sec (whole node) + sampler overhead %, ResNet-18 CIFAR-10 DP 1/2/4/8 GPU'
+# BASELINE.json configs 2-5 (config 1 is the CPU plumbing run: examples/cpu_reference_step.py)
+PRESETS = {
+    'resnet18-cifar10': dict(model='resnet18', classes=10, hw=32, n=50000, batch=32,
+                             metric=HEADLINE, dataset='cifar10-shape (32x32x3, 10 classes)'),
+    'mobilenetv2-cifar100': dict(model='mobilenetv2', classes=100, hw=32, n=50000, batch=32,
+                                 metric='images/sec (whole node) + sampler overhead %, '
+                                        'MobileNetV2 CIFAR-100 DP',
+                                 dataset='cifar100-shape (32x32x3, 100 classes)'),
+    'resnet50-imagenet': dict(model='resnet50_imagenet', classes=1000, hw=224, n=12800, batch=128,
+                              metric='images/sec (whole node) + sampler overhead %, '
+                                     'ResNet-50 ImageNet-shape 224 DP',
+                              dataset='imagenet-shape (224x224x3, 1000 classes; 12800 '
+                                      'synthetic images resident in HBM)'),
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
-    ap.add_argument('--model', default='resnet18')
-    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--config', default='resnet18-cifar10', choices=sorted(PRESETS))
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (0: preset)')
     ap.add_argument('--pool-batches', type=int, default=10)
     ap.add_argument('--no-overhead', action='store_true')
     ap.add_argument('--no-graphs', action='store_true')
     args = ap.parse_args()
+    pre = PRESETS[args.config]
+    args.batch = args.batch or pre['batch']
 
     import numpy as np
     import torch
@@ -56,17 +74,18 @@ def main():
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import build_model
 
-    x_all, y_all = synthetic_arrays(50000, 10, seed=8)
+    ncls, hw, n = pre['classes'], pre['hw'], pre['n']
+    x_all, y_all = synthetic_arrays(n, ncls, shape=(hw, hw, 3), seed=8)
     np.random.seed(102)
-    shards = dirichlet_partition(y_all, ws, 0.5, 10) if ws > 1 else {0: np.arange(50000)}
+    shards = dirichlet_partition(y_all, ws, 0.5, ncls) if ws > 1 else {0: np.arange(n)}
     idx = np.asarray(shards[rank])
     torch.manual_seed(1234)
-    net = build_model(args.model, 10).to(device)
+    net = build_model(pre['model'], ncls).to(device)
 
     def make(importance):
         eng = NativeEngine(net, device, args.batch, args.pool_batches, optimizer='adam',
                            lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
-                           use_graphs=not args.no_graphs)
+                           use_graphs=not args.no_graphs, image_hw=(hw, hw))
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)
@@ -108,7 +127,7 @@ def main():
         overhead = 100.0 * max(0.0, 1.0 - t_u / t_is)
     if rank == 0:
         out = {
-            'metric': 'images/sec (whole node) + sampler overhead %, ResNet-18 CIFAR-10 DP 1/2/4/8 GPU',
+            'metric': pre['metric'],
             'value': round(value, 2), 'unit': 'trained images/s', 'n_gpus': ws,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 4),
             'higher_is_better': True, 'scaling': 'weak',
@@ -118,7 +137,7 @@ def main():
             'sampler_overhead_pct': None if overhead is None else round(overhead, 2),
             'scored_images_per_sec': round(ws * args.batch * args.pool_batches * args.steps / t_is, 1),
             'dtype': 'bf16', 'data': 'synthetic',
-            'config': {'model': args.model, 'dataset': 'cifar10-shape (32x32x3, 10 classes)',
+            'config': {'model': pre['model'], 'dataset': pre['dataset'],
                        'global_batch': ws * args.batch, 'per_gpu_batch': args.batch,
                        'presample_pool': args.batch * args.pool_batches, 'seq_len': None,
                        'optimizer': 'adam', 'parallelism': 'dp%d' % ws,

@@ -40,7 +40,7 @@ def synthetic_arrays(n, num_classes, shape=(32, 32, 3), seed=0, noise=48):
         torch.from_numpy(small).permute(0, 3, 1, 2), size=(h, w), mode='bilinear',
         align_corners=False).permute(0, 2, 3, 1).numpy()
     x = np.empty((n,) + tuple(shape), dtype=np.uint8)
-    chunk = 4096
+    chunk = max(1, (64 << 20) // (int(np.prod(shape)) * 4))   # ~64 MB of fp32 noise per chunk
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         nz = rng.randint(-noise, noise + 1, size=(e - s,) + tuple(shape)).astype(np.float32)

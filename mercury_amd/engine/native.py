@@ -420,6 +420,12 @@ class NativeEngine(object):
         """Keep this rank's training shard resident in HBM: uint8 [Ns][H][W][3]."""
         x = torch.as_tensor(np.ascontiguousarray(images_u8)) if not torch.is_tensor(images_u8) \
             else images_u8
+        if x.dim() != 4 or tuple(x.shape[1:]) != (self.H, self.W, 3):
+            raise ValueError('shard must be uint8 [N][%d][%d][3], got %s'
+                             % (self.H, self.W, tuple(x.shape)))
+        if x.shape[0] < self.B:
+            # the device epoch permutation draws whole batches from the shard
+            raise ValueError('shard has %d samples < batch %d' % (x.shape[0], self.B))
         self.shard = x.to(self.device, torch.uint8).contiguous()
         self.shard_labels = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
         self.train_mode = self.mode('train', self.B, 0, True)

@@ -15,24 +15,27 @@ def _cos(a, b):
     return float((a @ b) / (a.norm() * b.norm() + 1e-30))
 
 
-def _engine(net, **kw):
+def _engine(net, hw=32, **kw):
     from mercury_amd.engine.native import NativeEngine
-    eng = NativeEngine(net, DEV, batch_size=32, pool_batches=10, use_graphs=False, **kw)
+    eng = NativeEngine(net, DEV, batch_size=32, pool_batches=10, use_graphs=False,
+                       image_hw=(hw, hw), **kw)
     rng = np.random.RandomState(0)
-    eng.set_shard(rng.randint(0, 256, (1000, 32, 32, 3), dtype=np.uint8), rng.randint(0, 10, 1000))
+    eng.set_shard(rng.randint(0, 256, (1000, hw, hw, 3), dtype=np.uint8), rng.randint(0, 10, 1000))
     return eng
 
 
-@pytest.mark.parametrize('arch', ['resnet18', 'resnet50', 'mobilenetv2'])
-def test_train_forward_backward_matches_torch(arch):
+@pytest.mark.parametrize('arch,hw', [('resnet18', 32), ('resnet50', 32), ('mobilenetv2', 32),
+                                     ('resnet50_imagenet', 64)])
+def test_train_forward_backward_matches_torch(arch, hw):
+    """Every supported family incl. the ImageNet stem (7x7/2 conv + 3x3/2 max-pool)."""
     from mercury_amd import ops
     from mercury_amd.models import build_model
     torch.manual_seed(0)
     ncls = 100 if arch == 'mobilenetv2' else 10
     net = build_model(arch, ncls).to(DEV)
-    eng = _engine(net)
+    eng = _engine(net, hw)
     tm = eng.train_mode
-    x = torch.randn(32, 3, 32, 32, device=DEV).to(torch.bfloat16).float()
+    x = torch.randn(32, 3, hw, hw, device=DEV).to(torch.bfloat16).float()
     y = torch.randint(0, ncls, (32,), device=DEV)
     w = torch.rand(32, device=DEV) + 0.5
     tm.input.copy_(ops.to_nhwc(x))
