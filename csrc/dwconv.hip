@@ -1,0 +1,322 @@
+// Depthwise 3x3 convolution (MobileNetV2 inverted residuals), NHWC bf16, fp32 weights [C][3][3].
+//
+// Depthwise conv has no reduction over channels, so there is nothing for MFMA to do: it is a
+// bandwidth / latency problem.  Design (per thread = one 16-byte chunk of 8 channels):
+//
+//   fwd   : a strip of DWL outputs along W.  The 3 x ((DWL-1)*S+3) input window is loaded once
+//           as 16-byte vectors and reused by the DWL outputs (4.5 loads/output at stride 1
+//           instead of 9); the thread's 72 weights are loaded once (18 x float4) into registers.
+//           BN batch statistics of the bf16-rounded outputs are fused: LDS float atomics per
+//           block, one global atomic per channel per block (ghost-BN groups respected).
+//   dgrad : the same strip shape over the input grid (stride 1: a correlation with the flipped
+//           taps through a sliding dy window; stride 2: parity-filtered gather).
+//   wgrad : one thread per (image, output row, chunk) walks the row with a sliding 3x3 input
+//           window (3 new loads per output at stride 1), 72 fp32 accumulators in registers, then
+//           LDS reduction across the block and one global atomic per (channel, tap) per block.
+//
+// Thread index -> (chunk fastest, then strip, row, image): adjacent lanes touch adjacent 16 B
+// chunks of the same pixel, so every wave access is a contiguous run of the NHWC row.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int DT = 256;
+constexpr int DWL = 4;
+
+MA_DEV void load_w72(const float* w, int c8, float (&wr)[9][8]) {
+  const f32x4* src = (const f32x4*)(w + (size_t)c8 * 72);
+  float t[72];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) {
+    const f32x4 v = src[i];
+    t[4 * i] = v.x;
+    t[4 * i + 1] = v.y;
+    t[4 * i + 2] = v.z;
+    t[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) wr[tap][k] = t[k * 9 + tap];
+}
+
+MA_DEV bf16x8 ld8(const bf16* p, bool ok) {
+  bf16x8 v;
+  if (ok) {
+    v = *(const bf16x8*)p;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = f2bf(0.f);
+  }
+  return v;
+}
+
+template <int S>
+__global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
+  extern __shared__ float red[];  // [2][C] block partial BN sums
+  const int C8 = a.C >> 3, QS = (a.Q + DWL - 1) / DWL;
+  const int per_img = a.P * QS * C8;
+  const int total = a.N * per_img;
+  const int g0 = blockIdx.x * DT, gt = g0 + threadIdx.x;
+  const int imgs_per_group = a.group_rows / (a.P * a.Q);
+  const int gfirst = (g0 / per_img) / imgs_per_group;
+  const int glast = (min(total - 1, g0 + DT - 1) / per_img) / imgs_per_group;
+  const bool lds_stats = a.stats && gfirst == glast;
+  if (lds_stats) {
+    for (int i = threadIdx.x; i < 2 * a.C; i += DT) red[i] = 0.f;
+    __syncthreads();
+  }
+  if (gt < total) {
+    const int c8 = gt % C8;
+    int r = gt / C8;
+    const int qs = r % QS;
+    r /= QS;
+    const int p = r % a.P, n = r / a.P;
+    float wr[9][8];
+    load_w72(a.w, c8, wr);
+    constexpr int NCOL = (DWL - 1) * S + 3;
+    const int q0 = qs * DWL, w0 = q0 * S - a.pad;
+    float acc[DWL][8];
+#pragma unroll
+    for (int o = 0; o < DWL; ++o)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const int h = p * S - a.pad + rr;
+      if (h >= 0 && h < a.H) {
+        const bf16* row = a.x + (size_t)(n * a.H + h) * a.W * a.C + c8 * 8;
+        bf16x8 col[NCOL];
+#pragma unroll
+        for (int j = 0; j < NCOL; ++j) {
+          const int ww = w0 + j;
+          col[j] = ld8(row + (size_t)ww * a.C, ww >= 0 && ww < a.W);
+        }
+#pragma unroll
+        for (int o = 0; o < DWL; ++o)
+#pragma unroll
+          for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o * S + t][k]) * wr[rr * 3 + t][k];
+      }
+    }
+    float s[8], ss[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = ss[k] = 0.f;
+    bf16* yrow = a.y + (size_t)(n * a.P + p) * a.Q * a.C + c8 * 8;
+#pragma unroll
+    for (int o = 0; o < DWL; ++o) {
+      if (q0 + o < a.Q) {
+        bf16x8 v;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          v[k] = f2bf(acc[o][k]);
+          const float f = bf2f(v[k]);
+          s[k] += f;
+          ss[k] += f * f;
+        }
+        *(bf16x8*)(yrow + (size_t)(q0 + o) * a.C) = v;
+      }
+    }
+    if (a.stats) {
+      if (lds_stats) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          atomicAdd(&red[c8 * 8 + k], s[k]);
+          atomicAdd(&red[a.C + c8 * 8 + k], ss[k]);
+        }
+      } else {  // block straddles two BN groups (tiny images): direct global atomics
+        float* dst = a.stats + (size_t)(n / imgs_per_group) * 2 * a.C;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          atomicAdd(dst + c8 * 8 + k, s[k]);
+          atomicAdd(dst + a.C + c8 * 8 + k, ss[k]);
+        }
+      }
+    }
+  }
+  if (lds_stats) {
+    __syncthreads();
+    float* dst = a.stats + (size_t)gfirst * 2 * a.C;
+    for (int c = threadIdx.x; c < a.C; c += DT) {
+      const float v0 = red[c], v1 = red[a.C + c];
+      if (v1 != 0.f) {  // sumsq == 0 <=> no (non-zero) output of this channel in the block
+        atomicAdd(dst + c, v0);
+        atomicAdd(dst + a.C + c, v1);
+      }
+    }
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const float* w, bf16* dx, int N,
+                                                      int H, int W, int C, int P, int Q, int pad) {
+  const int C8 = C >> 3, WS = (W + DWL - 1) / DWL;
+  const int total = N * H * WS * C8;
+  const int gt = blockIdx.x * DT + threadIdx.x;
+  if (gt >= total) return;
+  const int c8 = gt % C8;
+  int r = gt / C8;
+  const int ws = r % WS;
+  r /= WS;
+  const int h = r % H, n = r / H;
+  float wr[9][8];
+  load_w72(w, c8, wr);
+  const int x0 = ws * DWL;
+  float acc[DWL][8];
+#pragma unroll
+  for (int o = 0; o < DWL; ++o)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 3; ++rr) {
+    const int hp = h + pad - rr;
+    if (S == 1) {
+      if (hp >= 0 && hp < P) {
+        const bf16* row = dy + (size_t)(n * P + hp) * Q * C + c8 * 8;
+        bf16x8 col[DWL + 2];  // dy columns x0+pad-2 .. x0+DWL-1+pad
+#pragma unroll
+        for (int j = 0; j < DWL + 2; ++j) {
+          const int q = x0 + pad - 2 + j;
+          col[j] = ld8(row + (size_t)q * C, q >= 0 && q < Q);
+        }
+#pragma unroll
+        for (int o = 0; o < DWL; ++o)
+#pragma unroll
+          for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o + 2 - t][k]) * wr[rr * 3 + t][k];
+      }
+    } else {
+      if (hp >= 0 && (hp % S) == 0 && hp / S < P) {
+        const bf16* row = dy + (size_t)(n * P + hp / S) * Q * C + c8 * 8;
+#pragma unroll
+        for (int o = 0; o < DWL; ++o)
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int wp = x0 + o + pad - t;
+            if (wp >= 0 && (wp % S) == 0 && wp / S < Q) {
+              const bf16x8 v = *(const bf16x8*)(row + (size_t)(wp / S) * C);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(v[k]) * wr[rr * 3 + t][k];
+            }
+          }
+      }
+    }
+  }
+  bf16* xrow = dx + (size_t)(n * H + h) * W * C + c8 * 8;
+#pragma unroll
+  for (int o = 0; o < DWL; ++o) {
+    if (x0 + o < W) {
+      bf16x8 v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = f2bf(acc[o][k]);
+      *(bf16x8*)(xrow + (size_t)(x0 + o) * C) = v;
+    }
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
+                                                      int H, int W, int C, int P, int Q, int pad) {
+  extern __shared__ float red[];  // [9][C]
+  const int C8 = C >> 3;
+  const int total = N * P * C8;
+  const int gt = blockIdx.x * DT + threadIdx.x;
+  for (int i = threadIdx.x; i < 9 * C; i += DT) red[i] = 0.f;
+  __syncthreads();
+  if (gt < total) {
+    const int c8 = gt % C8;
+    const int r = gt / C8;
+    const int p = r % P, n = r / P;
+    float acc[9][8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
+    const bf16* rows[3];
+    bool rok[3];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const int h = p * S - pad + rr;
+      rok[rr] = h >= 0 && h < H;
+      rows[rr] = x + (size_t)(n * H + (rok[rr] ? h : 0)) * W * C + c8 * 8;
+    }
+    // sliding window win[rr][t] = x[h_rr][q*S - pad + t]
+    bf16x8 win[3][3];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int ww = -pad + t;
+        win[rr][t] = ld8(rows[rr] + (size_t)ww * C, rok[rr] && ww >= 0 && ww < W);
+      }
+    const bf16* grow = dy + (size_t)(n * P + p) * Q * C + c8 * 8;
+    for (int q = 0; q < Q; ++q) {
+      if (q > 0) {
+        const int base = q * S - pad;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          if (S == 1) {
+            win[rr][0] = win[rr][1];
+            win[rr][1] = win[rr][2];
+          } else {
+            win[rr][0] = win[rr][2];
+            win[rr][1] = ld8(rows[rr] + (size_t)(base + 1) * C, rok[rr] && base + 1 >= 0 && base + 1 < W);
+          }
+          win[rr][2] = ld8(rows[rr] + (size_t)(base + 2) * C, rok[rr] && base + 2 >= 0 && base + 2 < W);
+        }
+      }
+      const bf16x8 g = *(const bf16x8*)(grow + (size_t)q * C);
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[rr * 3 + t][k] += bf2f(g[k]) * bf2f(win[rr][t][k]);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(&red[t * C + c8 * 8 + k], acc[t][k]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 9 * C; i += DT) {
+    const float v = red[i];
+    if (v != 0.f) {
+      const int t = i / C, c = i - t * C;
+      atomicAdd(&dw[c * 9 + t], v);
+    }
+  }
+}
+}  // namespace
+
+void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
+  const int QS = (a.Q + DWL - 1) / DWL;
+  const long long total = (long long)a.N * a.P * QS * (a.C / 8);
+  const dim3 grid((unsigned)((total + DT - 1) / DT));
+  const size_t shm = a.stats ? 2 * (size_t)a.C * sizeof(float) : 0;
+  if (a.stride == 1)
+    hipLaunchKernelGGL(dw_fwd_kernel<1>, grid, dim3(DT), shm, st, a);
+  else
+    hipLaunchKernelGGL(dw_fwd_kernel<2>, grid, dim3(DT), shm, st, a);
+}
+void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int P,
+                         int Q, int stride, int pad, hipStream_t st) {
+  const long long total = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
+  const dim3 grid((unsigned)((total + DT - 1) / DT));
+  if (stride == 1)
+    hipLaunchKernelGGL(dw_dgrad_kernel<1>, grid, dim3(DT), 0, st, dy, w, dx, N, H, W, C, P, Q, pad);
+  else
+    hipLaunchKernelGGL(dw_dgrad_kernel<2>, grid, dim3(DT), 0, st, dy, w, dx, N, H, W, C, P, Q, pad);
+}
+void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,
+                         int Q, int stride, int pad, hipStream_t st) {
+  const long long total = (long long)N * P * (C / 8);
+  const dim3 grid((unsigned)((total + DT - 1) / DT));
+  const size_t shm = 9 * (size_t)C * sizeof(float);
+  if (stride == 1)
+    hipLaunchKernelGGL(dw_wgrad_kernel<1>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad);
+  else
+    hipLaunchKernelGGL(dw_wgrad_kernel<2>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad);
+}

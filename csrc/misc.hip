@@ -1,5 +1,4 @@
-// Remaining layer kernels: pooling (VGG / ImageNet stem), depthwise 3x3 conv
-// (MobileNetV2), stochastic quantisation (`util.py:65-70`) and
+// Remaining layer kernels: pooling (VGG / ImageNet stem), stochastic quantisation (`util.py:65-70`) and
 // NCHW fp32 -> NHWC bf16 layout conversion for host-fed tensors.
 #include "common.h"
 #include "kernels.h"
@@ -76,142 +75,6 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(PoolArgs a, const bf16*
   dx[i] = f2bf(s);
 }
 
-// --------------------------------------------------------------- depthwise 3x3
-// One block per (image, channel-block of 8*32 channels); threads = 8 pixel lanes x 32 chunks.
-__global__ __launch_bounds__(NT) void dw_fwd_kernel(DwArgs a) {
-  __shared__ float red[2 * 1024];
-  const int C8 = a.C >> 3;
-  const int n = blockIdx.x;
-  for (int i = threadIdx.x; i < 2 * a.C; i += NT) red[i] = 0.f;
-  __syncthreads();
-  const int items = a.P * a.Q * C8;
-  float s[8], ss[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s[k] = ss[k] = 0.f;
-  int c8_last = -1;
-  for (int it = threadIdx.x; it < items; it += NT) {
-    const int c8 = it % C8, pq = it / C8;
-    if (c8 != c8_last && c8_last >= 0 && a.stats) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        atomicAdd(&red[c8_last * 8 + k], s[k]);
-        atomicAdd(&red[a.C + c8_last * 8 + k], ss[k]);
-        s[k] = ss[k] = 0.f;
-      }
-    }
-    c8_last = c8;
-    const int p = pq / a.Q, q = pq - p * a.Q;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int r = 0; r < 3; ++r) {
-      const int h = p * a.stride - a.pad + r;
-      if (h < 0 || h >= a.H) continue;
-      for (int t = 0; t < 3; ++t) {
-        const int w = q * a.stride - a.pad + t;
-        if (w < 0 || w >= a.W) continue;
-        const bf16x8 v = *(const bf16x8*)(a.x + ((size_t)(n * a.H + h) * a.W + w) * a.C + c8 * 8);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += bf2f(v[k]) * a.w[(c8 * 8 + k) * 9 + r * 3 + t];
-      }
-    }
-    bf16x8 o;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      o[k] = f2bf(acc[k]);
-      const float f = bf2f(o[k]);
-      s[k] += f;
-      ss[k] += f * f;
-    }
-    *(bf16x8*)(a.y + ((size_t)(n * a.P + p) * a.Q + q) * a.C + c8 * 8) = o;
-  }
-  if (a.stats) {
-    if (c8_last >= 0) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        atomicAdd(&red[c8_last * 8 + k], s[k]);
-        atomicAdd(&red[a.C + c8_last * 8 + k], ss[k]);
-      }
-    }
-    __syncthreads();
-    const int g = (n * a.P * a.Q) / a.group_rows;
-    float* dst = a.stats + (size_t)g * 2 * a.C;
-    for (int c = threadIdx.x; c < a.C; c += NT) {
-      atomicAdd(dst + c, red[c]);
-      atomicAdd(dst + a.C + c, red[a.C + c]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(NT) void dw_dgrad_kernel(const bf16* dy, const float* w, bf16* dx, int N,
-                                                      int H, int W, int C, int P, int Q, int stride,
-                                                      int pad) {
-  const int C8 = C >> 3;
-  const long long total = (long long)N * H * W * C8;
-  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
-  if (i >= total) return;
-  const int c8 = (int)(i % C8);
-  const long long pix = i / C8;
-  const int x = (int)(pix % W), y = (int)((pix / W) % H), n = (int)(pix / ((long long)H * W));
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = 0; r < 3; ++r) {
-    const int hp = y + pad - r;
-    if (hp < 0 || hp % stride) continue;
-    const int p = hp / stride;
-    if (p >= P) continue;
-    for (int t = 0; t < 3; ++t) {
-      const int wp = x + pad - t;
-      if (wp < 0 || wp % stride) continue;
-      const int q = wp / stride;
-      if (q >= Q) continue;
-      const bf16x8 v = *(const bf16x8*)(dy + ((size_t)(n * P + p) * Q + q) * C + c8 * 8);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += bf2f(v[k]) * w[(c8 * 8 + k) * 9 + r * 3 + t];
-    }
-  }
-  bf16x8 o;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = f2bf(acc[k]);
-  *(bf16x8*)(dx + i * 8) = o;
-}
-
-// one block per image; each thread accumulates 9 taps x 8 channels for its chunk
-__global__ __launch_bounds__(NT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
-                                                      int H, int W, int C, int P, int Q, int stride,
-                                                      int pad) {
-  const int C8 = C >> 3;
-  const int n = blockIdx.x;
-  const int lanes = NT / C8 > 0 ? NT / C8 : 1;
-  const int sub = threadIdx.x / C8;
-  if (sub >= lanes) return;
-  for (int c8 = threadIdx.x % C8; c8 < C8; c8 += NT) {
-    float acc[9][8];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
-    for (int pq = sub; pq < P * Q; pq += lanes) {
-      const int p = pq / Q, q = pq - p * Q;
-      const bf16x8 g = *(const bf16x8*)(dy + ((size_t)(n * P + p) * Q + q) * C + c8 * 8);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int h = p * stride - pad + r;
-        if (h < 0 || h >= H) continue;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const int w = q * stride - pad + t;
-          if (w < 0 || w >= W) continue;
-          const bf16x8 v = *(const bf16x8*)(x + ((size_t)(n * H + h) * W + w) * C + c8 * 8);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[r * 3 + t][k] += bf2f(g[k]) * bf2f(v[k]);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(&dw[(c8 * 8 + k) * 9 + t], acc[t][k]);
-  }
-}
-
 // --------------------------------------------------------------- quantisation
 __global__ __launch_bounds__(NT) void absmax_kernel(const float* x, long long n, float* out) {
   float m = 0.f;
@@ -252,20 +115,6 @@ void maxpool2d_bwd_launch(const PoolArgs& a, const bf16* dy, bf16* dx, hipStream
   const long long total = (long long)a.N * a.H * a.W * a.C;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, a,
                      dy, dx);
-}
-void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(a.N), dim3(NT), 0, st, a);
-}
-void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int P,
-                         int Q, int stride, int pad, hipStream_t st) {
-  const long long total = (long long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(dw_dgrad_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, dy, w,
-                     dx, N, H, W, C, P, Q, stride, pad);
-}
-void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,
-                         int Q, int stride, int pad, hipStream_t st) {
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(N), dim3(NT), 0, st, dy, x, dw, N, H, W, C, P, Q, stride,
-                     pad);
 }
 void quantize_launch(const float* x, float* out, float* absmax_ws, long long n, uint32_t seed,
                      uint64_t counter, hipStream_t st) {

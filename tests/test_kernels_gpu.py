@@ -523,6 +523,37 @@ def test_quantize_pool_dwconv():
         close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize('case', [(8, 96, 16, 16, 1, 4), (8, 144, 15, 15, 2, 2),
+                                  (4, 960, 4, 4, 1, 2), (3, 16, 7, 9, 2, 1), (6, 40, 5, 11, 1, 3)])
+def test_depthwise_strips_ghost_stats(case):
+    """Strip/sliding-window depthwise kernels: odd widths, stride 2, ghost-BN groups, and
+    blocks that straddle two BN groups (tiny images, many channels)."""
+    ops = _ops()
+    N, C, H, W, st, G = case
+    torch.manual_seed(1)
+    xx = bf(torch.randn(N, C, H, W, device=DEV)).requires_grad_(True)
+    w = torch.randn(C, 1, 3, 3, device=DEV).requires_grad_(True)
+    ref = F.conv2d(xx, bf(w), stride=st, padding=1, groups=C)
+    P, Q = ref.shape[2:]
+    y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(G, 2, C, device=DEV)
+    wf = bf(w.detach()).reshape(C, 9).contiguous()
+    ops.dwconv_fwd(ops.to_nhwc(xx.detach()), wf, y, N, H, W, C, P, Q, st, 1, stats=stats,
+                   group_rows=(N // G) * P * Q)
+    close(ops.from_nhwc(y), ref)
+    yr = bf(ref).reshape(G, N // G, C, P, Q)
+    close(stats[:, 0], yr.sum((1, 3, 4)), 1e-2, 0.5)
+    close(stats[:, 1], yr.pow(2).sum((1, 3, 4)), 1e-2, 0.5)
+    gy = bf(torch.randn_like(ref))
+    ref.backward(gy)
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    ops.dwconv_dgrad(ops.to_nhwc(gy), wf, dx, N, H, W, C, P, Q, st, 1)
+    close(ops.from_nhwc(dx), xx.grad)
+    dw = torch.zeros(C, 9, device=DEV)
+    ops.dwconv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(xx.detach()), dw, N, H, W, C, P, Q, st, 1)
+    close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize('pipe', [3, 4])
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_pipelined_lds_dma(case, pipe):
