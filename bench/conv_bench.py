@@ -61,7 +61,7 @@ def main():
             y = torch.empty(sp.M, K, dtype=torch.bfloat16, device=dev)
             stats = torch.zeros(2, K, device=dev)
             pf = fwd_plan(sp)
-            slab = torch.empty(max(1, slab_bytes(sp.M, K, *pf) // 4), device=dev)
+            slab = torch.zeros(max(1, slab_bytes(sp.M, K, *pf) // 4), device=dev)
             ours_f = timeit(lambda: ops.conv_fwd(xn, wk, y, sp, stats=stats, slab=slab, plan=pf,
                                                  pipe=0), args.iters)
             pipe_f = {pp: timeit(lambda: ops.conv_fwd(xn, wk, y, sp, stats=stats, slab=slab,
@@ -77,7 +77,7 @@ def main():
             if C % 8 == 0:
                 dx = torch.empty(N * H * H, C, dtype=torch.bfloat16, device=dev)
                 pd_ = dgrad_plan(sp)
-                slab2 = torch.empty(max(1, slab_bytes(N * H * H, C, *pd_) // 4), device=dev)
+                slab2 = torch.zeros(max(1, slab_bytes(N * H * H, C, *pd_) // 4), device=dev)
                 r['dgrad_us'] = timeit(lambda: ops.conv_dgrad(gyn, wt, dx, sp, slab=slab2,
                                                               plan=pd_, pipe=0), args.iters)
                 r['dgrad_pipe4_us'] = timeit(lambda: ops.conv_dgrad(gyn, wt, dx, sp, slab=slab2,

@@ -22,7 +22,7 @@ def main():
     y = torch.empty(sp.M, K, dtype=torch.bfloat16, device='cuda')
     stats = torch.zeros(2, K, device='cuda')
     plan = fwd_plan(sp)
-    slab = torch.empty(max(1, slab_bytes(sp.M, K, *plan) // 4), device='cuda')
+    slab = torch.zeros(max(1, slab_bytes(sp.M, K, *plan) // 4), device='cuda')
     for _ in range(iters):
         ops.conv_fwd(x, wk, y, sp, stats=stats, slab=slab, plan=plan, pipe=pipe)
     torch.cuda.synchronize()

@@ -33,7 +33,8 @@
 // LDS rows are XOR-swizzled (chunk c of row r lives at c ^ (r&7)).  All address math
 // is 32-bit (per-row base offsets + one uniform per-tap offset), padding chunks read
 // a zero page.  Split-K writes fp32 partial tiles in fragment order (16 B per lane,
-// fully coalesced) and a reducer runs the same epilogue.
+// fully coalesced); the last-arriving slice of each tile reduces them and runs the
+// same epilogue inside the launch (see finish()).
 #include "common.h"
 #include "igemm.h"
 
@@ -271,18 +272,59 @@ MA_DEV void mma_stage(const bf16* a, const bf16* b, f32x4 (&acc)[BM / 32][BN / 3
   }
 }
 
+// Split-K: every K-slice block writes its fp32 partial tile (fragment order, 16 B per lane,
+// fully coalesced) behind the slab's tile-counter header; the LAST block to arrive on a tile
+// sums all slices and runs the epilogue in the same launch (no reducer kernel, no extra launch
+// in the step graph).  Hand-off (cdna_hip_programming.md §6 Guideline 16, R1 form): partials are
+// stored write-through (buffer store, sc1) and drained by every wave before the workgroup
+// barrier, one lane takes a relaxed agent-scope ticket; the last arriver reads the other slices
+// with sc1 loads only -- no L2 write-back fence per block, correct for any XCD placement.  The
+// counter is reset by the last arriver (slabs are zero-initialised at allocation).
+constexpr int SEM_INTS = 1024;   // tile counters at the head of the slab (4 KB)
+
 template <int BM, int BN>
 MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
                    int m0, int n0) {
   constexpr int TM = BM / 32, TN = BN / 32;
-  if (e.slab) {  // split-K partial in fragment order: [split][tile][TM*TN][256 threads] float4
-    const size_t ntiles = (size_t)gridDim.x;
-    f32x4* dst = (f32x4*)e.slab + ((size_t)blockIdx.y * ntiles + blockIdx.x) * (TM * TN) * NT;
+  if (e.slab) {
+    const int ntiles = gridDim.x;
+    const int splits = gridDim.y;
+    int* sem = (int*)e.slab;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(e.slab + SEM_INTS), 0, 0x7fffffff,
+                                                      0x00020000);
+    const int tile_bytes = TM * TN * NT * 16;
+    const int mine = (blockIdx.y * ntiles + blockIdx.x) * tile_bytes + threadIdx.x * 16;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) dst[(tm * TN + tn) * NT + threadIdx.x] = acc[tm][tn];
-    return;
+      for (int tn = 0; tn < TN; ++tn)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[tm][tn]), rs,
+                                               mine + (tm * TN + tn) * NT * 16, 0, 16 /*sc1*/);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+    int* flag = (int*)smem;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(&sem[blockIdx.x], 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == splits - 1;
+      if (last) __hip_atomic_store(&sem[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the ticket
+    for (int sp = 0; sp < splits; ++sp) {
+      if (sp == (int)blockIdx.y) continue;
+      const int base = (sp * ntiles + blockIdx.x) * tile_bytes + threadIdx.x * 16;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] += __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (tm * TN + tn) * NT * 16, 0,
+                                                           16 /*sc1*/));
+    }
+    __syncthreads();   // flag read by every wave before the epilogue reuses smem
   }
   epilogue<BM, BN>(acc, smem, e, M, N, m0, n0);
 }
@@ -472,29 +514,6 @@ __global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restric
   finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(NT) void splitk_reduce_kernel(ConvGeom g, EpiParams e, int splits) {
-  constexpr int TM = BM / 32, TN = BN / 32;
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::RED_BYTES];
-  const int tid = threadIdx.x;
-  const int ntn = (g.Ncols + BN - 1) / BN;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
-  const size_t ntiles = gridDim.x;
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int sp = 0; sp < splits; ++sp) {
-    const f32x4* src = (const f32x4*)e.slab + ((size_t)sp * ntiles + blockIdx.x) * (TM * TN) * NT;
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) acc[tm][tn] += src[(tm * TN + tn) * NT + tid];
-  }
-  epilogue<BM, BN>(acc, smem, e, g.M, g.Ncols, mt * BM, nt * BN);
-}
-
 template <int BM, int BN, bool TRANS>
 void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int per,
                  dim3 grid, int pipe, hipStream_t st) {
@@ -514,24 +533,19 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
   const int mtiles = (g.M + BM - 1) / BM, ntiles = (g.Ncols + BN - 1) / BN;
   const int ktiles = (g.Kc + 7) / 8;
   splits = splits < 1 ? 1 : (splits > ktiles ? ktiles : splits);
-  const int per = (ktiles + splits - 1) / splits;
+  int per = (ktiles + splits - 1) / splits;
   splits = (ktiles + per - 1) / per;
+  if (mtiles * ntiles > SEM_INTS) splits = 1, per = ktiles;   // no counter slot: no split
   dim3 grid(mtiles * ntiles, splits);
-  if (splits == 1) {
-    e.slab = nullptr;
-    launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);
-  } else {
-    launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);  // writes slabs
-    hipLaunchKernelGGL((splitk_reduce_kernel<BM, BN>), dim3(mtiles * ntiles), dim3(NT), 0, st, g, e,
-                       splits);
-  }
+  if (splits == 1) e.slab = nullptr;
+  launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);
 }
 
 }  // namespace
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   const size_t mtiles = (g.M + bm - 1) / bm, ntiles = (g.Ncols + bn - 1) / bn;
-  return (size_t)splits * mtiles * ntiles * bm * bn * 4;
+  return SEM_INTS * 4 + (size_t)splits * mtiles * ntiles * bm * bn * 4;
 }
 
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e,

@@ -260,7 +260,7 @@ class NativeEngine(object):
         m.losses = torch.zeros(N, device=dev)
         if train:
             m.dlogits = torch.zeros(N, self.classes, device=dev)
-        m.slab = torch.empty(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
+        m.slab = torch.zeros(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
         m.input = torch.zeros(N, self.H, self.W, cpad8(self.lw.in_channels), dtype=bf, device=dev)
         m.label = torch.zeros(N, dtype=torch.int32, device=dev)
         m.index = torch.zeros(N, dtype=torch.int32, device=dev)

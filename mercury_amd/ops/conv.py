@@ -82,10 +82,14 @@ def pick_tiles(M, Ncols, kchunks, group_rows=0, min_blocks=CU):
     return bm, bn, splits
 
 
+SEM_BYTES = 4096   # per-tile split-K arrival counters at the head of a slab (csrc/igemm.hip)
+
+
 def slab_bytes(M, Ncols, bm, bn, splits):
+    """Split-K workspace: tile counters (must start zeroed) + fp32 partial tiles."""
     if splits <= 1:
         return 0
-    return splits * math.ceil(M / bm) * math.ceil(Ncols / bn) * bm * bn * 4
+    return SEM_BYTES + splits * math.ceil(M / bm) * math.ceil(Ncols / bn) * bm * bn * 4
 
 
 def fwd_plan(spec: ConvSpec):
@@ -114,7 +118,7 @@ def _slab(slab, need, device):
     if slab is not None and slab.numel() * slab.element_size() >= need:
         return slab
     if slab is None and not torch.cuda.is_current_stream_capturing():
-        return torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+        return torch.zeros((need + 3) // 4, dtype=torch.float32, device=device)
     raise ValueError('split-K slab too small (%d < %d bytes)' % (
         0 if slab is None else slab.numel() * slab.element_size(), need))
 

@@ -63,7 +63,7 @@ def test_conv_fwd_and_stats(case):
     out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
     stats = torch.zeros(2, K, device=DEV)
     plan = fwd_plan(spec)
-    slab = torch.empty(max(1, slab_bytes(spec.M, K, *plan) // 4), device=DEV)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, K, *plan) // 4), device=DEV)
     ops.conv_fwd(xn, wk, out, spec, stats=stats, slab=slab, plan=plan)
     ref = F.conv2d(x, w, stride=st, padding=pd)
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2)
@@ -82,7 +82,7 @@ def test_conv_fwd_all_tiles(bm_bn_split):
     x, w = _mk(case, 3)
     spec = ConvSpec(*case)
     out = torch.empty(spec.M, 128, dtype=torch.bfloat16, device=DEV)
-    slab = torch.empty(max(1, slab_bytes(spec.M, 128, *bm_bn_split) // 4), device=DEV)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, 128, *bm_bn_split) // 4), device=DEV)
     ops.conv_fwd(ops.to_nhwc(x), ops.pack_conv_weight(w)[0], out, spec, slab=slab,
                  plan=bm_bn_split)
     close(out.view(4, 16, 16, 128).permute(0, 3, 1, 2), F.conv2d(x, w, padding=1))
@@ -117,7 +117,7 @@ def test_conv_dgrad(case):
     _, wt = ops.pack_conv_weight(w)
     dx = torch.empty(N * H * W, spec.Cp, dtype=torch.bfloat16, device=DEV)
     plan = dgrad_plan(spec)
-    slab = torch.empty(max(1, slab_bytes(N * H * W, spec.Cp, *plan) // 4), device=DEV)
+    slab = torch.zeros(max(1, slab_bytes(N * H * W, spec.Cp, *plan) // 4), device=DEV)
     ops.conv_dgrad(ops.to_nhwc(gy), wt, dx, spec, slab=slab, plan=plan)
     close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
     # accumulate mode adds onto existing contents
