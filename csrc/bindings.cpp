@@ -31,10 +31,14 @@ PYBIND11_MODULE(_C, m) {
                     uintptr_t stats, int stats_ld, int group_rows, int accumulate, uintptr_t slab,
                     int SH, int SW, int SC, int RP, int RQ, int R, int Sk, int stride, int pad, int Kc,
                     int Ncols, int M, int bm, int bn, int splits, bool trans, uintptr_t st,
-                    int pipe) {
+                    int pipe, uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
+                    uintptr_t bw_stats2, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
+                    int bw_act) {
     ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
     EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows,
-                accumulate, P<float>(slab)};
+                accumulate, P<float>(slab), P<const bf16>(bw_out), P<const bf16>(bw_y),
+                P<const float>(bw_stats), P<const bf16>(bw_y2), P<const float>(bw_stats2),
+                P<float>(bw_sums), bw_inv_count, bw_eps, bw_act};
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
     check_launch("igemm");
   });
@@ -71,12 +75,12 @@ PYBIND11_MODULE(_C, m) {
                      uintptr_t y2, uintptr_t stats2, uintptr_t gamma2, uintptr_t sums, uintptr_t dy,
                      uintptr_t dy2, uintptr_t dz, uintptr_t dgamma, uintptr_t dbeta,
                      uintptr_t dgamma2, uintptr_t dbeta2, int M, int C, int act, float eps,
-                     uintptr_t st) {
+                     uintptr_t st, int phases) {
     BnBwdArgs a{P<const bf16>(dout), P<const bf16>(out), P<const bf16>(y), P<const float>(stats),
                 P<const float>(gamma), P<const bf16>(y2), P<const float>(stats2),
                 P<const float>(gamma2), P<float>(sums), P<bf16>(dy), P<bf16>(dy2), P<bf16>(dz),
                 P<float>(dgamma), P<float>(dbeta), P<float>(dgamma2), P<float>(dbeta2), M, C, act,
-                eps};
+                eps, phases};
     bn_bwd_launch(a, S(st));
     check_launch("bn_bwd");
   });

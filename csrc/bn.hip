@@ -292,10 +292,12 @@ void bn_apply_launch(const BnApplyArgs& a, hipStream_t st) {
 void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
   // a.sums must be zero on entry (the engine zeroes one arena per step)
   const size_t chunks = (size_t)a.M * (a.C / 8);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 8, 256)), dim3(NT), 0,
-                     st, a);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0,
-                     st, a);
+  if (a.phases & 1)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 8, 256)), dim3(NT), 0,
+                       st, a);
+  if (a.phases & 2)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0,
+                       st, a);
 }
 
 void bn_running_launch(const BnRunEntry* tab, int nlayers, int maxC, float momentum,

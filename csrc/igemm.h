@@ -26,6 +26,18 @@ struct EpiParams {
   int group_rows;     // rows per ghost-BN group (tile never straddles a group)
   int accumulate;     // out += result
   float* slab;        // split-K workspace (set by the launcher's caller when splits > 1)
+  // Fused BN-backward reduction over the FINAL output values g (a gradient wrt the output of
+  // BN[+BN2]+act, e.g. dgrad of the next conv): dz = g * act'(bw_out);
+  //   bw_sums[0][c] += sum dz,  [1][c] += sum dz*xhat(bw_y),  [2][c] += sum dz*xhat(bw_y2)
+  // (the reduce pass of bn_bwd; bn_bwd then only applies).  Same [M][ldo] layout as out.
+  const bf16* bw_out;
+  const bf16* bw_y;
+  const float* bw_stats;   // [2][ldo] batch sum, sumsq of bw_y
+  const bf16* bw_y2;       // optional shortcut BN sharing dz
+  const float* bw_stats2;
+  float* bw_sums;          // [3][ldo] or null (feature off)
+  float bw_inv_count, bw_eps;
+  int bw_act;
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);

@@ -50,7 +50,7 @@ MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 template <int BM, int BN>
 struct Smem {
   static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
-  static constexpr int RED_BYTES = 2 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
+  static constexpr int RED_BYTES = 3 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
   static constexpr int bytes(int stages) {
     return stages * STAGE * 2 > RED_BYTES ? stages * STAGE * 2 : RED_BYTES;
   }
@@ -66,6 +66,25 @@ MA_DEV float row16_sum(float v) {
 }
 
 // ---------------------------------------------------------------- epilogue
+// BN-backward helpers (same arithmetic as bn.hip so fused and standalone reductions agree)
+MA_DEV float bn_act_mask(float out, int act) {
+  if (act == 1) return out > 0.f ? 1.f : 0.f;
+  if (act == 2) return (out > 0.f && out < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, float (&mean)[8],
+                          float (&rstd)[8]) {
+  const float4 a = *(const float4*)stats, b = *(const float4*)(stats + 4);
+  const float4 c = *(const float4*)(stats + ld), d = *(const float4*)(stats + ld + 4);
+  const float s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const float ss[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = s[k] * inv_cnt;
+    rstd[k] = rsqrtf(fmaxf(ss[k] * inv_cnt - mean[k] * mean[k], 0.f) + eps);
+  }
+}
+
 // acc[tm][tn][j] = OUT[m0 + wm*(BM/2) + tm*16 + (lane&15)][n0 + wn*(BN/2) + tn*16 + 4*(lane>>4) + j]
 template <int BM, int BN>
 MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
@@ -74,10 +93,11 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const bool stats = e.stats != nullptr;
-  float* red = (float*)smem;                       // [2][BN] sum, sumsq
-  bf16* tile = (bf16*)(smem + 2 * BN * 4);         // [BM][LDT] staged output
-  if (stats) {
-    for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
+  const bool bw = e.bw_sums != nullptr;
+  float* red = (float*)smem;                       // [2][BN] sum, sumsq  |  [3][BN] bwd sums
+  bf16* tile = (bf16*)(smem + 3 * BN * 4);         // [BM][LDT] staged output
+  if (stats || bw) {
+    for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
   }
   float4 bias[TN];
 #pragma unroll
@@ -139,20 +159,76 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
       }
     }
   }
-  // coalesced 16-byte row stores from the staged tile
+  // coalesced 16-byte row stores from the staged tile.  NT is a multiple of CPR, so every
+  // thread keeps ONE 8-column chunk for the whole loop (its BN constants load once).
   constexpr int CPR = BN / 8;
+  const int ch = tid % CPR;
+  const int colc = n0 + ch * 8;
+  float mean[8], rstd[8], mean2[8], rstd2[8], sdz[8], sx[8], sx2[8];
+  const bool two = bw && e.bw_y2 != nullptr;
+  if (bw) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = sx2[k] = mean2[k] = 0.f, rstd2[k] = 1.f;
+    const int cc = colc < N ? colc : 0;
+    bn_mean_rstd8(e.bw_stats + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean, rstd);
+    if (two) bn_mean_rstd8(e.bw_stats2 + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean2, rstd2);
+  }
   for (int i = tid; i < BM * CPR; i += NT) {
-    const int rl = i / CPR, ch = i - rl * CPR;
-    const int row = m0 + rl, col = n0 + ch * 8;
+    const int rl = i / CPR;
+    const int row = m0 + rl, col = colc;
     if (row >= M || col >= N) continue;
     bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
-    bf16* dst = e.out + (size_t)row * e.ldo + col;
+    const size_t off = (size_t)row * e.ldo + col;
+    bf16* dst = e.out + off;
     if (e.accumulate) {
       const bf16x8 o = *(const bf16x8*)dst;
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = f2bf(bf2f(v[k]) + bf2f(o[k]));
     }
     *(bf16x8*)dst = v;
+    if (bw) {
+      const bf16x8 ao = *(const bf16x8*)(e.bw_out + off);
+      const bf16x8 ay = *(const bf16x8*)(e.bw_y + off);
+      bf16x8 ay2;
+      if (two) ay2 = *(const bf16x8*)(e.bw_y2 + off);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = bf2f(v[k]) * bn_act_mask(bf2f(ao[k]), e.bw_act);
+        sdz[k] += dz;
+        sx[k] += dz * (bf2f(ay[k]) - mean[k]) * rstd[k];
+        if (two) sx2[k] += dz * (bf2f(ay2[k]) - mean2[k]) * rstd2[k];
+      }
+    }
+  }
+  if (bw) {
+    // lanes ch, ch+CPR, ... of a wave share the chunk: butterfly, then one LDS atomic per
+    // (wave, column), then one global atomic per column per block
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        sdz[k] += __shfl_xor(sdz[k], o, 64);
+        sx[k] += __shfl_xor(sx[k], o, 64);
+        if (two) sx2[k] += __shfl_xor(sx2[k], o, 64);
+      }
+    }
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        atomicAdd(&red[ch * 8 + k], sdz[k]);
+        atomicAdd(&red[BN + ch * 8 + k], sx[k]);
+        if (two) atomicAdd(&red[2 * BN + ch * 8 + k], sx2[k]);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < BN; i += NT) {
+      const int col = n0 + i;
+      if (col < N) {
+        atomicAdd(e.bw_sums + col, red[i]);
+        atomicAdd(e.bw_sums + e.ldo + col, red[BN + i]);
+        if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, red[2 * BN + i]);
+      }
+    }
   }
 }
 

@@ -48,6 +48,7 @@ struct BnBwdArgs {
   float* dbeta2;
   int M, C, act;
   float eps;
+  int phases;                    // 1 reduce, 2 apply, 3 both (reduce fused upstream -> 2)
 };
 void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st);
 

@@ -53,6 +53,7 @@ class _Mode(object):
         self.stats = {}
         self.slab = None
         self.G = 1 if not group_imgs else N // group_imgs
+        self.prereduced = {}             # block index -> BN sums already reduced by a dgrad
 
 
 class NativeEngine(object):
@@ -102,6 +103,7 @@ class NativeEngine(object):
         self.graphs = None
         self.shard = None
         self.scoring = True
+        self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
         self.sampler = sampler
         if score not in ('loss', 'gradnorm'):
             raise ValueError('score must be loss or gradnorm')
@@ -346,8 +348,10 @@ class NativeEngine(object):
         else:
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 
-    def _conv_bwd(self, m, u, dy, x, dx, accumulate):
-        """Weight gradient on the side stream (off the critical path), data gradient here."""
+    def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None):
+        """Weight gradient (optionally on a side stream), then the data gradient.  ``bw``:
+        the dgrad epilogue also reduces the BN-backward sums of the unit feeding ``dx``
+        (returns True when it did, so the caller skips bn_bwd's reduce pass)."""
         sp = m.spec[u.name]
         ws = self.s_wgrad
         if ws is not None:
@@ -363,12 +367,25 @@ class NativeEngine(object):
                 assert not accumulate
                 ops.dwconv_dgrad(dy, self._pview(u.w_seg), dx, sp.N, sp.H, sp.W, sp.C, sp.P,
                                  sp.Q, sp.stride, sp.pad)
-            return
+            return False
         if dx is not None:
+            if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
+                bw = None
             ops.conv_dgrad(dy, self.w_crsk[u.name], dx, sp, slab=m.slab,
-                           plan=m.plan[u.name, 'dgrad'], accumulate=accumulate)
+                           plan=m.plan[u.name, 'dgrad'], accumulate=accumulate, bw=bw)
+            return bw is not None
+        return False
 
-    def _bn_bwd(self, m, u, dout, out, act, dy, unit2=None, dy2=None, dz=None):
+    def _bw(self, m, u, out, act, unit2=None):
+        """Fused-reduce descriptor for the BN of ``u`` (+ shortcut BN ``unit2``) whose activation
+        output is ``out`` -- consumed by conv_dgrad(bw=...)."""
+        d = dict(out=out, y=m.buf[u.name, 'y'], stats=m.stats[u.name], sums=m.buf[u.name, 'sums'],
+                 act=act, eps=BN_EPS)
+        if unit2 is not None:
+            d.update(y2=m.buf[unit2.name, 'y'], stats2=m.stats[unit2.name])
+        return d
+
+    def _bn_bwd(self, m, u, dout, out, act, dy, unit2=None, dy2=None, dz=None, reduce=True):
         sp = m.spec[u.name]
         kw = {}
         if unit2 is not None:
@@ -378,7 +395,7 @@ class NativeEngine(object):
         ops.bn_bwd(dout, out, m.buf[u.name, 'y'], m.stats[u.name], self._gamma(u),
                    m.buf[u.name, 'sums'], dy, sp.M, u.K, act=act, eps=BN_EPS, dz=dz,
                    dgamma=self._gamma(u, True), dbeta=self._beta(u, True), zero_sums=False,
-                   **kw)
+                   reduce=reduce, **kw)
 
     def backward_block(self, m, bi):
         blk = self.lw.blocks[bi]
@@ -396,8 +413,9 @@ class NativeEngine(object):
         sc = blk.shortcut
         dy_last = m.buf[last.name, 'dy']
         dz = dx if (blk.identity and dx is not None) else None
+        pre = m.prereduced.pop(bi, False) and not blk.pool
         self._bn_bwd(m, last, dout, out, blk.final_act, dy_last, unit2=sc,
-                     dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz)
+                     dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz, reduce=not pre)
         if sc is not None:
             self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
         d = dy_last
@@ -407,13 +425,25 @@ class NativeEngine(object):
             if i > 0:
                 prev = units[i - 1]
                 da = m.buf[prev.name, 'da']
-                self._conv_bwd(m, u, d, inp, da, accumulate=False)
+                fused = self._conv_bwd(m, u, d, inp, da, accumulate=False,
+                                       bw=self._bw(m, prev, m.buf[prev.name, 'a'], prev.act))
                 dyp = m.buf[prev.name, 'dy']
-                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act, dyp)
+                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act, dyp, reduce=not fused)
                 d = dyp
             else:
                 acc = blk.identity or sc is not None
-                self._conv_bwd(m, u, d, inp, dx if u.need_dgrad else None, accumulate=acc)
+                bw = None
+                if bi > 0 and dx is not None:
+                    # this dgrad is the LAST writer of the previous block's output gradient:
+                    # reduce that block's final BN (+ shortcut BN) sums in its epilogue
+                    pb = self.lw.blocks[bi - 1]
+                    if not pb.pool:
+                        bw = self._bw(m, pb.units[-1], m.buf[bi - 1, 'out'], pb.final_act,
+                                      unit2=pb.shortcut)
+                fused = self._conv_bwd(m, u, d, inp, dx if u.need_dgrad else None,
+                                       accumulate=acc, bw=bw)
+                if fused:
+                    m.prereduced[bi - 1] = True
 
     # ------------------------------------------------------------------ data
     def set_shard(self, images_u8, labels):

@@ -36,17 +36,19 @@ def bn_apply(y, stats, gamma, beta, out, M, C, group_rows=0, act='relu', eps=1e-
 
 def bn_bwd(dout, out, y, stats, gamma, sums, dy, M, C, act='relu', eps=1e-5, y2=None,
            stats2=None, gamma2=None, dy2=None, dz=None, dgamma=None, dbeta=None, dgamma2=None,
-           dbeta2=None, zero_sums=True):
+           dbeta2=None, zero_sums=True, reduce=True):
     """BN(+shortcut BN)+activation backward for one stat group.
 
     ``sums``: [3][C] fp32 workspace that must be zero on entry; ``zero_sums=False`` when
-    the caller zeroes a whole arena once per step (one memset instead of one per layer)."""
+    the caller zeroes a whole arena once per step (one memset instead of one per layer).
+    ``reduce=False``: the sums were already reduced by the producing dgrad's epilogue
+    (``conv_dgrad(bw=...)``) -- only the apply pass runs."""
     _chk(sums, torch.float32, 'sums', 3 * C)
-    if zero_sums:
+    if zero_sums and reduce:
         sums.zero_()
     lib().bn_bwd(ptr(dout), ptr(out), ptr(y), ptr(stats), ptr(gamma), ptr(y2), ptr(stats2),
                  ptr(gamma2), ptr(sums), ptr(dy), ptr(dy2), ptr(dz), ptr(dgamma), ptr(dbeta),
-                 ptr(dgamma2), ptr(dbeta2), M, C, ACT[act], eps, stream_ptr())
+                 ptr(dgamma2), ptr(dbeta2), M, C, ACT[act], eps, stream_ptr(), 3 if reduce else 2)
     return dy
 
 

@@ -139,12 +139,35 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
                 int(accumulate), ptr(slab) if splits > 1 else 0,
                 spec.H, spec.W, Cp, spec.P, spec.Q, spec.R, spec.S, spec.stride, spec.pad,
                 spec.R * spec.S * Cp // 8, spec.K, spec.M, bm, bn, splits, False, stream_ptr(),
-                PIPE if pipe is None else pipe)
+                PIPE if pipe is None else pipe, *_NO_BW)
     return out
 
 
-def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, pipe=None):
-    """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2."""
+_NO_BW = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0)
+_ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
+
+
+def _bw_args(bw, Mx, Cp):
+    """Fused BN-backward reduction of the dgrad output (see EpiParams in csrc/igemm.h).
+
+    ``bw``: dict(out=, y=, stats=, sums=, act=, eps=, [y2=, stats2=]) -- the BN(+shortcut BN)
+    + activation whose output gradient this dgrad produces."""
+    if bw is None:
+        return _NO_BW
+    for k in ('out', 'y', 'y2'):
+        if bw.get(k) is not None:
+            _chk(bw[k], torch.bfloat16, 'bw.' + k, Mx * Cp)
+    _chk(bw['sums'], torch.float32, 'bw.sums', 3 * Cp)
+    _chk(bw['stats'], torch.float32, 'bw.stats', 2 * Cp)
+    return (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw.get('y2')),
+            ptr(bw.get('stats2')), ptr(bw['sums']), 1.0 / Mx, float(bw.get('eps', 1e-5)),
+            _ACT[bw.get('act')])
+
+
+def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, pipe=None,
+               bw=None):
+    """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2.  ``bw``: also reduce
+    the BN-backward sums of the (final, post-accumulate) dx in the epilogue."""
     if spec.stride not in (1, 2):
         raise ValueError('dgrad supports stride 1/2')
     if spec.K % 8:
@@ -161,7 +184,7 @@ def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=Fals
                 ptr(slab) if splits > 1 else 0,
                 spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
                 spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, True, stream_ptr(),
-                PIPE if pipe is None else pipe)
+                PIPE if pipe is None else pipe, *_bw_args(bw, Mx, Cp))
     return dx
 
 

@@ -126,6 +126,50 @@ def test_conv_dgrad(case):
     close(ops.from_nhwc(dx2.view(N, H, W, spec.Cp), C), 2 * xr.grad, rtol=3e-2)
 
 
+@pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] % 8 == 0])
+@pytest.mark.parametrize('two', [False, True])
+def test_conv_dgrad_fused_bn_backward_reduce(case, two):
+    """dgrad epilogue reduces sum(dz), sum(dz*xhat) [, sum(dz*xhat2)] of its FINAL output
+    (after accumulate), dz = dx * relu'(out) -- vs torch fp32 on the produced dx."""
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, dgrad_plan, slab_bytes
+    N, H, W, C, K, R, S, st, pd = case
+    x, w = _mk(case, 5)
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    Mx = N * H * W
+    gy = ops.to_nhwc(bf(torch.randn(N, K, spec.P, spec.Q, device=DEV)))
+    _, wt = ops.pack_conv_weight(w)
+    plan = dgrad_plan(spec)
+    slab = torch.zeros(max(1, slab_bytes(Mx, C, *plan) // 4), device=DEV)
+    y = bf(torch.randn(Mx, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    y2 = bf(torch.randn(Mx, C, device=DEV)).to(torch.bfloat16)
+    out = bf(torch.relu(torch.randn(Mx, C, device=DEV))).to(torch.bfloat16)
+    stats = torch.stack([y.float().sum(0), y.float().pow(2).sum(0)]).contiguous()
+    stats2 = torch.stack([y2.float().sum(0), y2.float().pow(2).sum(0)]).contiguous()
+    sums = torch.zeros(3, C, device=DEV)
+    prior = bf(torch.randn(Mx, C, device=DEV)).to(torch.bfloat16)
+    dx = prior.clone()
+    bw = dict(out=out, y=y, stats=stats, sums=sums, act='relu', eps=1e-5)
+    if two:
+        bw.update(y2=y2, stats2=stats2)
+    ops.conv_dgrad(gy, wt, dx, spec, slab=slab, plan=plan, accumulate=True, bw=bw)
+    d = dx.float()
+    dz = d * (out.float() > 0)
+
+    def xhat(t, s):
+        mu = s[0] / Mx
+        var = (s[1] / Mx - mu * mu).clamp_min(0)
+        return (t.float() - mu) / torch.sqrt(var + 1e-5)
+    ref0 = dz.sum(0)
+    ref1 = (dz * xhat(y, stats)).sum(0)
+    close(sums[0], ref0, 1e-3, 1e-2)
+    close(sums[1], ref1, 1e-3, 1e-2)
+    if two:
+        close(sums[2], (dz * xhat(y2, stats2)).sum(0), 1e-3, 1e-2)
+    else:
+        assert float(sums[2].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_wgrad(case):
     ops = _ops()
