@@ -42,6 +42,25 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
     check_launch("igemm");
   });
+  m.def("conv_bwd_pair", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int ldo, int accumulate,
+                            uintptr_t slab, int SH, int SW, int SC, int RP, int RQ, int R, int Sk,
+                            int stride, int pad, int Kc, int Ncols, int M, int bm, int bn,
+                            int splits, uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats,
+                            uintptr_t bw_y2, uintptr_t bw_stats2, uintptr_t bw_sums,
+                            float bw_inv_count, float bw_eps, int bw_act, uintptr_t x,
+                            uintptr_t dw, int N, int H, int W, int C, int Pp, int Q, int K,
+                            int Creal, int wbm, int wbn, int wsplits, uintptr_t st) {
+    ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
+    EpiParams e{P<bf16>(dx), ldo, nullptr, nullptr, 0, M, accumulate, P<float>(slab),
+                P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats),
+                P<const bf16>(bw_y2), P<const float>(bw_stats2), P<float>(bw_sums), bw_inv_count,
+                bw_eps, bw_act};
+    WgradGeom wg{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal};
+    const int ok = conv_bwd_pair_launch(P<const bf16>(dy), P<const bf16>(wt), g, e, bm, bn, splits,
+                                        P<const bf16>(x), wg, P<float>(dw), wbm, wbn, wsplits, S(st));
+    if (ok) check_launch("conv_bwd_pair");
+    return ok;
+  });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};
     g.M = M;

@@ -53,3 +53,8 @@ struct WgradGeom {
 };
 void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
                   int splits, hipStream_t st);
+
+// dgrad (TRANS igemm) + wgrad in ONE launch (returns 0 if the tile pair is not instantiated)
+int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
+                         int bm, int bn, int splits, const bf16* x, const WgradGeom& wg, float* dw,
+                         int wbm, int wbn, int wsplits, hipStream_t st);

@@ -37,6 +37,7 @@
 // same epilogue inside the launch (see finish()).
 #include "common.h"
 #include "igemm.h"
+#include "wgrad_body.h"
 
 namespace {
 
@@ -360,16 +361,16 @@ constexpr int SEM_INTS = 1024;   // tile counters at the head of the slab (4 KB)
 
 template <int BM, int BN>
 MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
-                   int m0, int n0) {
+                   int m0, int n0, int bx, int by, int gx, int gy) {
   constexpr int TM = BM / 32, TN = BN / 32;
   if (e.slab) {
-    const int ntiles = gridDim.x;
-    const int splits = gridDim.y;
+    const int ntiles = gx;
+    const int splits = gy;
     int* sem = (int*)e.slab;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(e.slab + SEM_INTS), 0, 0x7fffffff,
                                                       0x00020000);
     const int tile_bytes = TM * TN * NT * 16;
-    const int mine = (blockIdx.y * ntiles + blockIdx.x) * tile_bytes + threadIdx.x * 16;
+    const int mine = (by * ntiles + bx) * tile_bytes + threadIdx.x * 16;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -380,18 +381,17 @@ MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& 
     int* flag = (int*)smem;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(&sem[blockIdx.x], 1, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+      const int old = __hip_atomic_fetch_add(&sem[bx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == splits - 1;
-      if (last) __hip_atomic_store(&sem[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (last) __hip_atomic_store(&sem[bx], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the ticket
     for (int sp = 0; sp < splits; ++sp) {
-      if (sp == (int)blockIdx.y) continue;
-      const int base = (sp * ntiles + blockIdx.x) * tile_bytes + threadIdx.x * 16;
+      if (sp == by) continue;
+      const int base = (sp * ntiles + bx) * tile_bytes + threadIdx.x * 16;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -406,23 +406,22 @@ MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& 
 }
 
 // ---------------------------------------------------------------- register-staged loop
+// One (tile bx, K-split by) of the NT GEMM; gx tiles x gy splits in the launch.
 template <int BM, int BN, bool TRANS>
-__global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict__ src,
-                                                          const bf16* __restrict__ wt,
-                                                          ConvGeom g, EpiParams e,
-                                                          int ktiles_per_split) {
+MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__ wt,
+                          const ConvGeom& g, const EpiParams& e, int ktiles_per_split, char* smem,
+                          int bx, int by, int gx, int gy) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;  // rows per thread for A / B staging
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
   bf16* sA = (bf16*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int ntn = (g.Ncols + BN - 1) / BN;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+  const int mt = bx / ntn, nt = bx - mt * ntn;
   const int m0 = mt * BM, n0 = nt * BN;
   const int ktiles = (g.Kc + 7) / 8;
-  const int kt0 = blockIdx.y * ktiles_per_split;
+  const int kt0 = by * ktiles_per_split;
   const int kt1 = min(ktiles, kt0 + ktiles_per_split);
   const int Kelems = g.Kc * 8;
   const int cc = tid & 7;
@@ -493,7 +492,17 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
       buf ^= 1;
     }
   }
-  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
+  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, bx, by, gx, gy);
+}
+
+template <int BM, int BN, bool TRANS>
+__global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict__ src,
+                                                          const bf16* __restrict__ wt,
+                                                          ConvGeom g, EpiParams e,
+                                                          int ktiles_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
+  igemm_nt_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x, blockIdx.y,
+                               gridDim.x, gridDim.y);
 }
 
 // ---------------------------------------------------------------- LDS-DMA ring loop
@@ -587,7 +596,7 @@ __global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restric
   }
   wait_vmcnt<0>();
   __syncthreads();
-  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0);
+  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
 }
 
 template <int BM, int BN, bool TRANS>
@@ -603,18 +612,59 @@ void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiPa
     hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
 }
 
-template <int BM, int BN, bool TRANS>
-void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
-                int pipe, hipStream_t st) {
+// split-K decomposition (clamped; no split when the tile counters would not fit)
+inline void ig_grid(const ConvGeom& g, int BM, int BN, int splits, int& gx, int& per, int& gy) {
   const int mtiles = (g.M + BM - 1) / BM, ntiles = (g.Ncols + BN - 1) / BN;
   const int ktiles = (g.Kc + 7) / 8;
   splits = splits < 1 ? 1 : (splits > ktiles ? ktiles : splits);
-  int per = (ktiles + splits - 1) / splits;
-  splits = (ktiles + per - 1) / per;
-  if (mtiles * ntiles > SEM_INTS) splits = 1, per = ktiles;   // no counter slot: no split
-  dim3 grid(mtiles * ntiles, splits);
-  if (splits == 1) e.slab = nullptr;
-  launch_main<BM, BN, TRANS>(src, wt, g, e, per, grid, pipe, st);
+  per = (ktiles + splits - 1) / splits;
+  gy = (ktiles + per - 1) / per;
+  gx = mtiles * ntiles;
+  if (gx > SEM_INTS) gy = 1, per = ktiles;
+}
+
+template <int BM, int BN, bool TRANS>
+void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
+                int pipe, hipStream_t st) {
+  int gx, per, gy;
+  ig_grid(g, BM, BN, splits, gx, per, gy);
+  if (gy == 1) e.slab = nullptr;
+  launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), pipe, st);
+}
+
+// ---------------------------------------------------------------- dgrad + wgrad pair launch
+// The two backward GEMMs of a conv read the same dy and are independent; at small batch each
+// alone leaves most of the 256 CUs idle, and a second stream costs a cross-queue graph edge per
+// layer.  One launch runs both: blocks [0, nw) are weight-gradient tiles (the longer reduction
+// goes first), the rest data-gradient tiles, in one LDS allocation sized for the larger body.
+template <int DBM, int DBN, int WBM, int WBN>
+__global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict__ dy,
+                                                          const bf16* __restrict__ wt, ConvGeom g,
+                                                          EpiParams e, int dper, int dgx, int dgy,
+                                                          const bf16* __restrict__ x,
+                                                          WgradGeom wg, float* __restrict__ dw,
+                                                          int wper, int wgx, int wgy) {
+  constexpr int DB = Smem<DBM, DBN>::bytes(2), WB = wgb::WgSmem<WBM, WBN>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[DB > WB ? DB : WB];
+  const int nw = wgx * wgy;
+  const int b = blockIdx.x;
+  if (b < nw) {
+    wgb::wgrad_body<WBM, WBN>(dy, x, wg, dw, wper, (bf16*)smem, b % wgx, b / wgx, wgy);
+  } else {
+    const int d = b - nw;
+    igemm_nt_body<DBM, DBN, true>(dy, wt, g, e, dper, smem, d % dgx, d / dgx, dgx, dgy);
+  }
+}
+
+template <int DBM, int DBN, int WBM, int WBN>
+void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
+              const bf16* x, const WgradGeom& wg, float* dw, int wsplits, hipStream_t st) {
+  int dgx, dper, dgy, wgx, wper, wgy;
+  ig_grid(g, DBM, DBN, splits, dgx, dper, dgy);
+  if (dgy == 1) e.slab = nullptr;
+  wgb::wg_grid(wg, WBM, WBN, wsplits, wgx, wper, wgy);
+  hipLaunchKernelGGL((bwd_pair_kernel<DBM, DBN, WBM, WBN>), dim3(dgx * dgy + wgx * wgy), dim3(NT),
+                     0, st, dy, wt, g, e, dper, dgx, dgy, x, wg, dw, wper, wgx, wgy);
 }
 
 }  // namespace
@@ -638,4 +688,29 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiP
   MA_CASE(64, 64)
   MA_CASE(256, 64)
 #undef MA_CASE
+}
+
+int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
+                         int bm, int bn, int splits, const bf16* x, const WgradGeom& wg, float* dw,
+                         int wbm, int wbn, int wsplits, hipStream_t st) {
+#define MA_W(DBM_, DBN_, WBM_, WBN_)                                                   \
+  if (wbm == WBM_ && wbn == WBN_) {                                                   \
+    pair_cfg<DBM_, DBN_, WBM_, WBN_>(dy, wt, g, e, splits, x, wg, dw, wsplits, st);   \
+    return 1;                                                                         \
+  }
+#define MA_D(DBM_, DBN_)                                                               \
+  if (bm == DBM_ && bn == DBN_) {                                                     \
+    MA_W(DBM_, DBN_, 128, 128)                                                        \
+    MA_W(DBM_, DBN_, 128, 64)                                                         \
+    MA_W(DBM_, DBN_, 64, 128)                                                         \
+    MA_W(DBM_, DBN_, 64, 64)                                                          \
+  }
+  MA_D(128, 128)
+  MA_D(128, 64)
+  MA_D(64, 128)
+  MA_D(64, 64)
+  MA_D(256, 64)
+#undef MA_D
+#undef MA_W
+  return 0;   // no instantiation: caller launches the two kernels separately
 }

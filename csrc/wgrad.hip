@@ -20,182 +20,28 @@
 // Split-K over pixels (gridDim.y) accumulates with fp32 atomics into the flat
 // gradient buffer; without splitting it stores.  The output is written in the
 // engine's master layout [K][R][S][Creal] (channel padding dropped).
-#include "common.h"
-#include "igemm.h"
+
+#include "wgrad_body.h"
 
 namespace {
-constexpr int NT = 256;
-constexpr int BKP = 64;  // pixels per stage
-
-typedef short short4_t __attribute__((ext_vector_type(4)));
-
-MA_DEV bf16x4 tr_read(const bf16* p) {
-  short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) short4_t*)(p));
-  return __builtin_bit_cast(bf16x4, v);
-}
+using namespace wgb;
+constexpr int NT = WG_NT;
+constexpr int BKP = WG_BKP;
 
 template <int BM, int BN>
 __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const bf16* __restrict__ dy,
                                                        const bf16* __restrict__ x, WgradGeom g,
                                                        float* __restrict__ dw, int ptiles_per_split) {
-  constexpr int LDA = BM + 16, LDB = BN + 16;
-  constexpr int STAGE = BKP * (LDA + LDB);
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int ACH = BM / 8, BCH = BN / 8;          // chunks per row
-  constexpr int AR = BKP * ACH / NT, BR = BKP * BCH / NT;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int C8 = g.C >> 3;
-  const int Kc = g.R * g.S * C8;                       // reduction-free column chunks
-  const int ncols = Kc * 8;
-  const int ntn = (ncols + BN - 1) / BN;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int npix = g.N * g.P * g.Q;
-  const int ptiles = (npix + BKP - 1) / BKP;
-  const int pt0 = blockIdx.y * ptiles_per_split;
-  const int pt1 = min(ptiles, pt0 + ptiles_per_split);
-
-  // fixed column chunk per thread for the x tile
-  const int bcc = tid % BCH;
-  const int jc = n0 / 8 + bcc;
-  int xr = 0, xs = 0, xc8 = 0;
-  const bool jval = jc < Kc;
-  if (jval) {
-    const int rs = jc / C8;
-    xc8 = jc - rs * C8;
-    xr = rs / g.S;
-    xs = rs - xr * g.S;
-  }
-  const int acc_ = tid % ACH;
-
-  u32x4 ra[AR], rb[BR];
-  auto load_stage = [&](int pt) {
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int row = tid / ACH + i * (NT / ACH);
-      const int pix = pt * BKP + row;
-      const int k = m0 + acc_ * 8;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (pix < npix && k < g.K) v = *(const u32x4*)(dy + (size_t)pix * g.K + k);
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int row = tid / BCH + i * (NT / BCH);
-      const int pix = pt * BKP + row;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (pix < npix && jval) {
-        const int pq = g.P * g.Q;
-        const int n = pix / pq, rem = pix - n * pq;
-        const int p = rem / g.Q, q = rem - p * g.Q;
-        const int h = p * g.stride - g.pad + xr, ww = q * g.stride - g.pad + xs;
-        if (h >= 0 && ww >= 0 && h < g.H && ww < g.W)
-          v = *(const u32x4*)(x + ((size_t)(n * g.H + h) * g.W + ww) * g.C + xc8 * 8);
-      }
-      rb[i] = v;
-    }
-  };
-  auto store_stage = [&](int buf) {
-    bf16* a = smem + buf * STAGE;
-    bf16* b = a + BKP * LDA;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int row = tid / ACH + i * (NT / ACH);
-      *(u32x4*)(a + row * LDA + acc_ * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int row = tid / BCH + i * (NT / BCH);
-      *(u32x4*)(b + row * LDB + bcc * 8) = rb[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int g4 = lane >> 4, li = lane & 15;
-  const int tq = li >> 2, tp = li & 3;
-  if (pt0 < pt1) {
-    load_stage(pt0);
-    store_stage(0);
-    __syncthreads();
-    int buf = 0;
-    for (int pt = pt0; pt < pt1; ++pt) {
-      const bool more = pt + 1 < pt1;
-      if (more) load_stage(pt + 1);
-      const bf16* a = smem + buf * STAGE;
-      const bf16* b = a + BKP * LDA;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fa[TM], fb[TN];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int row = kk * 32 + 16 * h + 4 * g4 + tq;
-#pragma unroll
-          for (int tm = 0; tm < TM; ++tm) {
-            const bf16x4 v = tr_read(a + row * LDA + wm * (BM / 2) + tm * 16 + 4 * tp);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fa[tm][4 * h + e] = v[e];
-          }
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) {
-            const bf16x4 v = tr_read(b + row * LDB + wn * (BN / 2) + tn * 16 + 4 * tp);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fb[tn][4 * h + e] = v[e];
-          }
-        }
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
-      }
-      if (more) store_stage(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
-    }
-  }
-
-  const bool atomic = gridDim.y > 1;
-  const int RSCr = g.R * g.S * g.Creal;
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int col = n0 + wn * (BN / 2) + tn * 16 + li;
-    if (col >= ncols) continue;
-    const int rs = col / g.C, c = col - rs * g.C;
-    if (c >= g.Creal) continue;
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = m0 + wm * (BM / 2) + tm * 16 + g4 * 4 + j;
-        if (k >= g.K) continue;
-        float* dst = dw + (size_t)k * RSCr + rs * g.Creal + c;
-        if (atomic) atomicAdd(dst, acc[tm][tn][j]);
-        else *dst = acc[tm][tn][j];
-      }
-    }
-  }
+  __shared__ __attribute__((aligned(16))) bf16 smem[WgSmem<BM, BN>::STAGE * 2];
+  wgrad_body<BM, BN>(dy, x, g, dw, ptiles_per_split, smem, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
 template <int BM, int BN>
 void wlaunch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int splits,
              hipStream_t st) {
-  const int ncols = g.R * g.S * g.C;
-  const int mtiles = (g.K + BM - 1) / BM, ntiles = (ncols + BN - 1) / BN;
-  const int ptiles = (g.N * g.P * g.Q + BKP - 1) / BKP;
-  splits = splits < 1 ? 1 : (splits > ptiles ? ptiles : splits);
-  const int per = (ptiles + splits - 1) / splits;
-  splits = (ptiles + per - 1) / per;
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(mtiles * ntiles, splits), dim3(NT), 0, st, dy, x,
-                     g, dw, per);
+  int gx, per, gy;
+  wg_grid(g, BM, BN, splits, gx, per, gy);
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(gx, gy), dim3(NT), 0, st, dy, x, g, dw, per);
 }
 }  // namespace
 

@@ -104,6 +104,7 @@ class NativeEngine(object):
         self.shard = None
         self.scoring = True
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
+        self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
         self.sampler = sampler
         if score not in ('loss', 'gradnorm'):
             raise ValueError('score must be loss or gradnorm')
@@ -353,6 +354,15 @@ class NativeEngine(object):
         the dgrad epilogue also reduces the BN-backward sums of the unit feeding ``dx``
         (returns True when it did, so the caller skips bn_bwd's reduce pass)."""
         sp = m.spec[u.name]
+        if (dx is not None and not u.depthwise and self.s_wgrad is None and self.pair_bwd
+                and sp.K % 8 == 0):
+            if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
+                bw = None
+            # dgrad + wgrad of this conv in ONE launch (they share dy and are independent)
+            ops.conv_bwd(dy, self.w_crsk[u.name], dx, x, self._pview(u.w_seg, grad=True), sp,
+                         dplan=m.plan[u.name, 'dgrad'], wplan=m.plan[u.name, 'wgrad'],
+                         slab=m.slab, accumulate=accumulate, bw=bw)
+            return bw is not None
         ws = self.s_wgrad
         if ws is not None:
             ev = torch.cuda.Event()

@@ -68,7 +68,7 @@ def _chk(t, dtype, name, numel=None):
         raise ValueError('%s too small: %d < %d' % (name, t.numel(), numel))
 
 
-from .conv import (ConvSpec, conv_fwd, conv_dgrad, conv_wgrad, pick_tiles, pack_conv_weight,  # noqa: E402
+from .conv import (ConvSpec, conv_fwd, conv_dgrad, conv_wgrad, conv_bwd, pick_tiles, pack_conv_weight,  # noqa: E402
                    to_nhwc, from_nhwc)
 from .bn import bn_apply, bn_bwd, BnRunTable  # noqa: E402
 from .head import head_fwd, head_bwd  # noqa: E402
@@ -77,7 +77,7 @@ from .table import ImportanceTable  # noqa: E402
 from .optim import FlatOptimizer  # noqa: E402
 from .misc import quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad  # noqa: E402
 
-__all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_dgrad', 'conv_wgrad', 'pick_tiles',
+__all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
            'pack_conv_weight', 'to_nhwc', 'from_nhwc', 'bn_apply', 'bn_bwd', 'BnRunTable',
            'head_fwd', 'head_bwd', 'pool_build', 'is_sample', 'gather', 'ImportanceTable',
            'FlatOptimizer', 'quantize', 'pool2d_fwd', 'maxpool2d_bwd',

@@ -202,6 +202,36 @@ def conv_wgrad(dy, x, dw, spec: ConvSpec, plan=None):
     return dw
 
 
+def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=None,
+             accumulate=False, bw=None):
+    """Both backward GEMMs of one conv in ONE launch (csrc/igemm.hip bwd_pair_kernel):
+    dx (= conv_dgrad, optional fused BN-backward reduce ``bw``) and dw (= conv_wgrad)."""
+    if spec.stride not in (1, 2) or spec.K % 8:
+        raise ValueError('conv_bwd needs stride 1/2 and K % 8 == 0')
+    Cp = spec.Cp
+    _chk(dy, torch.bfloat16, 'dy', spec.M * spec.K)
+    _chk(wt, torch.bfloat16, 'wt', Cp * spec.R * spec.S * spec.K)
+    _chk(dx, torch.bfloat16, 'dx', spec.N * spec.H * spec.W * Cp)
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
+    _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
+    bm, bn, splits = dplan or dgrad_plan(spec)
+    wbm, wbn, wsplits = wplan or wgrad_plan(spec)
+    Mx = spec.N * spec.H * spec.W
+    if splits > 1:
+        slab = _slab(slab, slab_bytes(Mx, Cp, bm, bn, splits), dy.device)
+    ok = lib().conv_bwd_pair(
+        ptr(dy), ptr(wt), ptr(dx), Cp, int(accumulate), ptr(slab) if splits > 1 else 0,
+        spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
+        spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, *_bw_args(bw, Mx, Cp),
+        ptr(x), ptr(dw), spec.N, spec.H, spec.W, Cp, spec.P, spec.Q, spec.K, spec.C, wbm, wbn,
+        wsplits, stream_ptr())
+    if not ok:
+        conv_wgrad(dy, x, dw, spec, plan=(wbm, wbn, wsplits))
+        conv_dgrad(dy, wt, dx, spec, slab=slab, plan=(bm, bn, splits), accumulate=accumulate,
+                   bw=bw)
+    return dx, dw
+
+
 # ----------------------------------------------------------------------- layout helpers
 def to_nhwc(x, cpad=None):
     """NCHW float -> NHWC bf16 with channels padded to ``cpad`` (default: next multiple of 8)."""

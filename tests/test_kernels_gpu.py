@@ -170,6 +170,39 @@ def test_conv_dgrad_fused_bn_backward_reduce(case, two):
         assert float(sums[2].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0])
+def test_conv_bwd_pair_matches_separate_launches(case):
+    """dgrad + wgrad in one launch == the two standalone kernels (bitwise for dx when K is not
+    split, allclose for the atomically accumulated dw) and == torch."""
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, dgrad_plan, slab_bytes, wgrad_plan
+    N, H, W, C, K, R, S, st, pd = case
+    x, w = _mk(case, 3)
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    gy = bf(torch.randn(N, K, spec.P, spec.Q, device=DEV))
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=st, padding=pd).backward(gy)
+    _, wt = ops.pack_conv_weight(w)
+    dplan, wplan = dgrad_plan(spec), wgrad_plan(spec)
+    Mx = N * H * W
+    slab = torch.zeros(max(1, slab_bytes(Mx, spec.Cp, *dplan) // 4), device=DEV)
+    xn, gyn = ops.to_nhwc(x), ops.to_nhwc(gy)
+    dx = torch.empty(Mx, spec.Cp, dtype=torch.bfloat16, device=DEV)
+    dw = torch.zeros(K * R * S * C, device=DEV)
+    ops.conv_bwd(gyn, wt, dx, xn, dw, spec, dplan=dplan, wplan=wplan, slab=slab)
+    dx2 = torch.empty_like(dx)
+    dw2 = torch.zeros_like(dw)
+    ops.conv_dgrad(gyn, wt, dx2, spec, slab=slab, plan=dplan)
+    ops.conv_wgrad(gyn, xn, dw2, spec, plan=wplan)
+    if dplan[2] == 1:
+        assert torch.equal(dx, dx2)
+    close(dx.float(), dx2.float(), 1e-2, 1e-2)
+    close(dw, dw2, 1e-4, 1e-4)
+    close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
+    close(dw.view(K, R, S, C).permute(0, 3, 1, 2), wr.grad, 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_wgrad(case):
     ops = _ops()
