@@ -160,8 +160,9 @@ PYBIND11_MODULE(_C, m) {
                         uintptr_t meters, int Pn, int B, int group, int importance, float alpha,
                         float ema_alpha, uint32_t seed, uintptr_t st, int alias, uintptr_t gl,
                         int W) {
-    if (group <= 0 || Pn % group || Pn / group > 256)
-      throw std::runtime_error("is_sample: pool must be 1..256 groups of `group` samples");
+    if (group <= 0 || Pn % group || Pn / group > 1024)
+      throw std::runtime_error("is_sample: pool must be 1..1024 groups of `group` samples");
+    if (alias && is_sample_lds(Pn, 1) > 128 * 1024) alias = 0;   // table beyond LDS: inverse CDF
     IsSampleArgs a{P<const float>(losses), P<float>(ema), P<int64_t>(ctrl), P<int>(idx), P<float>(w),
                    P<float>(meters), Pn, B, group, importance, alpha, ema_alpha, seed, alias,
                    P<const float>(gl), W};

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
 }
 
 constexpr int IS_T = 1024;
-constexpr int MAX_GROUPS = 256;   // pool batches per pool
+constexpr int MAX_GROUPS = 1024;  // pool batches per pool
+constexpr int IS_LDS_MAX = 128 * 1024;   // dynamic LDS cap (static gsum[] rides on top)
 
 __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -137,32 +138,94 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
   const float total = tsum[IS_T - 1];
   const int64_t dc = a.ctrl[1];
   if (a.alias) {
-    // Walker/Vose alias table in LDS (prob in q[], alias[]), then O(1) draws.
-    float* q = tsum + IS_T + 64;                 // [P]
-    int* al = (int*)(q + a.P);                   // [P]
-    int* small = al + a.P;                       // [P]
-    int* large = small + a.P;                    // [P]
+    // Walker alias table built in PARALLEL in LDS (prob q[], alias al[]), then O(1) draws.
+    // Sequential Vose pairs one light with one heavy at a time (a P-long dependent chain:
+    // 70 us at P=320 on one lane).  The sweep it performs has a closed form (the PSA of
+    // Huebschle-Schneider & Sanders): with the lights' exclusive deficit prefix D_i and the
+    // heavies' exclusive excess prefix S_k,
+    //   light i's alias  = heavy k, the smallest k with D_i <= S_{k+1};
+    //   heavy k's prob   = 1 - (D_next - S_{k+1}), D_next = first light deficit prefix > S_{k+1},
+    //   heavy k's alias  = heavy k+1 (it was topped up by the next heavy in the sweep),
+    // so the build is three block scans + two binary searches per item.
+    float* q = tsum + IS_T + 64;                 // [P] bucket probability
+    int* al = (int*)(q + a.P);                   // [P] alias
+    int* Lidx = al + a.P;                        // [P] light items in order
+    int* Hidx = Lidx + a.P;                      // [P] heavy items in order
+    float* Ld = (float*)(Hidx + a.P);            // [P] exclusive deficit prefix of lights
+    float* Hs = Ld + a.P;                        // [P+1] exclusive excess prefix of heavies
+    int* ccnt = (int*)(Hs + a.P + 1);            // [IS_T] light-count scan
+    float* cdef = (float*)(ccnt + IS_T);         // [IS_T] deficit scan
+    float* cexc = cdef + IS_T;                   // [IS_T] excess scan
     const float scale = (float)a.P / total;
-    for (int i = tid; i < a.P; i += IS_T) {
-      q[i] = p[i] * scale;
-      al[i] = i;
+    int lc = 0;
+    float ld = 0.f, he = 0.f;
+    for (int i = s0; i < s1; ++i) {
+      const float v = p[i] * scale;
+      q[i] = v;
+      if (v < 1.f) {
+        ++lc;
+        ld += 1.f - v;
+      } else {
+        he += v - 1.f;
+      }
     }
+    ccnt[tid] = lc;
+    cdef[tid] = ld;
+    cexc[tid] = he;
     __syncthreads();
-    if (tid == 0) {
-      int ns = 0, nl = 0;
-      for (int i = 0; i < a.P; ++i) {
-        if (q[i] < 1.f) small[ns++] = i;
-        else large[nl++] = i;
+    for (int off = 1; off < IS_T; off <<= 1) {
+      const int c_ = tid >= off ? ccnt[tid - off] : 0;
+      const float d_ = tid >= off ? cdef[tid - off] : 0.f;
+      const float e_ = tid >= off ? cexc[tid - off] : 0.f;
+      __syncthreads();
+      ccnt[tid] += c_;
+      cdef[tid] += d_;
+      cexc[tid] += e_;
+      __syncthreads();
+    }
+    {
+      int li = tid > 0 ? ccnt[tid - 1] : 0, hi = s0 - li;
+      float dd = tid > 0 ? cdef[tid - 1] : 0.f, ee = tid > 0 ? cexc[tid - 1] : 0.f;
+      for (int i = s0; i < s1; ++i) {
+        const float v = q[i];
+        if (v < 1.f) {
+          Lidx[li] = i;
+          Ld[li++] = dd;
+          dd += 1.f - v;
+        } else {
+          Hidx[hi] = i;
+          Hs[hi++] = ee;
+          ee += v - 1.f;
+        }
       }
-      while (ns > 0 && nl > 0) {
-        const int s = small[--ns], l = large[--nl];
-        al[s] = l;                               // q[s] stays as prob[s]
-        q[l] = (q[l] + q[s]) - 1.f;
-        if (q[l] < 1.f) small[ns++] = l;
-        else large[nl++] = l;
+    }
+    const int nl = ccnt[IS_T - 1], nh = a.P - nl;
+    if (tid == 0) Hs[nh] = cexc[IS_T - 1];
+    __syncthreads();
+    const float dtot = cdef[IS_T - 1];
+    for (int j = tid; j < nl; j += IS_T) {      // lights: who tops me up
+      const float D = Ld[j];
+      int lo = 0, hi = nh - 1;                   // smallest k with D <= Hs[k+1]
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (D <= Hs[mid + 1]) hi = mid;
+        else lo = mid + 1;
       }
-      while (nl > 0) q[large[--nl]] = 1.f;
-      while (ns > 0) q[small[--ns]] = 1.f;       // numerical leftovers
+      al[Lidx[j]] = nh > 0 ? Hidx[lo] : Lidx[j];
+      if (nh == 0) q[Lidx[j]] = 1.f;             // numerically all-light: uniform fallback
+    }
+    for (int k = tid; k < nh; k += IS_T) {      // heavies: what is left in my own bucket
+      const float S1 = Hs[k + 1];
+      int lo = 0, hi = nl;                       // first light with Ld > S1
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (Ld[mid] > S1) hi = mid;
+        else lo = mid + 1;
+      }
+      const float Dn = lo < nl ? Ld[lo] : dtot;
+      const float r = (k == nh - 1) ? 1.f : fminf(1.f, fmaxf(0.f, 1.f - (Dn - S1)));
+      q[Hidx[k]] = r;
+      al[Hidx[k]] = k + 1 < nh ? Hidx[k + 1] : Hidx[k];
     }
     __syncthreads();
     for (int d = tid; d < a.B; d += IS_T) {
@@ -227,9 +290,19 @@ void pool_build_launch(const PoolBuildArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(pool_build_kernel, dim3(a.P), dim3(256), 0, st, a);
 }
 
+size_t is_sample_lds(int P, int alias) {
+  return (size_t)(P + IS_T + 64) * sizeof(float) +
+         (alias ? (6 * (size_t)P + 1 + 3 * IS_T) * 4 : 0);
+}
+
 void is_sample_launch(const IsSampleArgs& a, hipStream_t st) {
-  const size_t shm = (size_t)(a.P + IS_T + 64) * sizeof(float) + (a.alias ? 4 * (size_t)a.P * 4 : 0);
-  hipLaunchKernelGGL(is_sample_kernel, dim3(1), dim3(IS_T), shm, st, a);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)is_sample_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        IS_LDS_MAX);
+    attr = true;
+  }
+  hipLaunchKernelGGL(is_sample_kernel, dim3(1), dim3(IS_T), is_sample_lds(a.P, a.alias), st, a);
 }
 
 void gather_launch(const GatherArgs& a, hipStream_t st) {

@@ -122,6 +122,7 @@ struct IsSampleArgs {
   int W;
 };
 void is_sample_launch(const IsSampleArgs& a, hipStream_t st);
+size_t is_sample_lds(int P, int alias);   // dynamic LDS bytes (<= 128 KB: alias up to P ~ 4k)
 
 struct GatherArgs {
   const bf16* pool;              // [P][pix*8]

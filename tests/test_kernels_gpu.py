@@ -413,11 +413,12 @@ def test_pool_build_epoch_permutation_and_normalisation():
     assert torch.isfinite(pool.float()).all()
 
 
-@pytest.mark.parametrize('alias', [True, False])
-def test_is_sample_ema_and_distribution(alias):
+@pytest.mark.parametrize('alias,P', [(True, 320), (False, 320), (True, 2048)])
+def test_is_sample_ema_and_distribution(alias, P):
+    """EMA replay exact; draws (parallel-built alias table or inverse CDF) match p by chi^2."""
     ops = _ops()
     from mercury_amd.utils import EMAverage
-    P, B = 320, 32
+    B = 32
     torch.manual_seed(0)
     losses = torch.rand(P, device=DEV) ** 3 * 3      # skewed: many light, few heavy bins
     ema = torch.zeros(2, device=DEV)
@@ -427,7 +428,7 @@ def test_is_sample_ema_and_distribution(alias):
     ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1,
                   alias=alias)
     ref = EMAverage()
-    for j in range(10):
+    for j in range(P // 32):
         ref.update(losses[:32 * (j + 1)].mean().item())
     assert abs(ema[0].item() - ref.value) < 1e-5
     p = (losses + 0.5 * ema[0]) / (losses + 0.5 * ema[0]).sum()
@@ -435,7 +436,7 @@ def test_is_sample_ema_and_distribution(alias):
     assert int(ctrl[0].item()) == 1
     counts = torch.zeros(P, device=DEV)
     n = 0
-    for _ in range(600):
+    for _ in range(600 * P // 320):
         ops.is_sample(losses, ema, ctrl, idx, w, P, B, 32, alpha=0.5, ema_alpha=0.9, seed=1,
                       alias=alias)
         counts.index_add_(0, idx.long(), torch.ones(B, device=DEV))
