@@ -60,6 +60,13 @@ class Config:
     checkpoint_dir: str = ''
     checkpoint_every: int = 0
     resume: str = ''
+    # observability / health
+    check_replicas_every: int = 0   # DP replica fingerprint compare cadence (0 = off)
+    replica_rtol: float = 0.0       # allowed relative spread (0: bit-identical)
+    on_divergence: str = 'raise'    # 'raise' | 'warn'
+    roctx: bool = False             # per-phase roctx ranges (rocprofv3 --marker-trace)
+    profile_start: int = 0          # step at which the 'mercury_profile' roctx window opens
+    profile_steps: int = 0          # window length (0 = off)
 
     def lr(self, world_size):
         return self.base_lr * world_size

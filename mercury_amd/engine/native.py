@@ -33,6 +33,7 @@ from .. import ops
 from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
+from ..utils import profiling as prof
 from ..utils.meters import Accuracy, Average, EMAverage
 from .lower import lower, supports  # noqa: F401
 
@@ -104,6 +105,7 @@ class NativeEngine(object):
         self.shard = None
         self.scoring = True
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
+        self.roctx = False               # per-phase roctx ranges around the step's host calls
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
         self.sampler = sampler
         if score not in ('loss', 'gradnorm'):
@@ -638,8 +640,14 @@ class NativeEngine(object):
         ev_start.record(s0)
         self.s_score.wait_event(ev_start)
         graphs = self.graphs if self.use_graphs else None
+        rx = self.roctx
+        if rx:
+            prof.push('score')
         with torch.cuda.stream(self.s_score):
             self._score_stream_work(graphs)
+        if rx:
+            prof.pop()
+            prof.push('train')
         ev_score = torch.cuda.Event()
         ev_score.record(self.s_score)
         works = []
@@ -654,15 +662,23 @@ class NativeEngine(object):
                 s, e = bucket
                 works.append((dist.all_reduce(self.opt.g[s:e], op=self._avg_op,
                                               async_op=True), s, e))
+        if rx:
+            prof.pop()
+            prof.push('allreduce')
         for w, s, e in works:
             w.wait()
             if self._avg_op != dist.ReduceOp.AVG:   # gloo has no AVG
                 self.opt.g[s:e].mul_(1.0 / self.world_size)
         s0.wait_event(ev_score)
+        if rx:
+            prof.pop()
+            prof.push('tail')
         if graphs:
             graphs['tail'].replay()
         else:
             self.tail()
+        if rx:
+            prof.pop()
 
     # ------------------------------------------------------------------ misc API
     def reset_ema(self):
@@ -761,6 +777,12 @@ class NativeTrainer(Trainer):
             sampler=cfg.sampler, exchange_scores=cfg.exchange_scores,
             score=cfg.score, global_ema=cfg.global_ema)
         self.engine.set_shard(x, y)
+        self.engine.roctx = cfg.roctx
+        from ..utils.profiling import StepWindow
+        self.profile_window = StepWindow(cfg.profile_start, cfg.profile_steps)
+
+    def _flat_params(self):
+        return self.engine.opt.p
 
     def average_model(self):
         if self.world_size == 1:
@@ -807,6 +829,7 @@ class NativeTrainer(Trainer):
         t0 = time.perf_counter()
         for _ in range(self.steps_per_epoch):
             e.step()
+            self._health()
             if self.cfg.print_every and self.step % self.cfg.print_every == 0:
                 self._log(t0)
                 t0 = time.perf_counter()

@@ -73,6 +73,8 @@ class Trainer(object):
             if not fcs:
                 raise ValueError("score='gradnorm' needs a final nn.Linear classifier")
             fcs[-1].register_forward_pre_hook(self._keep_fc_input)
+        from .utils.profiling import StepWindow
+        self.profile_window = StepWindow(self.cfg.profile_start, self.cfg.profile_steps)
         self.score_exchange = None
         if self.world_size > 1 and (self.cfg.global_ema or self.cfg.exchange_scores):
             from .parallel.scores import ScoreExchange
@@ -217,8 +219,30 @@ class Trainer(object):
     def _stop(self):
         return self.step * self.world_size > self.cfg.max_samples
 
+    def _flat_params(self):
+        return self.flat.data
+
+    def _health(self):
+        """Replica-divergence check + profiler window, once per step."""
+        cfg = self.cfg
+        self.profile_window.step(self.step)
+        if cfg.check_replicas_every and self.world_size > 1 and \
+                self.step % cfg.check_replicas_every == 0:
+            from .parallel.health import ReplicaDivergence, check_replicas
+            ok, spread = check_replicas(self._flat_params(), rtol=cfg.replica_rtol)
+            if not ok:
+                msg = 'rank %d: DP replicas diverged at step %d (relative spread %.3g)' % (
+                    self.rank, self.step, spread)
+                if cfg.on_divergence == 'raise':
+                    raise ReplicaDivergence(msg)
+                print('[mercury_amd] WARNING ' + msg, flush=True)
+        if cfg.checkpoint_dir and cfg.checkpoint_every and self.step % cfg.checkpoint_every == 0:
+            from .ckpt import save_checkpoint
+            save_checkpoint(self, os.path.join(cfg.checkpoint_dir, 'ckpt_rank%d.pt' % self.rank))
+
     def _after_step(self, running_loss, running_acc, ema, t0):
         cfg = self.cfg
+        self._health()
         if cfg.print_every and self.step % cfg.print_every == 0 and self.rank == 0:
             ph = self.timer.collect()
             print('step:{}, running train loss: {}, running train acc: {}, presam_ema_loss: {}, '
@@ -236,9 +260,6 @@ class Trainer(object):
             if self.rank == 0:
                 print('(Eval) Step: {}, train loss: {}, train acc: {} test loss: {}, test acc: {}'
                       .format(self.step, train_loss, train_acc, test_loss, test_acc), flush=True)
-        if cfg.checkpoint_dir and cfg.checkpoint_every and self.step % cfg.checkpoint_every == 0:
-            from .ckpt import save_checkpoint
-            save_checkpoint(self, os.path.join(cfg.checkpoint_dir, 'ckpt_rank%d.pt' % self.rank))
 
     def fit(self, epochs):
         if self.rank == 0:
@@ -255,6 +276,7 @@ class Trainer(object):
             self.scheduler.step()
             if self._stop():
                 break
+        self.profile_window.close()
         if self.writer is not None:
             self.writer.close()
 

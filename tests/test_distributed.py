@@ -113,3 +113,30 @@ def _global_ema(rank, ws):
 
 def test_trainer_global_ema_gradnorm_two_ranks():
     spawn(_global_ema, 2)
+
+
+def _health(rank, ws):
+    from mercury_amd.parallel.health import check_replicas, replica_fingerprint
+    from mercury_amd.config import Config
+    from mercury_amd.trainer import Trainer
+    from test_importance import FakeLoader, TinyNet
+    flat = torch.arange(1000, dtype=torch.float32) / 7
+    ok, spread = check_replicas(flat)
+    assert ok and spread == 0.0
+    bad = flat.clone()
+    if rank == 1:
+        bad[3], bad[4] = bad[4].item(), bad[3].item()    # a permutation: same sum / sumsq
+    ok, spread = check_replicas(bad)
+    assert not ok and spread > 0
+    assert replica_fingerprint(flat).shape == (3,)
+    # the trainer checks every step and keeps training (replicas stay identical)
+    torch.manual_seed(rank)
+    net = TinyNet()
+    cfg = Config(print_every=0, eval_every=0, check_replicas_every=1)
+    t = Trainer(net, torch.optim.Adam(net.parameters(), lr=1e-3), FakeLoader(n=3),
+                FakeLoader(n=6, seed=rank), None, 'cpu', cfg)
+    t.fit(1)
+
+
+def test_replica_divergence_check():
+    spawn(_health, 2)
