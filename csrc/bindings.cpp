@@ -13,6 +13,17 @@
 
 #include "kernels.h"
 
+// native RCCL communicator (comm.hip)
+std::string comm_unique_id();
+uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
+void comm_destroy(uintptr_t c);
+void comm_allreduce(uintptr_t c, uintptr_t buf, long long count, int dtype, int avg, uintptr_t st);
+void comm_allgather(uintptr_t c, uintptr_t send, uintptr_t recv, long long count, int dtype,
+                    uintptr_t st);
+void comm_broadcast(uintptr_t c, uintptr_t buf, long long count, int dtype, int root, uintptr_t st);
+void comm_ring_allreduce(uintptr_t c, uintptr_t buf, long long count, uintptr_t work, int avg,
+                         uintptr_t st);
+
 namespace py = pybind11;
 
 template <typename T>
@@ -60,6 +71,19 @@ PYBIND11_MODULE(_C, m) {
                                         P<const bf16>(x), wg, P<float>(dw), wbm, wbn, wsplits, S(st));
     if (ok) check_launch("conv_bwd_pair");
     return ok;
+  });
+  m.def("comm_unique_id", []() { return py::bytes(comm_unique_id()); });
+  m.def("comm_init", [](py::bytes id, int rank, int nranks) {
+    return comm_init(std::string(id), rank, nranks);
+  });
+  m.def("comm_destroy", &comm_destroy);
+  m.def("comm_allreduce", &comm_allreduce);
+  m.def("comm_allgather", &comm_allgather);
+  m.def("comm_broadcast", &comm_broadcast);
+  m.def("comm_ring_allreduce", [](uintptr_t c, uintptr_t buf, long long count, uintptr_t work,
+                                  int avg, uintptr_t st) {
+    comm_ring_allreduce(c, buf, count, work, avg, st);
+    check_launch("comm_ring_allreduce");
   });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};

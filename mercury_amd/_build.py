@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, 'csrc')
 OBJ = os.path.join(ROOT, 'build', 'obj')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950').split(';')[0]
-HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
+HIPCC = os.environ.get('HIPCC', os.path.join(ROCM, 'bin', 'hipcc'))
 EXT_SUFFIX = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
 TARGET = os.path.join(ROOT, 'mercury_amd', '_C' + EXT_SUFFIX)
 
@@ -79,7 +80,9 @@ def build(verbose=True, jobs=None):
             list(ex.map(lambda w: _compile(*w), work))
     if work or not os.path.exists(TARGET) or any(
             os.path.getmtime(o) > os.path.getmtime(TARGET) for o in objs):
-        cmd = [HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objs + ['-o', TARGET]
+        # librccl.so.1 resolves at import to the RCCL torch already loaded (same soname)
+        cmd = ([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objs +
+               ['-L' + os.path.join(ROCM, 'lib'), '-lrccl', '-o', TARGET])
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('link failed: %s\n%s' % (r.stdout, r.stderr))
