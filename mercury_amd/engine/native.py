@@ -482,14 +482,20 @@ class NativeEngine(object):
         self._build_bn_table()
 
     def _build_bn_table(self):
-        rows = []
+        """Running-stat update table: the train batch, then (importance mode) the 10 scored
+        pool batches, each a train-mode forward in the reference.  The uniform baseline
+        scores nothing, so its table updates from the train batch only."""
+        tables = []
         tm, sm = self.train_mode, self.score_mode
-        for u in self.units:
-            sp_t, sp_s = tm.spec[u.name], sm.spec[u.name]
-            rows.append((u.bn.running_mean, u.bn.running_var, tm.stats[u.name], sm.stats[u.name],
-                         u.bn.num_batches_tracked, u.K, 1, sm.G, float(sp_t.M),
-                         float(sp_s.group_rows or sp_s.M)))
-        self.bn_table = ops.BnRunTable(rows, self.device)
+        for n_score in (sm.G, 0):
+            rows = []
+            for u in self.units:
+                sp_t, sp_s = tm.spec[u.name], sm.spec[u.name]
+                rows.append((u.bn.running_mean, u.bn.running_var, tm.stats[u.name],
+                             sm.stats[u.name], u.bn.num_batches_tracked, u.K, 1, n_score,
+                             float(sp_t.M), float(sp_s.group_rows or sp_s.M)))
+            tables.append(ops.BnRunTable(rows, self.device))
+        self.bn_table, self.bn_table_uniform = tables
 
     # ------------------------------------------------------------------ step pieces
     def score_branch(self):
@@ -599,7 +605,7 @@ class NativeEngine(object):
         return cuts
 
     def tail(self):
-        self.bn_table.launch(0.1)
+        (self.bn_table if self.scoring else self.bn_table_uniform).launch(0.1)
         self.opt.step(self.ctrl[2:3])
         self.gather_batch()
 
@@ -622,6 +628,7 @@ class NativeEngine(object):
         }
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
+        self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
     def prime(self):
@@ -640,6 +647,8 @@ class NativeEngine(object):
         ev_start.record(s0)
         self.s_score.wait_event(ev_start)
         graphs = self.graphs if self.use_graphs else None
+        if graphs and self._graph_scoring != self.scoring:
+            raise RuntimeError('scoring was toggled after build_graphs(); rebuild the graphs')
         rx = self.roctx
         if rx:
             prof.push('score')

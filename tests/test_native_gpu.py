@@ -145,3 +145,20 @@ def test_steps_reduce_loss_and_graph_matches_eager(graphs):
         lo = net(((xx - mean) / std).to(torch.bfloat16).float())
         ref_loss = F.cross_entropy(lo, torch.as_tensor(y[:1000]).to(DEV)).item()
     assert n == 1000 and abs(loss - ref_loss) < 0.05 * ref_loss + 0.05, (loss, ref_loss)
+
+
+def test_uniform_baseline_keeps_running_stats_sane():
+    """Uniform sampling scores no pool: running stats update from the train batch only
+    (a stale score-group table would drive running_var to zero and break eval)."""
+    from mercury_amd.models import build_model
+    torch.manual_seed(0)
+    net = build_model('resnet18', 10).to(DEV)
+    eng = _engine(net, importance=False)
+    eng.scoring = False
+    eng.prime()
+    for _ in range(30):
+        eng.step()
+    torch.cuda.synchronize()
+    rv = net.bn1.running_var
+    assert float(rv.min()) > 1e-3, float(rv.min())
+    assert int(net.bn1.num_batches_tracked) == 30
