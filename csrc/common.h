@@ -67,6 +67,16 @@ MA_DEV u32x4 philox4x32(u32x4 ctr, uint32_t k0, uint32_t k1) {
   }
   return ctr;
 }
+// x / d for 0 <= x < 2^24 and a wave-uniform divisor d via the float reciprocal (rcp is
+// uniform, so it is computed once), with a one-step fix-up: ~6 VALU instead of the ~30 of an
+// integer division.  Every pixel/row index of a conv GEMM is < 2^24.
+MA_DEV int udiv24(int x, int d, float rcp) {
+  int q = (int)((float)x * rcp);
+  const int r = x - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
 MA_DEV float u01(uint32_t x) { return (x >> 8) * (1.0f / 16777216.0f); }  // [0,1)
 
 // ---------------------------------------------------------------------------------

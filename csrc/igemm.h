@@ -15,6 +15,7 @@ struct ConvGeom {
   int Kc;            // reduction length in 8-element chunks = R*S*SC/8
   int Ncols;         // GEMM N (output channels)
   int M;             // GEMM M = images * RP * RQ
+  const bf16* zero;  // 16-byte zero page for padding taps (set by the launcher; kernel arg -> SGPR)
 };
 
 struct EpiParams {
@@ -50,6 +51,7 @@ struct WgradGeom {
   int P, Q, K;        // dy dims (K = output channels)
   int R, S, stride, pad;
   int Creal;          // unpadded input channels (layout of dW)
+  const bf16* zero;   // 16-byte zero page (set by the launcher)
 };
 void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
                   int splits, hipStream_t st);

@@ -238,46 +238,46 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
 // by hipcc, which turned every gather into a scratch load + vmcnt(0))
 template <bool TRANS>
 MA_DEV void row_init(const ConvGeom& g, int m, int& off, int& h, int& w) {
-  if (m < g.M) {
-    const int pq = g.RP * g.RQ;
-    const int n = m / pq, rem = m - n * pq;
-    const int p = rem / g.RQ, q = rem - p * g.RQ;
-    off = n * g.SH * g.SW;
-    h = TRANS ? p + g.pad : p * g.stride - g.pad;
-    w = TRANS ? q + g.pad : q * g.stride - g.pad;
-  } else {
-    off = -1;
-    h = w = 0;
-  }
+  const int pq = g.RP * g.RQ;
+  const int mm = m < g.M ? m : 0;
+  const int n = udiv24(mm, pq, 1.f / (float)pq), rem = mm - n * pq;
+  const int p = udiv24(rem, g.RQ, 1.f / (float)g.RQ), q = rem - p * g.RQ;
+  off = m < g.M ? n * g.SH * g.SW : -1;
+  h = TRANS ? p + g.pad : p * g.stride - g.pad;
+  w = TRANS ? q + g.pad : q * g.stride - g.pad;
 }
 
-// element offset of (row, tap r/s, channel chunk c8) or -1 for a zero chunk
+// element offset of (row, tap r/s, channel chunk c8) or -1 for a zero chunk.  Branch-free:
+// the bounds tests become compares + one select, so the per-row gather of a stage is straight-
+// line VALU and every load issues unconditionally (a divergent branch per row made hipcc wrap
+// each load in exec-mask save/restore and re-derive the zero-page address in every branch).
 template <bool TRANS>
 MA_DEV int row_at(const ConvGeom& g, int off, int h, int w, int r, int s, int c8) {
-  if (off < 0) return -1;
   int hh, ww;
+  bool ok = off >= 0;
   if (TRANS) {
     const int hp = h - r, wp = w - s;
-    if (hp < 0 || wp < 0) return -1;
-    if (g.stride == 2) {
-      if ((hp | wp) & 1) return -1;
-      hh = hp >> 1;
+    if (g.stride == 2) {                 // kernel-uniform: scalar branch
+      ok = ok && ((hp | wp) & 1) == 0;
+      hh = hp >> 1;                      // arithmetic shift keeps negatives negative
       ww = wp >> 1;
     } else {
       hh = hp;
       ww = wp;
     }
-    if (hh >= g.SH || ww >= g.SW) return -1;
   } else {
     hh = h + r;
     ww = w + s;
-    if (hh < 0 || ww < 0 || hh >= g.SH || ww >= g.SW) return -1;
   }
-  return (off + hh * g.SW + ww) * g.SC + c8 * 8;
+  ok = ok && (unsigned)hh < (unsigned)g.SH && (unsigned)ww < (unsigned)g.SW;
+  const int o = (off + hh * g.SW + ww) * g.SC + c8 * 8;
+  return ok ? o : -1;
 }
 
 // k-chunk -> (r, s, c8) cursor.  When C/8 is a multiple of 8 a 64-deep stage lies in one
-// filter tap, so the tap advances incrementally (no division in the loop).
+// filter tap, so the tap advances incrementally (no division in the loop).  Otherwise the
+// stage base is decoded once (uniform) and each lane steps its <= 7 extra chunks forward;
+// the tap split r = rs / S uses an exact float reciprocal (rs <= R*S <= 49).
 struct KCursor {
   int tr, ts, tc;
   bool fast;
@@ -303,9 +303,14 @@ struct KCursor {
       c8 = tc + lcc;
     } else {
       const int C8 = g.SC >> 3;
-      const int rs = kc / C8;
-      c8 = kc - rs * C8;
-      r = rs / g.S;
+      const int k0 = kt * 8;                       // uniform
+      int rs = k0 / C8;
+      c8 = k0 - rs * C8 + lcc;
+      while (c8 >= C8) {                           // <= 8 / C8 trips
+        c8 -= C8;
+        ++rs;
+      }
+      r = (int)(((float)rs + 0.5f) * (1.f / (float)g.S));
       s = rs - r * g.S;
     }
   }
@@ -437,7 +442,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   }
   KCursor kc;
   kc.init(g, kt0);
-  const bf16* zp = g_zero_page;
+  const bf16* zp = g.zero;
 
   u32x4 ra[AR], rb[BR];
   auto load_stage = [&](int kt) {
@@ -447,7 +452,8 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     kc.advance(g);
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const int o = kval ? row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8) : -1;
+      int o = row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8);
+      o = kval ? o : -1;                       // select, not a branch around the gather
       ra[i] = *(const u32x4*)(o >= 0 ? src + o : zp);
     }
 #pragma unroll
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restric
   }
   KCursor kc;
   kc.init(g, kt0);
-  const bf16* zp = g_zero_page;
+  const bf16* zp = g.zero;
 
   auto issue = [&](int kt, int slot) {
     bf16* a_st = sbase + slot * STAGE;
@@ -563,7 +569,8 @@ __global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restric
     kc.advance(g);
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int o = kval ? row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8) : -1;
+      int o = row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8);
+      o = kval ? o : -1;                       // select, not a branch around the gather
       glds16(o >= 0 ? (const void*)(src + o) : (const void*)zp, a_st + (w * (BM / 4) + i * 8) * BK);
     }
 #pragma unroll
@@ -674,8 +681,20 @@ size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   return SEM_INTS * 4 + (size_t)splits * mtiles * ntiles * bm * bn * 4;
 }
 
-void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e,
+static const bf16* zero_page() {
+  static const bf16* zp = nullptr;
+  if (!zp) {
+    void* p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_zero_page));
+    zp = (const bf16*)p;
+  }
+  return zp;
+}
+
+void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const EpiParams& e,
                   int bm, int bn, int splits, bool trans, hipStream_t st, int pipe) {
+  ConvGeom g = g_in;
+  g.zero = zero_page();
 #define MA_CASE(BM_, BN_)                                                      \
   if (bm == BM_ && bn == BN_) {                                                \
     if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, pipe, st);    \
@@ -690,9 +709,13 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiP
 #undef MA_CASE
 }
 
-int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
-                         int bm, int bn, int splits, const bf16* x, const WgradGeom& wg, float* dw,
-                         int wbm, int wbn, int wsplits, hipStream_t st) {
+int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g_in, const EpiParams& e,
+                         int bm, int bn, int splits, const bf16* x, const WgradGeom& wg_in,
+                         float* dw, int wbm, int wbn, int wsplits, hipStream_t st) {
+  ConvGeom g = g_in;
+  g.zero = zero_page();
+  WgradGeom wg = wg_in;
+  wg.zero = g.zero;
 #define MA_W(DBM_, DBN_, WBM_, WBN_)                                                   \
   if (wbm == WBM_ && wbn == WBN_) {                                                   \
     pair_cfg<DBM_, DBN_, WBM_, WBN_>(dy, wt, g, e, splits, x, wg, dw, wsplits, st);   \

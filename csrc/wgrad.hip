@@ -45,8 +45,18 @@ void wlaunch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int s
 }
 }  // namespace
 
-void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
+__device__ __attribute__((aligned(16))) bf16 g_wg_zero[64];
+
+void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g_in, float* dw, int bm, int bn,
                   int splits, hipStream_t st) {
+  static const bf16* zp = nullptr;
+  if (!zp) {
+    void* p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_wg_zero));
+    zp = (const bf16*)p;
+  }
+  WgradGeom g = g_in;
+  g.zero = zp;
   if (bm == 128 && bn == 128) return wlaunch<128, 128>(dy, x, g, dw, splits, st);
   if (bm == 128 && bn == 64) return wlaunch<128, 64>(dy, x, g, dw, splits, st);
   if (bm == 64 && bn == 128) return wlaunch<64, 128>(dy, x, g, dw, splits, st);

@@ -60,6 +60,7 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
   }
   const int acc_ = tid % ACH;
 
+  const float rpq = 1.f / (float)(g.P * g.Q), rq = 1.f / (float)g.Q;
   u32x4 ra[AR], rb[BR];
   auto load_stage = [&](int pt) {
 #pragma unroll
@@ -67,24 +68,21 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
       const int row = tid / ACH + i * (NT / ACH);
       const int pix = pt * BKP + row;
       const int k = m0 + acc_ * 8;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (pix < npix && k < g.K) v = *(const u32x4*)(dy + (size_t)pix * g.K + k);
-      ra[i] = v;
+      const bool ok = pix < npix && k < g.K;
+      // select the address, load unconditionally (no exec-masked branch per row)
+      ra[i] = *(const u32x4*)(ok ? dy + (size_t)pix * g.K + k : g.zero);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int row = tid / BCH + i * (NT / BCH);
       const int pix = pt * BKP + row;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (pix < npix && jval) {
-        const int pq = g.P * g.Q;
-        const int n = pix / pq, rem = pix - n * pq;
-        const int p = rem / g.Q, q = rem - p * g.Q;
-        const int h = p * g.stride - g.pad + xr, ww = q * g.stride - g.pad + xs;
-        if (h >= 0 && ww >= 0 && h < g.H && ww < g.W)
-          v = *(const u32x4*)(x + ((size_t)(n * g.H + h) * g.W + ww) * g.C + xc8 * 8);
-      }
-      rb[i] = v;
+      const int px = pix < npix ? pix : 0;
+      const int pq = g.P * g.Q;
+      const int n = udiv24(px, pq, rpq), rem = px - n * pq;
+      const int p = udiv24(rem, g.Q, rq), q = rem - p * g.Q;
+      const int h = p * g.stride - g.pad + xr, ww = q * g.stride - g.pad + xs;
+      const bool ok = pix < npix && jval && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+      rb[i] = *(const u32x4*)(ok ? x + ((size_t)(n * g.H + h) * g.W + ww) * g.C + xc8 * 8 : g.zero);
     }
   };
   auto store_stage = [&](int buf) {
