@@ -44,6 +44,10 @@ PRESETS = {
                                      'ResNet-50 ImageNet-shape 224 DP',
                               dataset='imagenet-shape (224x224x3, 1000 classes; 12800 '
                                       'synthetic images resident in HBM)'),
+    'vgg11-speech': dict(model='vgg11', classes=30, hw=(101, 161), n=20000, batch=32, chans=1,
+                         metric='images/sec (whole node) + sampler overhead %, VGG11 '
+                                'speech-commands-shape DP',
+                         dataset='GSC-shape spectrograms (1x101x161 float, 30 classes)'),
 }
 
 
@@ -75,7 +79,14 @@ def main():
     from mercury_amd.models import build_model
 
     ncls, hw, n = pre['classes'], pre['hw'], pre['n']
-    x_all, y_all = synthetic_arrays(n, ncls, shape=(hw, hw, 3), seed=8)
+    hw = hw if isinstance(hw, tuple) else (hw, hw)
+    if pre.get('chans', 3) == 3:
+        x_all, y_all = synthetic_arrays(n, ncls, shape=(hw[0], hw[1], 3), seed=8)
+    else:   # float "spectrograms": class-dependent low-frequency pattern + noise
+        rng = np.random.RandomState(8)
+        y_all = rng.randint(0, ncls, n).astype(np.int64)
+        proto = rng.randn(ncls, pre['chans'], hw[0], hw[1]).astype(np.float32)
+        x_all = (proto[y_all] + rng.randn(n, pre['chans'], hw[0], hw[1]).astype(np.float32) * 2)
     np.random.seed(102)
     shards = dirichlet_partition(y_all, ws, 0.5, ncls) if ws > 1 else {0: np.arange(n)}
     idx = np.asarray(shards[rank])
@@ -85,7 +96,7 @@ def main():
     def make(importance):
         eng = NativeEngine(net, device, args.batch, args.pool_batches, optimizer='adam',
                            lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
-                           use_graphs=not args.no_graphs, image_hw=(hw, hw))
+                           use_graphs=not args.no_graphs, image_hw=hw)
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)

@@ -172,11 +172,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_build", [](uintptr_t shard, uintptr_t labels, uintptr_t ctrl, uintptr_t pool,
                          uintptr_t pool_label, uintptr_t pool_index, int Ns, int H, int W, int Pn,
                          int batch, int pad, int flip, int augment, int shuffle, uint32_t seed,
-                         std::vector<float> mean, std::vector<float> inv_std, uintptr_t st) {
+                         std::vector<float> mean, std::vector<float> inv_std, uintptr_t st,
+                         int prebuilt) {
     PoolBuildArgs a{P<const uint8_t>(shard), P<const int64_t>(labels), P<const int64_t>(ctrl),
                     P<bf16>(pool), P<int>(pool_label), P<int>(pool_index), Ns, H, W, Pn, batch,
                     pad, flip, augment, shuffle, seed, {mean[0], mean[1], mean[2]},
-                    {inv_std[0], inv_std[1], inv_std[2]}};
+                    {inv_std[0], inv_std[1], inv_std[2]}, prebuilt};
     pool_build_launch(a, S(st));
     check_launch("pool_build");
   });

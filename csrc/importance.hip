@@ -17,18 +17,44 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
-  const int slot = blockIdx.x;
-  const int j = slot / a.batch, t = slot - j * a.batch;
+// Which shard sample fills pool slot `slot` (epoch permutation, drop_last batches), and the
+// global batch number gb that seeds its augmentation.
+MA_DEV uint32_t pool_src(const PoolBuildArgs& a, int slot, int64_t& gb, int& t) {
+  const int j = slot / a.batch;
+  t = slot - j * a.batch;
   const int64_t pc = a.ctrl[0];
   const int per_pool = a.P / a.batch;
   const int nb = max(1, a.Ns / a.batch);
-  const int64_t gb = pc * per_pool + j;
+  gb = pc * per_pool + j;
   const uint32_t epoch = (uint32_t)(gb / nb);
   const int bi = (int)(gb % nb);
   const uint32_t pos = (uint32_t)(bi * a.batch + t);
-  const uint32_t src = a.shuffle ? permute_index(pos, (uint32_t)a.Ns, a.seed, epoch)
-                                 : (uint32_t)((gb * a.batch + t) % a.Ns);
+  return a.shuffle ? permute_index(pos, (uint32_t)a.Ns, a.seed, epoch)
+                   : (uint32_t)((gb * a.batch + t) % a.Ns);
+}
+
+// Pre-converted shard (non-image inputs, e.g. the speech VGG's 1x101x161 spectrograms, stored
+// once as NHWC bf16 with channels padded to 8): the pool is a straight 16-byte-chunk gather.
+__global__ __launch_bounds__(256) void pool_take_kernel(PoolBuildArgs a) {
+  const int slot = blockIdx.x;
+  int64_t gb;
+  int t;
+  const uint32_t src = pool_src(a, slot, gb, t);
+  if (threadIdx.x == 0) {
+    a.pool_label[slot] = (int)a.labels[src];
+    a.pool_index[slot] = (int)src;
+  }
+  const int npx = a.H * a.W;
+  const u32x4* in = (const u32x4*)a.shard + (size_t)src * npx;
+  u32x4* out = (u32x4*)a.pool + (size_t)slot * npx;
+  for (int px = threadIdx.x; px < npx; px += 256) out[px] = in[px];
+}
+
+__global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
+  const int slot = blockIdx.x;
+  int64_t gb;
+  int t;
+  const uint32_t src = pool_src(a, slot, gb, t);
   int dy = a.pad, dx = a.pad, flip = 0;
   if (a.augment) {
     const u32x4 r = philox4x32(u32x4{(uint32_t)gb, (uint32_t)(gb >> 32), (uint32_t)t, 0x5eedu},
@@ -287,7 +313,10 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherArgs a) {
 }  // namespace
 
 void pool_build_launch(const PoolBuildArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(pool_build_kernel, dim3(a.P), dim3(256), 0, st, a);
+  if (a.prebuilt)
+    hipLaunchKernelGGL(pool_take_kernel, dim3(a.P), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(pool_build_kernel, dim3(a.P), dim3(256), 0, st, a);
 }
 
 size_t is_sample_lds(int P, int alias) {

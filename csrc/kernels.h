@@ -104,6 +104,7 @@ struct PoolBuildArgs {
   int Ns, H, W, P, batch, pad, flip, augment, shuffle;
   uint32_t seed;
   float mean[3], inv_std[3];
+  int prebuilt;                  // shard is already NHWC bf16 [Ns][H][W][8]: plain gather
 };
 void pool_build_launch(const PoolBuildArgs& a, hipStream_t st);
 

@@ -7,7 +7,8 @@ model zoo (``models/resnet.py`` = `pytorch_model.py:14-113`, and
 * ``Unit``  -- one conv (implicit-GEMM or depthwise) + its BatchNorm + activation;
 * ``Block`` -- main-path units, an optional shortcut unit or identity skip, the
   final activation and an optional max-pool (ImageNet stem);
-* the classifier head (global average pool + linear).
+* the classifier head (global average pool + linear, or -- speech VGG -- flatten +
+  two linears).
 
 Parameters are laid out in ONE flat fp32 buffer in module registration order
 (so the flat order matches ``named_parameters()``, and backward produces
@@ -26,6 +27,7 @@ import torch.nn as nn
 
 from ..models.mobilenetv2 import InvertedResidual, MobileNetV2
 from ..models.resnet import BasicBlock, Bottleneck, ResNet
+from ..models.vgg import VGG
 
 
 @dataclass
@@ -90,11 +92,12 @@ class Lowered:
     total: int = 0
     in_channels: int = 3
     num_classes: int = 10
-    head_pool: str = 'avg'
+    head_pool: str = 'avg'           # 'avg': global avg-pool + fc;  'mlp2': flatten + fc1 + fc2
+    fc1: Optional[nn.Linear] = None  # first layer of the 'mlp2' head (VGG)
 
 
 def supports(net):
-    return isinstance(net, (ResNet, MobileNetV2))
+    return isinstance(net, (ResNet, MobileNetV2, VGG))
 
 
 def _bn_unit(name, conv, bn, act, depthwise=False):
@@ -151,10 +154,42 @@ def lower(net) -> Lowered:
                             final_act='relu6'))
         fc = net.linear
         in_ch = 3
+    elif isinstance(net, VGG):
+        # speech VGG (`pytorch_model.py:117-153`): conv3x3(+bias)-BN-ReLU units, a 2x2 max-pool
+        # after the units the config marks 'M', trailing AvgPool2d(1,1) (identity), then
+        # flatten -> fc1 -> fc2 -> log_softmax.  Each conv is a one-unit block.
+        feats = list(net.features)
+        i = 0
+        while i < len(feats):
+            mod = feats[i]
+            if isinstance(mod, nn.Conv2d):
+                name = 'features.%d' % i
+                u = _bn_unit(name, mod, feats[i + 1], 'relu')
+                first = not blocks
+                blk = Block(name, [u], None, identity=False, final_act='relu', need_dx=not first)
+                if first:
+                    u.need_dgrad = False
+                i += 3
+                if i < len(feats) and isinstance(feats[i], nn.MaxPool2d):
+                    mp = feats[i]
+                    blk.pool = (int(mp.kernel_size if isinstance(mp.kernel_size, int)
+                                    else mp.kernel_size[0]),
+                                int(mp.stride if isinstance(mp.stride, int) else mp.stride[0]), 0)
+                    i += 1
+                blocks.append(blk)
+            elif isinstance(mod, nn.AvgPool2d) and mod.kernel_size in (1, (1, 1)):
+                i += 1
+            else:
+                raise TypeError('unexpected VGG feature module %s' % type(mod).__name__)
+        fc = net.fc2
+        in_ch = feats[0].in_channels
     else:
         raise TypeError('native engine does not support %s' % type(net).__name__)
 
     lw = Lowered(blocks, fc, in_channels=in_ch, num_classes=fc.out_features)
+    if isinstance(net, VGG):
+        lw.head_pool = 'mlp2'
+        lw.fc1 = net.fc1
     # flat layout in registration order
     unit_of = {}
     for blk in blocks:
@@ -169,7 +204,7 @@ def lower(net) -> Lowered:
         role = unit_of.get(id(p))
         if role is not None and role[0] == 'w':
             kind = 'dw' if role[1].depthwise else 'conv'
-        elif p is fc.weight:
+        elif p is fc.weight or (lw.fc1 is not None and p is lw.fc1.weight):
             kind = 'fc'
         else:
             kind = 'vec'
@@ -189,4 +224,7 @@ def lower(net) -> Lowered:
     lw.total = off
     lw.fc_w = next(s for s in lw.segs if s.param is fc.weight)
     lw.fc_b = next(s for s in lw.segs if s.param is fc.bias)
+    if lw.fc1 is not None:
+        lw.fc1_w = next(s for s in lw.segs if s.param is lw.fc1.weight)
+        lw.fc1_b = next(s for s in lw.segs if s.param is lw.fc1.bias)
     return lw

@@ -87,9 +87,8 @@ class NativeEngine(object):
         self.units = []
         for blk in self.lw.blocks:
             self.units += blk.units + ([blk.shortcut] if blk.shortcut else [])
-        for u in self.units:
-            if u.conv.bias is not None:
-                raise NotImplementedError('conv bias not supported by the native engine')
+        # conv bias (speech VGG) is added in the conv epilogue; under train-mode BN its gradient
+        # is exactly zero (the batch mean absorbs it), so its grad segment is never written
         self._make_params(optimizer, lr, betas, eps, weight_decay, momentum)
         self.modes = {}
         self.ctrl = torch.zeros(8, dtype=torch.int64, device=self.device)
@@ -163,6 +162,7 @@ class NativeEngine(object):
                 p = p.permute(0, 2, 3, 1)
             self.opt.p[s.off:s.off + s.numel].copy_(p.reshape(-1))
         self.opt.pack_weights()
+        self._mlp_refresh()
 
     @torch.no_grad()
     def sync_to_module(self):
@@ -292,7 +292,8 @@ class NativeEngine(object):
                            sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M)
         else:
             ops.conv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, slab=m.slab,
-                         plan=m.plan[u.name, 'fwd'])
+                         plan=m.plan[u.name, 'fwd'],
+                         bias=self._pview(u.b_seg) if u.b_seg is not None else None)
 
     def _bn_apply(self, m, u, y, out, act, res=None, res_unit=None):
         sp = m.spec[u.name]
@@ -342,7 +343,74 @@ class NativeEngine(object):
             x = m.buf[bi, 'out']
         return x
 
+    # ------------------------------------------------------------------ speech-VGG head
+    # flatten -> fc1 -> fc2 (-> log_softmax; CE on log-probs == CE on logits).  Plain GEMMs
+    # at M = batch, so they go to hipBLASLt through torch.matmul (captured in the step graphs).
+    # fc1's columns are stored in torch's (C,H,W) flatten order; activations are NHWC, so a
+    # bf16 copy with (H,W,C) column order is refreshed after every optimizer step.
+    def _mlp_refresh(self):
+        if self.lw.head_pool != 'mlp2' or getattr(self, 'mlp_hwc', None) is None:
+            return
+        h, w, c = self.mlp_hwc
+        W1 = self._pview(self.lw.fc1_w).view(-1, c, h, w)
+        self.w1p.copy_(W1.permute(0, 2, 3, 1).reshape(W1.shape[0], -1))
+
+    def _mlp_setup(self, m):
+        last = len(self.lw.blocks) - 1
+        h, w = m.buf[last, 'hw']
+        self.mlp_hwc = (h, w, m.final_C)
+        f1 = self.lw.fc1.out_features
+        if getattr(self, 'w1p', None) is None:
+            self.w1p = torch.zeros(f1, h * w * m.final_C, dtype=torch.bfloat16, device=self.device)
+            self._mlp_refresh()
+
+    def _mlp_head(self, m, x, mode, isw=None, meters=None):
+        N, f1 = m.N, self.lw.fc1.out_features
+        xf = x.view(N, -1)
+        h1 = (xf @ self.w1p.t()).float() + self._pview(self.lw.fc1_b)
+        W2 = self._pview(self.lw.fc_w).view(self.classes, f1)
+        logits = torch.addmm(self._pview(self.lw.fc_b), h1, W2.t())
+        lab = m.label.long()
+        lse = torch.logsumexp(logits, 1)
+        loss = lse - logits.gather(1, lab[:, None])[:, 0]
+        p = torch.exp(logits - lse[:, None])
+        d = p.clone()
+        d[torch.arange(N, device=d.device), lab] -= 1.0
+        if mode == 'score':
+            if self.score == 'gradnorm':
+                m.losses.copy_(d.norm(dim=1) * torch.sqrt(h1.pow(2).sum(1) + 1.0))
+            else:
+                m.losses.copy_(loss)
+            return
+        if meters is not None:
+            wl = loss / isw if (mode == 'train' and isw is not None) else loss
+            meters[0:1].add_(wl.sum())
+            meters[1:2].add_(float(N))
+            meters[2:3].add_((logits.argmax(1) == lab).float().sum())
+        if mode == 'train':
+            m.losses.copy_(loss)
+            m.mlp_h1 = h1
+            m.dlogits.copy_(d / (float(N) * isw[:, None]))
+
+    def _mlp_head_bwd(self, m, dout):
+        """Grads of fc2 / fc1 into the flat buffer and d(activation) (NHWC bf16) into dout."""
+        N, f1 = m.N, self.lw.fc1.out_features
+        h, w, c = self.mlp_hwc
+        g = m.dlogits
+        W2 = self._pview(self.lw.fc_w).view(self.classes, f1)
+        self._pview(self.lw.fc_w, True).view(self.classes, f1).copy_(g.t() @ m.mlp_h1)
+        self._pview(self.lw.fc_b, True).copy_(g.sum(0))
+        dh1 = g @ W2
+        self._pview(self.lw.fc1_b, True).copy_(dh1.sum(0))
+        xf = m.buf[len(self.lw.blocks) - 1, 'out'].view(N, -1)
+        dW1p = dh1.t() @ xf.float()                                 # (H,W,C) column order
+        self._pview(self.lw.fc1_w, True).view(f1, c, h, w).copy_(
+            dW1p.view(f1, h, w, c).permute(0, 3, 1, 2))
+        dout.view(N, -1).copy_(dh1.to(torch.bfloat16) @ self.w1p)
+
     def head(self, m, x, mode, isw=None, meters=None):
+        if self.lw.head_pool == 'mlp2':
+            return self._mlp_head(m, x, mode, isw=isw, meters=meters)
         ops.head_fwd(x, self._pview(self.lw.fc_w), self._pview(self.lw.fc_b), m.label, m.N,
                      m.final_hw, m.final_C, self.classes, mode, pooled=m.pooled,
                      dlogits=getattr(m, 'dlogits', None) if mode == 'train' else None,
@@ -464,20 +532,40 @@ class NativeEngine(object):
                     m.prereduced[bi - 1] = True
 
     # ------------------------------------------------------------------ data
-    def set_shard(self, images_u8, labels):
-        """Keep this rank's training shard resident in HBM: uint8 [Ns][H][W][3]."""
-        x = torch.as_tensor(np.ascontiguousarray(images_u8)) if not torch.is_tensor(images_u8) \
-            else images_u8
-        if x.dim() != 4 or tuple(x.shape[1:]) != (self.H, self.W, 3):
-            raise ValueError('shard must be uint8 [N][%d][%d][3], got %s'
-                             % (self.H, self.W, tuple(x.shape)))
+    def _device_inputs(self, images):
+        """uint8 HWC images stay uint8 [N][H][W][3] (augmented on the fly); float inputs
+        [N][C][H][W] (e.g. spectrograms) are converted ONCE to NHWC bf16 [N][H][W][8]."""
+        x = torch.as_tensor(np.ascontiguousarray(images)) if not torch.is_tensor(images) \
+            else images
+        if x.dtype == torch.uint8:
+            if x.dim() != 4 or tuple(x.shape[1:]) != (self.H, self.W, 3):
+                raise ValueError('uint8 shard must be [N][%d][%d][3], got %s'
+                                 % (self.H, self.W, tuple(x.shape)))
+            return x.to(self.device).contiguous()
+        C = self.lw.in_channels
+        if x.dim() != 4 or tuple(x.shape[1:]) != (C, self.H, self.W):
+            raise ValueError('float shard must be [N][%d][%d][%d], got %s'
+                             % (C, self.H, self.W, tuple(x.shape)))
+        out = torch.empty(x.shape[0], self.H, self.W, 8, dtype=torch.bfloat16, device=self.device)
+        step = 4096
+        for s0 in range(0, x.shape[0], step):
+            blk = x[s0:s0 + step].to(self.device, torch.float32).contiguous()
+            ops.nchw_to_nhwc8(blk, out[s0:s0 + step])
+        return out
+
+    def set_shard(self, images, labels):
+        """Keep this rank's training shard resident in HBM: uint8 [Ns][H][W][3] images, or
+        float [Ns][C][H][W] inputs pre-converted to NHWC bf16."""
+        x = self._device_inputs(images)
         if x.shape[0] < self.B:
             # the device epoch permutation draws whole batches from the shard
             raise ValueError('shard has %d samples < batch %d' % (x.shape[0], self.B))
-        self.shard = x.to(self.device, torch.uint8).contiguous()
+        self.shard = x
         self.shard_labels = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
         self.train_mode = self.mode('train', self.B, 0, True)
         self.score_mode = self.mode('score', self.P, self.B, False)
+        if self.lw.head_pool == 'mlp2':
+            self._mlp_setup(self.train_mode)
         self.idx = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._arange_b = torch.arange(self.B, dtype=torch.int32, device=self.device)
         self.isw = torch.ones(self.B, dtype=torch.float32, device=self.device)
@@ -576,6 +664,9 @@ class NativeEngine(object):
             x = self.forward(tm)
             self.head(tm, x, 'train', isw=self.isw, meters=self.meters)
             last = len(self.lw.blocks) - 1
+            if self.lw.head_pool == 'mlp2':
+                self._mlp_head_bwd(tm, tm.buf[last, 'dout'])
+                return
             ops.head_bwd(tm.pooled, tm.dlogits, self._pview(self.lw.fc_w),
                          self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True),
                          tm.buf[last, 'dout'], self.B, tm.final_hw, tm.final_C, self.classes)
@@ -613,6 +704,7 @@ class NativeEngine(object):
     def tail(self):
         (self.bn_table if self.scoring else self.bn_table_uniform).launch(0.1)
         self.opt.step(self.ctrl[2:3])
+        self._mlp_refresh()
         self.gather_batch()
 
     # ------------------------------------------------------------------ graphs
@@ -717,9 +809,10 @@ class NativeEngine(object):
         self.opt.pack_weights()
 
     @torch.no_grad()
-    def evaluate_arrays(self, images_u8, labels, batch=500):
-        """Eval-mode (running-stats BN) loss / accuracy over uint8 HWC images on device."""
-        imgs = torch.as_tensor(np.ascontiguousarray(images_u8)).to(self.device)
+    def evaluate_arrays(self, images, labels, batch=500):
+        """Eval-mode (running-stats BN) loss / accuracy over uint8 HWC images (or float NCHW
+        inputs) on device."""
+        imgs = self._device_inputs(images)
         labs = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
         n = imgs.shape[0]
         self.eval_meters.zero_()

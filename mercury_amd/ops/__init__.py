@@ -75,10 +75,11 @@ from .head import head_fwd, head_bwd  # noqa: E402
 from .importance import pool_build, is_sample, gather  # noqa: E402
 from .table import ImportanceTable  # noqa: E402
 from .optim import FlatOptimizer  # noqa: E402
-from .misc import quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad  # noqa: E402
+from .misc import (quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad,  # noqa: E402
+                   nchw_to_nhwc8)
 
 __all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
            'pack_conv_weight', 'to_nhwc', 'from_nhwc', 'bn_apply', 'bn_bwd', 'BnRunTable',
            'head_fwd', 'head_bwd', 'pool_build', 'is_sample', 'gather', 'ImportanceTable',
            'FlatOptimizer', 'quantize', 'pool2d_fwd', 'maxpool2d_bwd',
-           'dwconv_fwd', 'dwconv_dgrad', 'dwconv_wgrad']
+           'dwconv_fwd', 'dwconv_dgrad', 'dwconv_wgrad', 'nchw_to_nhwc8']

@@ -9,14 +9,21 @@ from ..data.transforms import CIFAR_MEAN, CIFAR_STD
 
 def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed, pad=4,
                flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD, shuffle=True):
-    """Build a P-sample presample pool from the uint8 shard [Ns][H][W][3] on device."""
-    _chk(shard, torch.uint8, 'shard')
+    """Build a P-sample presample pool on device from either the uint8 image shard
+    [Ns][H][W][3] (crop/flip/normalise on the fly) or a pre-converted bf16 shard
+    [Ns][H][W][8] (non-image inputs: plain gather, no augmentation)."""
     _chk(labels, torch.int64, 'labels')
+    prebuilt = shard.dtype == torch.bfloat16
+    if not prebuilt:
+        _chk(shard, torch.uint8, 'shard')
+    elif shard.shape[-1] != 8:
+        raise ValueError('pre-converted shard must be NHWC bf16 with 8 channels')
     Ns, H, W, _ = shard.shape
     _chk(pool, torch.bfloat16, 'pool', P * H * W * 8)
     lib().pool_build(ptr(shard), ptr(labels), ptr(ctrl), ptr(pool), ptr(pool_label),
                      ptr(pool_index), Ns, H, W, P, batch, pad, int(flip), int(augment), int(shuffle),
-                     int(seed) & 0xffffffff, list(mean), [1.0 / s for s in std], stream_ptr())
+                     int(seed) & 0xffffffff, list(mean), [1.0 / s for s in std], stream_ptr(),
+                     int(prebuilt))
 
 
 def is_sample(losses, ema, ctrl, idx, w, P, B, group, alpha=0.5, ema_alpha=0.9, seed=0,

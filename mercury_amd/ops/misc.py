@@ -36,3 +36,13 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad):
 
 def dwconv_wgrad(dy, x, dw, N, H, W, C, P, Q, stride, pad):
     lib().dwconv_wgrad(ptr(dy), ptr(x), ptr(dw), N, H, W, C, P, Q, stride, pad, stream_ptr())
+
+
+def nchw_to_nhwc8(x, y):
+    """float32 [N][C][H][W] -> bf16 [N][H][W][Cpad] (channels zero-padded), on device."""
+    _chk(x, torch.float32, 'x')
+    N, C, H, W = x.shape
+    Cpad = y.shape[-1]
+    _chk(y, torch.bfloat16, 'y', N * H * W * Cpad)
+    lib().nchw_to_nhwc8(ptr(x), ptr(y), N, C, H, W, Cpad, stream_ptr())
+    return y

@@ -27,6 +27,19 @@ def test_other_models_lower():
     assert lw.blocks[0].pool == (3, 2, 1)
     lw = lower(MobileNetV2(100))
     assert sum(1 for b in lw.blocks for u in b.units if u.depthwise) == 17
-    assert supports(MobileNetV2()) and not supports(VGG('VGG11', 30))
-    with pytest.raises(TypeError):
-        lower(VGG('VGG11', 30))
+    assert supports(MobileNetV2()) and supports(VGG('VGG11', 30))
+
+
+@pytest.mark.parametrize('name,nconv', [('VGG11', 8), ('VGG16', 13)])
+def test_vgg_lowering(name, nconv):
+    """Speech VGG: one-unit blocks (conv+bias, BN, ReLU), 2x2 pools where the config has 'M',
+    flatten + fc1 + fc2 head; every parameter laid out in registration order."""
+    net = VGG(name, 30)
+    lw = lower(net)
+    assert len(lw.blocks) == nconv and lw.head_pool == 'mlp2'
+    assert sum(1 for b in lw.blocks if b.pool) == 5
+    assert all(b.units[0].b_seg is not None for b in lw.blocks)
+    assert lw.in_channels == 1 and lw.num_classes == 30
+    assert lw.fc1_w.param is net.fc1.weight and lw.fc_w.param is net.fc2.weight
+    assert [s.name for s in lw.segs] == [n for n, _ in net.named_parameters()]
+    assert not lw.blocks[0].need_dx and not lw.blocks[0].units[0].need_dgrad
