@@ -24,7 +24,7 @@ struct EpiParams {
   const float* bias;  // [N] or null
   float* stats;       // BN sums: [G][2][stats_ld] (sum, sumsq) or null
   int stats_ld;
-  int group_rows;     // rows per ghost-BN group (tile never straddles a group)
+  int group_rows;     // rows per ghost-BN group (>= BM; a tile straddles at most one boundary)
   int accumulate;     // out += result
   float* slab;        // split-K workspace (set by the launcher's caller when splits > 1)
   // Fused BN-backward reduction over the FINAL output values g (a gradient wrt the output of

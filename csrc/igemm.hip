@@ -51,7 +51,7 @@ MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 template <int BM, int BN>
 struct Smem {
   static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
-  static constexpr int RED_BYTES = 3 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
+  static constexpr int RED_BYTES = 4 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
   static constexpr int bytes(int stages) {
     return stages * STAGE * 2 > RED_BYTES ? stages * STAGE * 2 : RED_BYTES;
   }
@@ -95,11 +95,16 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
   const int wm = w >> 1, wn = w & 1;
   const bool stats = e.stats != nullptr;
   const bool bw = e.bw_sums != nullptr;
-  float* red = (float*)smem;                       // [2][BN] sum, sumsq  |  [3][BN] bwd sums
-  bf16* tile = (bf16*)(smem + 3 * BN * 4);         // [BM][LDT] staged output
+  float* red = (float*)smem;   // [2][2][BN] (group, sum|sumsq)  |  [3][BN] bwd sums
+  bf16* tile = (bf16*)(smem + 4 * BN * 4);         // [BM][LDT] staged output
   if (stats || bw) {
-    for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
+    for (int i = tid; i < 4 * BN; i += NT) red[i] = 0.f;
   }
+  // ghost-BN groups: a tile may straddle ONE group boundary (groups are >= BM rows), e.g. when
+  // the per-image pixel count is odd (speech VGG 101x161); rows >= bnd go to group g + 1
+  const int g0 = stats ? m0 / e.group_rows : 0;
+  const int bnd = stats ? (g0 + 1) * e.group_rows : 0;
+  const bool straddle = stats && bnd < m0 + BM && bnd < M;
   float4 bias[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) bias[tn] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -116,6 +121,7 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
   for (int tn = 0; tn < TN; ++tn) {
     const int nl = wn * (BN / 2) + tn * 16 + 4 * (lane >> 4);
     float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+    float s2[4] = {0.f, 0.f, 0.f, 0.f}, ss2[4] = {0.f, 0.f, 0.f, 0.f};
     const float bb[4] = {bias[tn].x, bias[tn].y, bias[tn].z, bias[tn].w};
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -124,12 +130,22 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j] + bb[j]);
       *(bf16x4*)(tile + ml * LDT + nl) = o;   // one 8-byte LDS write per lane
-      if (stats && mrow + tm * 16 < M) {
+      const int row = mrow + tm * 16;
+      if (stats && row < M) {
+        if (!straddle || row < bnd) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float f = bf2f(o[j]);
-          s[j] += f;
-          ss[j] += f * f;
+          for (int j = 0; j < 4; ++j) {
+            const float f = bf2f(o[j]);
+            s[j] += f;
+            ss[j] += f * f;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float f = bf2f(o[j]);
+            s2[j] += f;
+            ss2[j] += f * f;
+          }
         }
       }
     }
@@ -139,24 +155,36 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
         s[j] = row16_sum(s[j]);
         ss[j] = row16_sum(ss[j]);
       }
+      if (straddle) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s2[j] = row16_sum(s2[j]);
+          ss2[j] = row16_sum(ss2[j]);
+        }
+      }
       if ((lane & 15) == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           atomicAdd(&red[nl + j], s[j]);
           atomicAdd(&red[BN + nl + j], ss[j]);
+          if (straddle) {
+            atomicAdd(&red[2 * BN + nl + j], s2[j]);
+            atomicAdd(&red[3 * BN + nl + j], ss2[j]);
+          }
         }
       }
     }
   }
   __syncthreads();
   if (stats) {
-    const int g = m0 / e.group_rows;
-    float* dst = e.stats + (size_t)g * 2 * e.stats_ld;
-    for (int i = tid; i < BN; i += NT) {
-      const int col = n0 + i;
-      if (col < N) {
-        atomicAdd(dst + col, red[i]);
-        atomicAdd(dst + e.stats_ld + col, red[BN + i]);
+    for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
+      float* dst = e.stats + (size_t)(g0 + gi) * 2 * e.stats_ld;
+      for (int i = tid; i < BN; i += NT) {
+        const int col = n0 + i;
+        if (col < N) {
+          atomicAdd(dst + col, red[2 * BN * gi + i]);
+          atomicAdd(dst + e.stats_ld + col, red[2 * BN * gi + BN + i]);
+        }
       }
     }
   }

@@ -64,16 +64,18 @@ def pick_tiles(M, Ncols, kchunks, group_rows=0, min_blocks=CU):
     """(bm, bn, splits) for the NT implicit GEMM."""
     bn = 64 if Ncols <= 64 else 128
     cands = [128, 64] if bn == 128 else [256, 128, 64]
+    # ghost-BN groups need not be tile multiples: the epilogue splits a tile that straddles
+    # one group boundary (requires group_rows >= bm)
     grp = group_rows if group_rows and group_rows < M else 0
     bm = None
     for c in cands:
-        if grp and grp % c:
+        if grp and grp < c:
             continue
         bm = c
         if math.ceil(M / c) * math.ceil(Ncols / bn) >= min_blocks:
             break
     if bm is None:
-        raise ValueError('no tile divides the BN ghost group (%d rows)' % group_rows)
+        raise ValueError('BN ghost group (%d rows) smaller than every tile' % group_rows)
     blocks = math.ceil(M / bm) * math.ceil(Ncols / bn)
     ktiles = math.ceil(kchunks / 8)
     splits = 1

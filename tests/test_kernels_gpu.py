@@ -88,20 +88,27 @@ def test_conv_fwd_all_tiles(bm_bn_split):
     close(out.view(4, 16, 16, 128).permute(0, 3, 1, 2), F.conv2d(x, w, padding=1))
 
 
-def test_conv_ghost_group_stats():
+@pytest.mark.parametrize('case,gimgs', [((64, 8, 8, 64, 64, 3, 3, 1, 1), 32),
+                                        ((12, 7, 9, 32, 64, 3, 3, 1, 1), 4),
+                                        ((8, 11, 13, 64, 128, 3, 3, 1, 1), 2)])
+def test_conv_ghost_group_stats(case, gimgs):
+    """Per-group BN sums from the conv epilogue, incl. groups that are not a tile multiple
+    (odd pixel counts: tiles straddle a group boundary)."""
     ops = _ops()
     from mercury_amd.ops.conv import ConvSpec
-    N = 64
-    case = (N, 8, 8, 64, 64, 3, 3, 1, 1)
+    N, K = case[0], case[4]
+    G = N // gimgs
     x, w = _mk(case, 1)
-    spec = ConvSpec(*case, group_rows=32 * 64)
-    out = torch.empty(spec.M, 64, dtype=torch.bfloat16, device=DEV)
-    stats = torch.zeros(2, 2, 64, device=DEV)
+    spec = ConvSpec(*case)
+    spec.group_rows = gimgs * spec.P * spec.Q
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(G, 2, K, device=DEV)
     ops.conv_fwd(ops.to_nhwc(x), ops.pack_conv_weight(w)[0], out, spec, stats=stats)
     ref = bf(F.conv2d(x, w, padding=1))
-    for gi in range(2):
-        r = ref[gi * 32:(gi + 1) * 32]
+    for gi in range(G):
+        r = ref[gi * gimgs:(gi + 1) * gimgs]
         close(stats[gi, 0], r.sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+        close(stats[gi, 1], r.pow(2).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
 
 
 @pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] % 8 == 0])

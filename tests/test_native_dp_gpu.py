@@ -100,5 +100,7 @@ def test_native_trainer_api_checkpoint(tmp_path):
     # HBM importance table: scored samples carry their latest loss and scoring step
     tab = tr.engine.table
     scored = tab.group > 0
-    assert int(scored.sum()) > 0 and bool((tab.importance[scored] > 0).all())
+    # (a confidently classified sample can score exactly 0.0 in fp32)
+    assert int(scored.sum()) > 0 and bool((tab.importance[scored] >= 0).all())
+    assert float(tab.importance[scored].sum()) > 0
     assert torch.equal(tr2.engine.table.importance, tab.importance)
