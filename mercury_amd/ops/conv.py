@@ -100,19 +100,31 @@ def fwd_plan(spec: ConvSpec):
 
 
 def dgrad_plan(spec: ConvSpec):
+    """dgrad tiles.  Measured at the train batch (bench/bwd_pair_sweep.py, MI355X): the dgrad
+    half of the pair launch is fastest with narrow 64x64 tiles reaching ~2 blocks per CU
+    before any K split (e.g. 32x32x64 3x3: 22 us vs 31 us with 128x64 tiles)."""
     kchunks = spec.R * spec.S * cpad8(spec.K) // 8
-    return pick_tiles(spec.N * spec.H * spec.W, spec.Cp, kchunks, 0)
+    M, N = spec.N * spec.H * spec.W, spec.Cp
+    ktiles = math.ceil(kchunks / 8)
+    tiles = math.ceil(M / 64) * math.ceil(N / 64)
+    if tiles <= 2 * CU and ktiles >= 4 and N <= 128:
+        splits = max(1, min(2 * CU // tiles, ktiles // 4, 16))
+        return 64, 64, splits
+    return pick_tiles(M, N, kchunks, 0)
 
 
 def wgrad_plan(spec: ConvSpec):
+    """wgrad tiles + pixel split.  Measured (bench/bwd_pair_sweep.py): ~1 block per CU total,
+    each K-split covering >= 4 pixel tiles (fewer fp32 atomics into the flat gradient), 64x64
+    tiles up to K=256 / 1152 columns, 128x128 beyond."""
     ncols = spec.R * spec.S * spec.Cp
-    bm = 64 if spec.K <= 64 else 128
-    bn = 64 if ncols <= 64 or spec.K > 256 and ncols < 1024 else 128
+    if spec.K <= 256 and ncols <= 1152:
+        bm, bn = 64, 64
+    else:
+        bm, bn = 128, 128
     blocks = math.ceil(spec.K / bm) * math.ceil(ncols / bn)
     ptiles = math.ceil(spec.M / 64)
-    splits = 1
-    if blocks < CU:
-        splits = max(1, min(math.ceil(2 * CU / blocks), ptiles // 4, 64))
+    splits = max(1, min(int(round(CU / blocks)), max(1, ptiles // 4), 64))
     return bm, bn, splits
 
 
