@@ -107,25 +107,30 @@ def dgrad_plan(spec: ConvSpec):
     M, N = spec.N * spec.H * spec.W, spec.Cp
     ktiles = math.ceil(kchunks / 8)
     tiles = math.ceil(M / 64) * math.ceil(N / 64)
-    if tiles <= 2 * CU and ktiles >= 4 and N <= 128:
+    if tiles <= 2 * CU and ktiles >= 4:
         splits = max(1, min(2 * CU // tiles, ktiles // 4, 16))
         return 64, 64, splits
     return pick_tiles(M, N, kchunks, 0)
 
 
+ATOMIC_BUDGET = 1_200_000   # fp32 atomic adds per wgrad launch before splitting stops paying
+
+
 def wgrad_plan(spec: ConvSpec):
-    """wgrad tiles + pixel split.  Measured (bench/bwd_pair_sweep.py): ~1 block per CU total,
-    each K-split covering >= 4 pixel tiles (fewer fp32 atomics into the flat gradient), 64x64
-    tiles up to K=256 / 1152 columns, 128x128 beyond."""
+    """wgrad tiles + pixel split.  Measured (bench/bwd_pair_sweep.py, MI355X, B=32): ~1 block
+    per CU, each K-split covering >= 4 pixel tiles, and at most ~1.2M fp32 atomics per launch
+    (layer4 3x3 512->512: split 1 = 22 us vs split 2 = 36 us); 64x64 tiles unless the weight
+    gradient itself exceeds that budget (then 128x128, unsplit)."""
     ncols = spec.R * spec.S * spec.Cp
-    if spec.K <= 256 and ncols <= 1152:
+    out = spec.K * ncols                      # fp32 elements each K-split adds atomically
+    if out <= ATOMIC_BUDGET:
         bm, bn = 64, 64
     else:
         bm, bn = 128, 128
     blocks = math.ceil(spec.K / bm) * math.ceil(ncols / bn)
     ptiles = math.ceil(spec.M / 64)
-    splits = max(1, min(int(round(CU / blocks)), max(1, ptiles // 4), 64))
-    return bm, bn, splits
+    splits = min(int(round(CU / blocks)), ATOMIC_BUDGET // out, ptiles // 4, 64)
+    return bm, bn, max(1, splits)
 
 
 def _slab(slab, need, device):
