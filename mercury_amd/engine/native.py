@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..ops import tune
 from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
@@ -65,8 +66,10 @@ class NativeEngine(object):
                  weight_decay=0.0, momentum=0.9, seed=0, alpha=0.5, ema_alpha=0.9,
                  importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
                  sampler='alias', exchange_scores=False, global_table=True, score='loss',
-                 global_ema=False):
+                 global_ema=False, autotune=None):
         ops.lib()
+        if autotune is not None:
+            tune.enable(autotune)
         self.net = net
         self.device = torch.device(device)
         self.lw = lower(net)
@@ -215,13 +218,18 @@ class NativeEngine(object):
                     sp.group_rows = group_imgs * sp.P * sp.Q
                 m.spec[u.name] = sp
                 if not u.depthwise:
-                    m.plan[u.name, 'fwd'] = p = fwd_plan(sp)
-                    slab = max(slab, slab_bytes(sp.M, sp.K, *p))
+                    # measured-best plans from the tuning cache (ops/tune.py) when present
+                    m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(sp, fwd_plan(sp))
+                    slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
                     if train:
+                        if u.need_dgrad and sp.K % 8 == 0:
+                            dp, wp = tune.bwd_plans_for(sp, dgrad_plan(sp), wgrad_plan(sp))
+                        else:
+                            dp, wp = dgrad_plan(sp), wgrad_plan(sp)
                         if u.need_dgrad:
-                            m.plan[u.name, 'dgrad'] = p = dgrad_plan(sp)
-                            slab = max(slab, slab_bytes(N * h * w, sp.Cp, *p))
-                        m.plan[u.name, 'wgrad'] = wgrad_plan(sp)
+                            m.plan[u.name, 'dgrad'] = dp
+                            slab = max(slab, slab_bytes(N * h * w, sp.Cp, *dp))
+                        m.plan[u.name, 'wgrad'] = wp
                 m.buf[u.name, 'y'] = act(sp.M, u.K)
                 m.stats[u.name] = nstats
                 nstats += m.G * 2 * u.K

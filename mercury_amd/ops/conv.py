@@ -150,7 +150,10 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * Cp)
     _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
     _chk(stats, torch.float32, 'stats')
-    bm, bn, splits = plan or fwd_plan(spec)
+    plan = plan or fwd_plan(spec)
+    bm, bn, splits = plan[:3]
+    if pipe is None and len(plan) > 3 and plan[3] is not None:
+        pipe = plan[3]                       # tuned pipeline variant (ops/tune.py)
     if splits > 1:
         slab = _slab(slab, slab_bytes(spec.M, spec.K, bm, bn, splits), x.device)
     grp = spec.group_rows if spec.group_rows else spec.M

@@ -1,0 +1,199 @@
+"""Per-shape kernel-plan autotuner with a persistent cache (the MIOpen "find" idea, for our
+own kernels).
+
+The implicit-GEMM conv kernels take a plan -- (tile M, tile N, K-splits[, pipe]) for the
+forward / data-gradient GEMM and (tile, pixel-splits) for the weight gradient.  The best plan
+depends on the shape and batch in ways heuristics only approximate (bench/fwd_sweep.py,
+bench/bwd_pair_sweep.py: 10-35 % per layer between the heuristic and the best candidate at
+batch 32).  So:
+
+* ``fwd_plan_for(spec)`` / ``bwd_plans_for(spec)`` return the cached best plan for the exact
+  (shape, ghost-group, batch) key when present, else -- if tuning is enabled
+  (``MERCURY_TUNE=1`` or ``enable(True)``) -- time every candidate on the device right
+  now (event-timed median, a few ms per shape) and cache the winner, else fall back to the
+  heuristic in ``conv.py``;
+* the cache is JSON (``tune_cache.json`` next to this file, shipped with the repo, tuned on
+  MI355X) plus an optional user file (``MERCURY_TUNE_CACHE``); new results are written back.
+
+Tuning runs only outside graph capture (the engine builds its plans when it allocates a
+batch mode, before any capture).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import threading
+
+import torch
+
+_LOCK = threading.Lock()
+_BUILTIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'tune_cache.json')
+_CACHE = None
+_ENABLED = os.environ.get('MERCURY_TUNE', '0') == '1'
+_DIRTY = False
+
+
+def enable(flag=True):
+    global _ENABLED
+    _ENABLED = bool(flag)
+
+
+def enabled():
+    return _ENABLED
+
+
+def _path():
+    return os.environ.get('MERCURY_TUNE_CACHE', _BUILTIN)
+
+
+def _load():
+    global _CACHE
+    if _CACHE is None:
+        _CACHE = {}
+        for p in dict.fromkeys([_BUILTIN, _path()]):
+            if os.path.exists(p):
+                try:
+                    with open(p) as f:
+                        _CACHE.update(json.load(f))
+                except (OSError, ValueError):
+                    pass
+    return _CACHE
+
+
+def save(path=None):
+    """Write the cache (tuned entries included) to ``path`` (default: the active cache file)."""
+    global _DIRTY
+    with _LOCK:
+        data = dict(sorted(_load().items()))
+        path = path or _path()
+        tmp = path + '.tmp'
+        with open(tmp, 'w') as f:
+            json.dump(data, f, indent=0, sort_keys=True)
+        os.replace(tmp, path)
+        _DIRTY = False
+    return path
+
+
+def cache():
+    return _load()
+
+
+def _key(kind, sp):
+    return '%s|%d|%d|%d|%d|%d|%d|%d|%d|%d|%d' % (kind, sp.N, sp.H, sp.W, sp.C, sp.K, sp.R, sp.S,
+                                                  sp.stride, sp.pad, sp.group_rows or 0)
+
+
+def _time(fn, iters=15):
+    fn()
+    torch.cuda.synchronize()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    fn()
+    t1.record()
+    torch.cuda.synchronize()
+    if t0.elapsed_time(t1) > 1.0:          # big shapes: fewer repetitions
+        iters = min(iters, 5)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    ev[0].record()
+    for i in range(iters):
+        fn()
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(iters))
+    return ts[len(ts) // 2]
+
+
+def _fwd_candidates(sp):
+    kt = math.ceil(sp.R * sp.S * sp.Cp / 64)
+    out = []
+    for bm, bn in ((256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
+        if sp.group_rows and sp.group_rows < bm:
+            continue
+        if bn == 128 and sp.K <= 64:
+            continue
+        for s in (1, 2, 4, 8):
+            if s <= max(1, kt // 2):
+                for pipe in (0, 3):
+                    out.append((bm, bn, s, pipe))
+    return out
+
+
+def _bwd_candidates(sp):
+    kt = math.ceil(sp.R * sp.S * sp.K / 64)
+    ptiles = math.ceil(sp.M / 64)
+    d = [(bm, bn, s) for bm, bn in ((128, 128), (128, 64), (64, 128), (64, 64))
+         for s in (1, 2, 4, 8) if s <= max(1, kt // 2)]
+    w = [(bm, bn, s) for bm, bn in ((128, 128), (64, 128), (64, 64))
+         for s in (1, 2, 4, 8, 16, 32) if s <= ptiles]
+    return d, w
+
+
+def fwd_plan_for(sp, heuristic):
+    """(bm, bn, splits, pipe) for the forward conv of ``sp``."""
+    c = _load()
+    k = _key('fwd', sp)
+    if k in c:
+        return tuple(c[k])
+    if not (_ENABLED and torch.cuda.is_available()) or torch.cuda.is_current_stream_capturing():
+        return tuple(heuristic) + (None,) if len(heuristic) == 3 else tuple(heuristic)
+    from . import conv as cv
+    dev = 'cuda'
+    x = torch.randn(sp.N * sp.H * sp.W * sp.Cp, device=dev).to(torch.bfloat16)
+    w = torch.randn(sp.K * sp.R * sp.S * sp.Cp, device=dev).to(torch.bfloat16) * 0.05
+    y = torch.empty(sp.M * sp.K, dtype=torch.bfloat16, device=dev)
+    G = max(1, sp.M // sp.group_rows) if sp.group_rows else 1
+    stats = torch.zeros(G * 2 * sp.K, device=dev)
+    cands = _fwd_candidates(sp)
+    slab = torch.zeros(max([cv.slab_bytes(sp.M, sp.K, *p[:3]) for p in cands] + [4]) // 4 + 1,
+                       device=dev)
+    best = None
+    for p in cands:
+        t = _time(lambda: cv.conv_fwd(x, w, y, sp, stats=stats, slab=slab, plan=p))
+        if best is None or t < best[0]:
+            best = (t, p)
+    with _LOCK:
+        c[k] = list(best[1])
+    _mark_dirty()
+    return best[1]
+
+
+def bwd_plans_for(sp, dheur, wheur):
+    """((bm, bn, splits), (wbm, wbn, wsplits)) for the dgrad+wgrad pair of ``sp``."""
+    c = _load()
+    k = _key('bwd', sp)
+    if k in c:
+        d, w = c[k]
+        return tuple(d), tuple(w)
+    if not (_ENABLED and torch.cuda.is_available()) or torch.cuda.is_current_stream_capturing():
+        return tuple(dheur), tuple(wheur)
+    from . import conv as cv
+    dev = 'cuda'
+    Mx = sp.N * sp.H * sp.W
+    dy = torch.randn(sp.M * sp.K, device=dev).to(torch.bfloat16)
+    wt = torch.randn(sp.Cp * sp.R * sp.S * sp.K, device=dev).to(torch.bfloat16) * 0.05
+    x = torch.randn(Mx * sp.Cp, device=dev).to(torch.bfloat16)
+    dx = torch.empty(Mx * sp.Cp, dtype=torch.bfloat16, device=dev)
+    dw = torch.zeros(sp.K * sp.R * sp.S * sp.C, device=dev)
+    dc, wc = _bwd_candidates(sp)
+    slab = torch.zeros(max([cv.slab_bytes(Mx, sp.Cp, *p) for p in dc] + [4]) // 4 + 1, device=dev)
+    best = None
+    # coordinate search: best dgrad plan with the heuristic wgrad, then best wgrad with it
+    dbest = min(dc, key=lambda p: _time(lambda: cv.conv_bwd(dy, wt, dx, x, dw, sp, dplan=p,
+                                                            wplan=wheur, slab=slab), 9))
+    for wp in wc:
+        t = _time(lambda: cv.conv_bwd(dy, wt, dx, x, dw, sp, dplan=dbest, wplan=wp, slab=slab))
+        if best is None or t < best[0]:
+            best = (t, wp)
+    with _LOCK:
+        c[k] = [list(dbest), list(best[1])]
+    _mark_dirty()
+    return tuple(dbest), tuple(best[1])
+
+
+def _mark_dirty():
+    global _DIRTY
+    _DIRTY = True
+    if os.environ.get('MERCURY_TUNE_SAVE', '1') == '1' and _path() != _BUILTIN:
+        save()
