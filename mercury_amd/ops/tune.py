@@ -17,6 +17,14 @@ batch 32).  So:
 
 Tuning runs only outside graph capture (the engine builds its plans when it allocates a
 batch mode, before any capture).
+
+Measured caveat (MI355X, round 1): plans that win in isolation LOST in the two-stream IS step
+(ResNet-18 1.67 -> 1.71-1.74 ms/step, MobileNetV2 4.37 -> 4.47-4.52; all-shape, pipe-0-only
+and train-batch-only caches alike): split-K and small tiles that shorten one kernel alone add
+blocks and slab traffic that the concurrently running scoring stream pays for.  The shipped
+cache is therefore empty and the heuristics -- derived from the same sweeps but chosen for
+the concurrent step -- are the default; the tuner is the tool for single-stream workloads
+and for re-deriving the heuristics.
 """
 from __future__ import annotations
 
@@ -32,6 +40,10 @@ _BUILTIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'tune_cache.
 _CACHE = None
 _ENABLED = os.environ.get('MERCURY_TUNE', '0') == '1'
 _DIRTY = False
+# pipeline variants tried for the forward GEMM.  The LDS-DMA ring (pipe 3) wins several shapes
+# in isolation but holds a whole CU per block; in the two-stream step it slowed the step
+# (ResNet-18 1.67 -> 1.71 ms), so only the register-staged loop is tuned by default.
+PIPES = tuple(int(p) for p in os.environ.get('MERCURY_TUNE_PIPES', '0').split(','))
 
 
 def enable(flag=True):
@@ -115,7 +127,7 @@ def _fwd_candidates(sp):
             continue
         for s in (1, 2, 4, 8):
             if s <= max(1, kt // 2):
-                for pipe in (0, 3):
+                for pipe in PIPES:
                     out.append((bm, bn, s, pipe))
     return out
 
