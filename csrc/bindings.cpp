@@ -85,6 +85,20 @@ PYBIND11_MODULE(_C, m) {
     comm_ring_allreduce(c, buf, count, work, avg, st);
     check_launch("comm_ring_allreduce");
   });
+  // a HIP stream whose kernels may only use the CUs set in `mask` (bit i = CU i); wrapped on
+  // the Python side with torch.cuda.ExternalStream
+  m.def("cu_mask_stream", [](std::vector<uint32_t> mask) {
+    hipStream_t st = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess)
+      throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+    return reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("cu_mask_of", [](uintptr_t st, int words) {
+    std::vector<uint32_t> mask((size_t)words, 0u);
+    (void)hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(st), (uint32_t)words, mask.data());
+    return mask;
+  });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};
     g.M = M;

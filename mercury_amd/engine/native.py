@@ -102,7 +102,7 @@ class NativeEngine(object):
         # MI355X it cost 2.4 % (1.897 vs 1.852 ms/step, ResNet-18) -- the extra stream hop
         # outweighs any dispatch-order gain
         prio = os.environ.get('MERCURY_STREAM_PRIO', '0') == '1'
-        self.s_score = torch.cuda.Stream(self.device, priority=0)
+        self.s_score = self._score_stream()
         self.s_train = torch.cuda.Stream(self.device, priority=-1) if prio else None
         # Optional side stream for weight gradients.  Off by default: measured on MI355X
         # (bench/host_overhead.py) a fork/join per conv inside a captured graph is spread
@@ -126,6 +126,26 @@ class NativeEngine(object):
         if world_size > 1 and (exchange_scores or global_ema):
             from ..parallel.scores import ScoreExchange
             self.score_exchange = ScoreExchange(self.P, self.device)
+
+    def _score_stream(self):
+        """The scoring stream.  ``MERCURY_SCORE_CU_FRAC`` (0 < f < 1) restricts it to that
+        fraction of the CUs (HIP CU-masked stream, every k-th CU kept so each XCD loses the
+        same share), so the latency-bound train kernels always find free CUs.  Off by default:
+        measured on MI355X the masked stream made the ResNet-18 step 2.54 ms at f = 0.5, 0.75
+        and 0.875 alike (1.65 ms unmasked) -- a fixed cost of the masked queue, not of the
+        CUs given up."""
+        frac = float(os.environ.get('MERCURY_SCORE_CU_FRAC', '1'))
+        if not 0.0 < frac < 1.0:
+            return torch.cuda.Stream(self.device, priority=0)
+        n = torch.cuda.get_device_properties(self.device).multi_processor_count
+        keep = [int(i * frac) != int((i + 1) * frac) for i in range(n)]   # evenly spread
+        words = [0] * ((n + 31) // 32)
+        for i, k in enumerate(keep):
+            if k:
+                words[i // 32] |= 1 << (i % 32)
+        ptr_ = ops.lib().cu_mask_stream(words)
+        self._cu_mask_words = words
+        return torch.cuda.ExternalStream(ptr_, device=self.device)
 
     # ------------------------------------------------------------------ parameters
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
