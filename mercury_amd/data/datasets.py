@@ -23,9 +23,13 @@ IMG_EXTENSIONS = ('.jpg', '.jpeg', '.png', '.ppm', '.bmp', '.pgm', '.tif', '.tif
 _CACHE = {}
 
 
-def synthetic_arrays(n, num_classes, shape=(32, 32, 3), seed=0, noise=48):
-    """Class-conditional synthetic images: template[class] + uniform noise."""
-    key = (n, num_classes, tuple(shape), seed, noise)
+def synthetic_arrays(n, num_classes, shape=(32, 32, 3), seed=0, noise=48, template_seed=None):
+    """Class-conditional synthetic images: template[class] + uniform noise.
+
+    The class templates come from ``template_seed`` (default: fixed per class count and
+    shape), NOT from ``seed`` -- so a train set and a test set drawn with different seeds share
+    the same classes and only their noise/labels differ."""
+    key = (n, num_classes, tuple(shape), seed, noise, template_seed)
     if key in _CACHE:
         return _CACHE[key]
     rng = np.random.RandomState(seed)
@@ -35,7 +39,9 @@ def synthetic_arrays(n, num_classes, shape=(32, 32, 3), seed=0, noise=48):
     rng.shuffle(y)
     # low-frequency templates so crops/flips keep the class signal
     h, w, c = shape
-    small = rng.randint(40, 216, size=(num_classes, 4, 4, c)).astype(np.float32)
+    tseed = template_seed if template_seed is not None else 0xC1A55 + 131 * num_classes + c
+    small = np.random.RandomState(tseed).randint(
+        40, 216, size=(num_classes, 4, 4, c)).astype(np.float32)
     tmpl = torch.nn.functional.interpolate(
         torch.from_numpy(small).permute(0, 3, 1, 2), size=(h, w), mode='bilinear',
         align_corners=False).permute(0, 2, 3, 1).numpy()

@@ -44,3 +44,17 @@ def test_noniid_loaders_world1_allowed():
     idx, data, label = next(iter(pres[0]))
     assert data.shape == (32, 3, 32, 32) and idx.shape == (32,)
     assert abs(float(data.mean())) < 3.0
+
+
+def test_synthetic_train_test_share_classes():
+    """Train and test synthetic CIFAR arrays come from different seeds but the SAME class
+    templates (otherwise held-out accuracy is meaningless)."""
+    from mercury_amd.data.datasets import load_cifar_arrays
+    xa, ya = load_cifar_arrays('/nonexistent', train=True)
+    xb, yb = load_cifar_arrays('/nonexistent', train=False)
+    assert not np.array_equal(xa[:100], xb[:100])
+    ma = np.stack([xa[ya == k][:500].mean(0) for k in range(10)])
+    mb = np.stack([xb[yb == k][:500].mean(0) for k in range(10)])
+    same = np.abs(ma - mb).mean()
+    cross = np.abs(ma - np.roll(mb, 1, axis=0)).mean()
+    assert same < 0.2 * cross, (same, cross)
