@@ -28,7 +28,8 @@ MA_DEV uint32_t pool_src(const PoolBuildArgs& a, int slot, int64_t& gb, int& t) 
   gb = pc * per_pool + j;
   const uint32_t epoch = (uint32_t)(gb / nb);
   const int bi = (int)(gb % nb);
-  const uint32_t pos = (uint32_t)(bi * a.batch + t);
+  // (% Ns only matters for a shard smaller than one batch: the batch cycles the shard)
+  const uint32_t pos = (uint32_t)((bi * a.batch + t) % a.Ns);
   return a.shuffle ? permute_index(pos, (uint32_t)a.Ns, a.seed, epoch)
                    : (uint32_t)((gb * a.batch + t) % a.Ns);
 }

@@ -585,9 +585,10 @@ class NativeEngine(object):
         """Keep this rank's training shard resident in HBM: uint8 [Ns][H][W][3] images, or
         float [Ns][C][H][W] inputs pre-converted to NHWC bf16."""
         x = self._device_inputs(images)
-        if x.shape[0] < self.B:
-            # the device epoch permutation draws whole batches from the shard
-            raise ValueError('shard has %d samples < batch %d' % (x.shape[0], self.B))
+        if x.shape[0] < 1:
+            raise ValueError('empty shard')
+        # (a shard smaller than one batch -- possible for a Dirichlet non-IID split at large
+        # world size -- is cycled: every batch is the shard's epoch permutation, wrapped)
         self.shard = x
         self.shard_labels = torch.as_tensor(np.asarray(labels), dtype=torch.int64).to(self.device)
         self.train_mode = self.mode('train', self.B, 0, True)

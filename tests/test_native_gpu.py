@@ -224,3 +224,23 @@ def test_vgg_speech_native_matches_torch():
         eng2.step()
     torch.cuda.synchronize()
     assert np.isfinite(eng2.read_meters()['loss_sum'])
+
+
+def test_tiny_shard_smaller_than_batch_cycles():
+    """A Dirichlet shard can be smaller than one batch at large world size: the pool cycles
+    the shard (every sample index stays in range) instead of failing."""
+    from mercury_amd.engine.native import NativeEngine
+    from mercury_amd.models import build_model
+    torch.manual_seed(0)
+    net = build_model('resnet18', 10).to(DEV)
+    eng = NativeEngine(net, DEV, 32, 10, use_graphs=False)
+    rng = np.random.RandomState(1)
+    eng.set_shard(rng.randint(0, 256, (10, 32, 32, 3), dtype=np.uint8), rng.randint(0, 10, 10))
+    eng.prime()
+    for _ in range(3):
+        eng.step()
+    torch.cuda.synchronize()
+    idx = eng.score_mode.index
+    assert int(idx.min()) >= 0 and int(idx.max()) < 10
+    assert sorted(set(idx[:10].tolist())) == list(range(10))    # one batch = a permutation, wrapped
+    assert np.isfinite(eng.read_meters()['loss_sum'])
