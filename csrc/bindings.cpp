@@ -187,11 +187,11 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t pool_label, uintptr_t pool_index, int Ns, int H, int W, int Pn,
                          int batch, int pad, int flip, int augment, int shuffle, uint32_t seed,
                          std::vector<float> mean, std::vector<float> inv_std, uintptr_t st,
-                         int prebuilt) {
+                         int prebuilt, uintptr_t zero, int nzero) {
     PoolBuildArgs a{P<const uint8_t>(shard), P<const int64_t>(labels), P<const int64_t>(ctrl),
                     P<bf16>(pool), P<int>(pool_label), P<int>(pool_index), Ns, H, W, Pn, batch,
                     pad, flip, augment, shuffle, seed, {mean[0], mean[1], mean[2]},
-                    {inv_std[0], inv_std[1], inv_std[2]}, prebuilt};
+                    {inv_std[0], inv_std[1], inv_std[2]}, prebuilt, P<float>(zero), nzero};
     pool_build_launch(a, S(st));
     check_launch("pool_build");
   });
@@ -270,8 +270,9 @@ PYBIND11_MODULE(_C, m) {
     transpose_weights_launch(P<const OptSeg>(segs), P<const int>(jobs), njobs, S(st));
     check_launch("transpose_weights");
   });
-  m.def("step_begin", [](uintptr_t ctrl, uintptr_t st) {
-    step_begin_launch(P<int64_t>(ctrl), S(st));
+  m.def("step_begin", [](uintptr_t ctrl, uintptr_t st, uintptr_t z0, int n0, uintptr_t z1,
+                         int n1) {
+    step_begin_launch(P<int64_t>(ctrl), P<float>(z0), n0, P<float>(z1), n1, S(st));
     check_launch("step_begin");
   });
 

@@ -36,8 +36,13 @@ MA_DEV uint32_t pool_src(const PoolBuildArgs& a, int slot, int64_t& gb, int& t) 
 
 // Pre-converted shard (non-image inputs, e.g. the speech VGG's 1x101x161 spectrograms, stored
 // once as NHWC bf16 with channels padded to 8): the pool is a straight 16-byte-chunk gather.
+MA_DEV void zero_slice(const PoolBuildArgs& a) {
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < a.nzero; j += gridDim.x * 256) a.zero[j] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void pool_take_kernel(PoolBuildArgs a) {
   const int slot = blockIdx.x;
+  if (a.zero) zero_slice(a);
   int64_t gb;
   int t;
   const uint32_t src = pool_src(a, slot, gb, t);
@@ -53,6 +58,7 @@ __global__ __launch_bounds__(256) void pool_take_kernel(PoolBuildArgs a) {
 
 __global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
   const int slot = blockIdx.x;
+  if (a.zero) zero_slice(a);
   int64_t gb;
   int t;
   const uint32_t src = pool_src(a, slot, gb, t);

@@ -105,6 +105,8 @@ struct PoolBuildArgs {
   uint32_t seed;
   float mean[3], inv_std[3];
   int prebuilt;                  // shard is already NHWC bf16 [Ns][H][W][8]: plain gather
+  float* zero;                   // optional buffer zeroed by the launch (the pass's BN stats)
+  int nzero;
 };
 void pool_build_launch(const PoolBuildArgs& a, hipStream_t st);
 
@@ -193,7 +195,7 @@ struct OptArgs {
   int zero_grad;
 };
 void optimizer_launch(const OptArgs& a, hipStream_t st);
-void step_begin_launch(int64_t* ctrl, hipStream_t st);
+void step_begin_launch(int64_t* ctrl, float* z0, int n0, float* z1, int n1, hipStream_t st);
 // jobs: [njobs][4] = (segment index, r*S+s, k0, c0) -> one 64x64 tile each
 void transpose_weights_launch(const OptSeg* segs, const int* jobs, int njobs, hipStream_t st);
 void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long long total,

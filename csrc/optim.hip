@@ -132,7 +132,16 @@ __global__ __launch_bounds__(NT) void pack_kernel(const float* p, const OptSeg* 
   write_copies(sg, e - sg.off, p[e]);
 }
 
-__global__ void step_begin_kernel(int64_t* ctrl) { ctrl[2] += 1; }
+// start of a train step: bump the Adam step counter and zero the step's BN-statistics and
+// BN-backward-sum arenas (one launch instead of one kernel + two memsets on the critical path)
+__global__ __launch_bounds__(256) void step_begin_kernel(int64_t* ctrl, float* z0, int n0,
+                                                         float* z1, int n1) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl[2] += 1;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int stride = gridDim.x * 256;
+  for (int j = i; j < n0; j += stride) z0[j] = 0.f;
+  for (int j = i; j < n1; j += stride) z1[j] = 0.f;
+}
 }  // namespace
 
 void optimizer_launch(const OptArgs& a, hipStream_t st) {
@@ -151,6 +160,9 @@ void transpose_weights_launch(const OptSeg* segs, const int* jobs, int njobs, hi
     hipLaunchKernelGGL(transpose_weights_kernel, dim3(njobs), dim3(256), 0, st, segs, jobs);
 }
 
-void step_begin_launch(int64_t* ctrl, hipStream_t st) {
-  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, st, ctrl);
+void step_begin_launch(int64_t* ctrl, float* z0, int n0, float* z1, int n1, hipStream_t st) {
+  const int n = n0 > n1 ? n0 : n1;
+  int blocks = (n + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 256 ? 256 : blocks);
+  hipLaunchKernelGGL(step_begin_kernel, dim3(blocks), dim3(256), 0, st, ctrl, z0, n0, z1, n1);
 }

@@ -637,9 +637,8 @@ class NativeEngine(object):
             self.idx.copy_(self._arange_b)
             self.isw.fill_(1.0)
             return
-        sm.stats_arena.zero_()
         ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label, sm.index,
-                       self.P, self.B, self.seed)
+                       self.P, self.B, self.seed, zero=sm.stats_arena)
         x = self.forward(sm)
         self.head(sm, x, 'score')
         if self.table is not None:
@@ -687,9 +686,9 @@ class NativeEngine(object):
         segs = []
 
         def fwd_head():
-            ops.lib().step_begin(ops.ptr(self.ctrl), ops.stream_ptr())
-            tm.stats_arena.zero_()
-            tm.sums_arena.zero_()
+            ops.lib().step_begin(ops.ptr(self.ctrl), ops.stream_ptr(), ops.ptr(tm.stats_arena),
+                                 tm.stats_arena.numel(), ops.ptr(tm.sums_arena),
+                                 tm.sums_arena.numel())
             x = self.forward(tm)
             self.head(tm, x, 'train', isw=self.isw, meters=self.meters)
             last = len(self.lw.blocks) - 1

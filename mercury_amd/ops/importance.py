@@ -8,10 +8,11 @@ from ..data.transforms import CIFAR_MEAN, CIFAR_STD
 
 
 def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed, pad=4,
-               flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD, shuffle=True):
+               flip=True, augment=True, mean=CIFAR_MEAN, std=CIFAR_STD, shuffle=True, zero=None):
     """Build a P-sample presample pool on device from either the uint8 image shard
     [Ns][H][W][3] (crop/flip/normalise on the fly) or a pre-converted bf16 shard
-    [Ns][H][W][8] (non-image inputs: plain gather, no augmentation)."""
+    [Ns][H][W][8] (non-image inputs: plain gather, no augmentation).  ``zero``: an fp32
+    buffer the same launch zeroes (the scoring pass's BN-statistics arena)."""
     _chk(labels, torch.int64, 'labels')
     prebuilt = shard.dtype == torch.bfloat16
     if not prebuilt:
@@ -23,7 +24,7 @@ def pool_build(shard, labels, ctrl, pool, pool_label, pool_index, P, batch, seed
     lib().pool_build(ptr(shard), ptr(labels), ptr(ctrl), ptr(pool), ptr(pool_label),
                      ptr(pool_index), Ns, H, W, P, batch, pad, int(flip), int(augment), int(shuffle),
                      int(seed) & 0xffffffff, list(mean), [1.0 / s for s in std], stream_ptr(),
-                     int(prebuilt))
+                     int(prebuilt), ptr(zero), zero.numel() if zero is not None else 0)
 
 
 def is_sample(losses, ema, ctrl, idx, w, P, B, group, alpha=0.5, ema_alpha=0.9, seed=0,
