@@ -53,6 +53,23 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
     check_launch("igemm");
   });
+  // forward conv whose A operand is BN-applied + activated on load (ProParams, igemm.h)
+  m.def("igemm_pro", [](uintptr_t src, uintptr_t wt, uintptr_t out, int ldo, uintptr_t bias,
+                        uintptr_t stats, int stats_ld, int group_rows, uintptr_t slab, int SH,
+                        int SW, int SC, int RP, int RQ, int R, int Sk, int stride, int pad, int Kc,
+                        int Ncols, int M, int bm, int bn, int splits, uintptr_t st,
+                        uintptr_t p_stats, uintptr_t p_rmean, uintptr_t p_rvar, uintptr_t p_gamma,
+                        uintptr_t p_beta, uintptr_t p_keep, int p_group_rows, float p_inv_count,
+                        float p_eps, int p_act, int p_keep_tap) {
+    ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
+    EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows, 0,
+                P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
+    ProParams pr{P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
+                 P<const float>(p_gamma), P<const float>(p_beta), P<bf16>(p_keep), p_group_rows,
+                 p_inv_count, p_eps, p_act, p_keep_tap};
+    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, false, S(st), 0, &pr);
+    check_launch("igemm_pro");
+  });
   m.def("conv_bwd_pair", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int ldo, int accumulate,
                             uintptr_t slab, int SH, int SW, int SC, int RP, int RQ, int R, int Sk,
                             int stride, int pad, int Kc, int Ncols, int M, int bm, int bn,

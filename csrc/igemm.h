@@ -41,10 +41,35 @@ struct EpiParams {
   int bw_act;
 };
 
+// Forward-only A-operand prologue: the conv reads the PRODUCING conv's raw output y and applies
+// that layer's BatchNorm + activation per input channel while staging the tile,
+//   a = act(y * scale + shift),  scale = gamma * rsqrt(var + eps),  shift = beta - mean * scale
+// (batch / ghost-group statistics from the producer's epilogue sums, or running statistics),
+// so the normalised activation never makes its own HBM round trip.  Padding taps stay zero (the
+// zero lives in activation space).  ``keep`` (optional) receives the activation as well: the
+// chunk loaded at tap ``keep_tap`` of a stride-1 "same" conv is exactly the output pixel's own
+// input pixel, so the N-tile-0 blocks write every element of ``a`` once (train mode: backward
+// needs it).
+struct ProParams {
+  const float* stats;   // [G][2][SC] (sum, sumsq) of y per stat group, or null (running stats)
+  const float* rmean;   // running mean / var (used when stats == null)
+  const float* rvar;
+  const float* gamma;
+  const float* beta;
+  bf16* keep;           // [SH*SW*images][SC] activation write-back, or null
+  int group_rows;       // OUTPUT rows per stat group (a multiple of the tile's BM)
+  float inv_count;      // 1 / y-pixels per stat group
+  float eps;
+  int act;              // 0 none, 1 relu, 2 relu6
+  int keep_tap;         // r*S + s of the tap whose pixel is the output pixel itself
+};
+
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
-// pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages
+// pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages.
+// pro != null: BN-apply prologue (forward, pipe 0 only).
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
-                  int bn, int splits, bool trans, hipStream_t st, int pipe = 0);
+                  int bn, int splits, bool trans, hipStream_t st, int pipe = 0,
+                  const ProParams* pro = nullptr);
 
 struct WgradGeom {
   int N, H, W, C;     // input x (C padded), NHWC

@@ -440,10 +440,14 @@ MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& 
 
 // ---------------------------------------------------------------- register-staged loop
 // One (tile bx, K-split by) of the NT GEMM; gx tiles x gy splits in the launch.
-template <int BM, int BN, bool TRANS>
+// PRO: BN-apply + activation of the A operand between the global load and the LDS write
+// (ProParams in igemm.h).  Everything it needs for the chunk staged next -- the 8 channels'
+// statistics / gamma / beta, which rows are padding, where the activation is kept -- is loaded
+// or computed in load_stage, so it is in flight under the MFMA phase like the tile itself.
+template <int BM, int BN, bool TRANS, bool PRO = false>
 MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                           const ConvGeom& g, const EpiParams& e, int ktiles_per_split, char* smem,
-                          int bx, int by, int gx, int gy) {
+                          int bx, int by, int gx, int gy, const ProParams& pro) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;  // rows per thread for A / B staging
   bf16* sA = (bf16*)smem;
@@ -473,16 +477,45 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   const bf16* zp = g.zero;
 
   u32x4 ra[AR], rb[BR];
+  // prologue state for the chunk in flight (PRO only; dead code otherwise)
+  float4 pst[8];
+  int pz = 0;
+  int pko[AR];
+  const float* pbase = nullptr;
+  if constexpr (PRO) {
+    const int grp = m0 / pro.group_rows;
+    pbase = pro.stats ? pro.stats + (size_t)grp * 2 * g.SC : nullptr;
+  }
   auto load_stage = [&](int kt) {
     int r, s, c8;
     bool kval;
     kc.decode(g, kt, cc, r, s, c8, kval);
     kc.advance(g);
+    bool keep = false;
+    if constexpr (PRO) {
+      const int ch = kval ? c8 * 8 : 0;
+      const float* m0p = pbase ? pbase + ch : pro.rmean + ch;
+      const float* v0p = pbase ? pbase + g.SC + ch : pro.rvar + ch;
+      pst[0] = *(const float4*)m0p;
+      pst[1] = *(const float4*)(m0p + 4);
+      pst[2] = *(const float4*)v0p;
+      pst[3] = *(const float4*)(v0p + 4);
+      pst[4] = *(const float4*)(pro.gamma + ch);
+      pst[5] = *(const float4*)(pro.gamma + ch + 4);
+      pst[6] = *(const float4*)(pro.beta + ch);
+      pst[7] = *(const float4*)(pro.beta + ch + 4);
+      keep = pro.keep != nullptr && nt == 0 && kval && r * g.S + s == pro.keep_tap;
+      pz = 0;
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       int o = row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8);
       o = kval ? o : -1;                       // select, not a branch around the gather
       ra[i] = *(const u32x4*)(o >= 0 ? src + o : zp);
+      if constexpr (PRO) {
+        pz |= (o < 0 ? 1 : 0) << i;
+        pko[i] = keep ? o : -1;
+      }
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -493,6 +526,38 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   auto store_stage = [&](int buf) {
     bf16* a = sA + buf * Smem<BM, BN>::STAGE;
     bf16* b = a + BM * BK;
+    if constexpr (PRO) {
+      const float mv[8] = {pst[0].x, pst[0].y, pst[0].z, pst[0].w, pst[1].x, pst[1].y, pst[1].z, pst[1].w};
+      const float vv[8] = {pst[2].x, pst[2].y, pst[2].z, pst[2].w, pst[3].x, pst[3].y, pst[3].z, pst[3].w};
+      const float gv[8] = {pst[4].x, pst[4].y, pst[4].z, pst[4].w, pst[5].x, pst[5].y, pst[5].z, pst[5].w};
+      const float bv[8] = {pst[6].x, pst[6].y, pst[6].z, pst[6].w, pst[7].x, pst[7].y, pst[7].z, pst[7].w};
+      float sc[8], sh[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {   // same arithmetic as bn.hip scale_shift8
+        float mean = mv[k], var = vv[k];
+        if (pbase) {
+          mean = mv[k] * pro.inv_count;
+          var = fmaxf(vv[k] * pro.inv_count - mean * mean, 0.f);
+        }
+        sc[k] = gv[k] * rsqrtf(var + pro.eps);
+        sh[k] = bv[k] - mean * sc[k];
+      }
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const bf16x8 y = __builtin_bit_cast(bf16x8, ra[i]);
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = bf2f(y[k]) * sc[k] + sh[k];
+          if (pro.act == 1) v = fmaxf(v, 0.f);
+          else if (pro.act == 2) v = fminf(fmaxf(v, 0.f), 6.f);
+          o[k] = f2bf(v);
+        }
+        const u32x4 t = __builtin_bit_cast(u32x4, o);
+        ra[i] = ((pz >> i) & 1) ? u32x4{0u, 0u, 0u, 0u} : t;
+        if (pko[i] >= 0) *(u32x4*)(pro.keep + pko[i]) = ra[i];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = (tid >> 3) + 32 * i;
@@ -535,8 +600,20 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
                                                           ConvGeom g, EpiParams e,
                                                           int ktiles_per_split) {
   __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
+  const ProParams none{};
   igemm_nt_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x, blockIdx.y,
-                               gridDim.x, gridDim.y);
+                               gridDim.x, gridDim.y, none);
+}
+
+// forward conv with the BN-apply prologue on its input (ProParams)
+template <int BM, int BN>
+__global__ __launch_bounds__(NT, 2) void igemm_pro_kernel(const bf16* __restrict__ src,
+                                                           const bf16* __restrict__ wt,
+                                                           ConvGeom g, EpiParams e,
+                                                           int ktiles_per_split, ProParams pro) {
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
+  igemm_nt_body<BM, BN, false, true>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x,
+                                     blockIdx.y, gridDim.x, gridDim.y, pro);
 }
 
 // ---------------------------------------------------------------- LDS-DMA ring loop
@@ -660,10 +737,15 @@ inline void ig_grid(const ConvGeom& g, int BM, int BN, int splits, int& gx, int&
 
 template <int BM, int BN, bool TRANS>
 void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
-                int pipe, hipStream_t st) {
+                int pipe, hipStream_t st, const ProParams* pro) {
   int gx, per, gy;
   ig_grid(g, BM, BN, splits, gx, per, gy);
   if (gy == 1) e.slab = nullptr;
+  if (pro != nullptr && !TRANS) {
+    hipLaunchKernelGGL((igemm_pro_kernel<BM, BN>), dim3(gx, gy), dim3(NT), 0, st, src, wt, g, e,
+                       per, *pro);
+    return;
+  }
   launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), pipe, st);
 }
 
@@ -687,7 +769,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict_
     wgb::wgrad_body<WBM, WBN>(dy, x, wg, dw, wper, (bf16*)smem, b % wgx, b / wgx, wgy);
   } else {
     const int d = b - nw;
-    igemm_nt_body<DBM, DBN, true>(dy, wt, g, e, dper, smem, d % dgx, d / dgx, dgx, dgy);
+    const ProParams none{};
+    igemm_nt_body<DBM, DBN, true>(dy, wt, g, e, dper, smem, d % dgx, d / dgx, dgx, dgy, none);
   }
 }
 
@@ -720,14 +803,15 @@ static const bf16* zero_page() {
 }
 
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const EpiParams& e,
-                  int bm, int bn, int splits, bool trans, hipStream_t st, int pipe) {
+                  int bm, int bn, int splits, bool trans, hipStream_t st, int pipe,
+                  const ProParams* pro) {
   ConvGeom g = g_in;
   g.zero = zero_page();
-#define MA_CASE(BM_, BN_)                                                      \
-  if (bm == BM_ && bn == BN_) {                                                \
-    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, pipe, st);    \
-    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, pipe, st);         \
-    return;                                                                    \
+#define MA_CASE(BM_, BN_)                                                           \
+  if (bm == BM_ && bn == BN_) {                                                     \
+    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, pipe, st, nullptr); \
+    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, pipe, st, pro);          \
+    return;                                                                         \
   }
   MA_CASE(128, 128)
   MA_CASE(128, 64)

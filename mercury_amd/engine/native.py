@@ -33,6 +33,7 @@ import torch.distributed as dist
 from .. import ops
 from ..ops import tune
 from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
+from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
 from ..utils import profiling as prof
@@ -115,6 +116,8 @@ class NativeEngine(object):
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
         self.roctx = False               # per-phase roctx ranges around the step's host calls
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
+        # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
+        self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
         self.sampler = sampler
         if score not in ('loss', 'gradnorm'):
             raise ValueError('score must be loss or gradnorm')
@@ -313,7 +316,7 @@ class NativeEngine(object):
     def _beta(self, u, grad=False):
         return self._pview(u.beta_seg, grad)
 
-    def _conv_fwd(self, m, u, x, y, stats):
+    def _conv_fwd(self, m, u, x, y, stats, pro=None):
         sp = m.spec[u.name]
         if u.depthwise:
             ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
@@ -321,7 +324,25 @@ class NativeEngine(object):
         else:
             ops.conv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, slab=m.slab,
                          plan=m.plan[u.name, 'fwd'],
-                         bias=self._pview(u.b_seg) if u.b_seg is not None else None)
+                         bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
+
+    def _pro_for(self, m, u, nxt):
+        """BN-apply of ``u`` folded into the load of its consumer ``nxt`` (csrc/igemm.h
+        ProParams), or None when that conv/plan cannot take it.  Train mode also keeps the
+        activation (backward reads it) through the consumer's centre-tap write-back."""
+        if not self.fuse_bn_fwd or nxt.depthwise or u.act not in ('relu', 'relu6', 'none'):
+            return None
+        sp = m.spec[nxt.name]
+        if not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=m.train):
+            return None
+        su = m.spec[u.name]
+        d = dict(gamma=self._gamma(u), beta=self._beta(u), act=u.act, eps=BN_EPS,
+                 keep=m.buf[u.name, 'a'] if m.train else None)
+        if m.train or m.group_imgs:
+            d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
+        else:
+            d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+        return d
 
     def _bn_apply(self, m, u, y, out, act, res=None, res_unit=None):
         sp = m.spec[u.name]
@@ -346,10 +367,17 @@ class NativeEngine(object):
         for bi, blk in enumerate(self.lw.blocks):
             inp = x
             nu = len(blk.units)
+            pro = None
             for i, u in enumerate(blk.units):
                 y = m.buf[u.name, 'y']
-                self._conv_fwd(m, u, inp, y, m.stats[u.name] if stats_on else None)
+                self._conv_fwd(m, u, inp, y, m.stats[u.name] if stats_on else None, pro=pro)
                 if i < nu - 1:
+                    # intra-block BN + activation: inside the next conv's operand load when it
+                    # can take it, else its own pass
+                    pro = self._pro_for(m, u, blk.units[i + 1])
+                    if pro is not None:
+                        inp = y
+                        continue
                     a = m.buf[u.name, 'a']
                     self._bn_apply(m, u, y, a, u.act)
                     inp = a

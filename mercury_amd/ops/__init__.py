@@ -14,6 +14,7 @@ gradients and optimizer state fp32.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 
 import torch
@@ -26,6 +27,12 @@ def lib():
     """The loaded extension; builds it in-tree on first use if absent."""
     global _lib, _err
     if _lib is not None:
+        return _lib
+    alt = os.environ.get('MERCURY_EXT_PATH')
+    if alt:   # A/B builds: another build of the same extension (bench/build_variant.py)
+        spec = importlib.util.spec_from_file_location('mercury_amd._C', alt)
+        _lib = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(_lib)
         return _lib
     try:
         _lib = importlib.import_module('mercury_amd._C')

@@ -142,9 +142,47 @@ def _slab(slab, need, device):
         0 if slab is None else slab.numel() * slab.element_size(), need))
 
 
+def pro_ok(spec: ConvSpec, plan, keep=False):
+    """Can this forward conv take the BN-apply prologue (``conv_fwd(pro=...)``)?  Needs the
+    register-staged loop, real channels a multiple of 8, ghost-BN groups that are whole tiles,
+    and -- to keep the activation -- a stride-1 'same' conv (its centre tap is a bijection)."""
+    bm = plan[0]
+    pipe = plan[3] if len(plan) > 3 and plan[3] is not None else PIPE
+    if pipe != 0 or spec.C % 8:
+        return False
+    # pointwise convs only: a 3x3 conv re-loads every input chunk once per tap, and redoing the
+    # normalisation 9x in VALU made the conv 2-2.5x slower than a separate bn_apply pass
+    # (bench/pro_bench.py, MI355X: B=320 64->64 3x3 135 us vs 53 + 20 us)
+    if spec.R != 1 or spec.S != 1:
+        return False
+    if spec.group_rows and spec.group_rows < spec.M and spec.group_rows % bm:
+        return False
+    if keep and not (spec.stride == 1 and spec.R == spec.S and spec.R % 2 == 1
+                     and spec.pad == spec.R // 2):
+        return False
+    return True
+
+
+def _pro_args(pro, spec):
+    """ProParams (csrc/igemm.h) from a dict: the PRODUCER's BN -- stats=[G][2][C] batch sums
+    (or rmean/rvar), gamma, beta, act, eps, count (= y pixels per stat group) -- and keep=
+    (optional activation output, [N*H*W][C])."""
+    for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta'):
+        _chk(pro.get(k), torch.float32, 'pro.' + k)
+    _chk(pro.get('keep'), torch.bfloat16, 'pro.keep', spec.N * spec.H * spec.W * spec.Cp)
+    if pro.get('stats') is None and pro.get('rmean') is None:
+        raise ValueError('pro needs stats or running statistics')
+    grp = spec.group_rows if spec.group_rows else spec.M
+    return (ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')), ptr(pro['gamma']),
+            ptr(pro['beta']), ptr(pro.get('keep')), grp, 1.0 / float(pro.get('count', 1)),
+            float(pro.get('eps', 1e-5)), _ACT[pro.get('act')], (spec.R // 2) * spec.S + spec.S // 2)
+
+
 def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=None,
-             accumulate=False, pipe=None):
-    """out[M][K] = conv(x NHWC, w [K][R][S][Cp]); optional BN-sum epilogue."""
+             accumulate=False, pipe=None, pro=None):
+    """out[M][K] = conv(x NHWC, w [K][R][S][Cp]); optional BN-sum epilogue.  ``pro``: x is the
+    producer's raw conv output and its BN + activation are applied while loading (see
+    ``pro_ok`` / ``_pro_args``)."""
     Cp = spec.Cp
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
     _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * Cp)
@@ -157,6 +195,14 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     if splits > 1:
         slab = _slab(slab, slab_bytes(spec.M, spec.K, bm, bn, splits), x.device)
     grp = spec.group_rows if spec.group_rows else spec.M
+    if pro is not None:
+        if accumulate or not pro_ok(spec, (bm, bn, splits, pipe), keep=pro.get('keep') is not None):
+            raise ValueError('BN-apply prologue not supported for this conv/plan')
+        lib().igemm_pro(ptr(x), ptr(w), ptr(out), spec.K, ptr(bias), ptr(stats), spec.K, grp,
+                        ptr(slab) if splits > 1 else 0, spec.H, spec.W, Cp, spec.P, spec.Q,
+                        spec.R, spec.S, spec.stride, spec.pad, spec.R * spec.S * Cp // 8, spec.K,
+                        spec.M, bm, bn, splits, stream_ptr(), *_pro_args(pro, spec))
+        return out
     lib().igemm(ptr(x), ptr(w), ptr(out), spec.K, ptr(bias), ptr(stats), spec.K, grp,
                 int(accumulate), ptr(slab) if splits > 1 else 0,
                 spec.H, spec.W, Cp, spec.P, spec.Q, spec.R, spec.S, spec.stride, spec.pad,

@@ -1,4 +1,6 @@
 """Multi-process CPU tests over gloo (SURVEY §4 layer 3)."""
+import tempfile
+
 import numpy as np
 import pytest
 import torch
@@ -74,7 +76,7 @@ def _trainer_dp(rank, ws):
     from test_importance import FakeLoader, TinyNet
     torch.manual_seed(rank)            # different init per rank: broadcast must fix it
     net = TinyNet()
-    cfg = Config(print_every=0, eval_every=0, bucket_mb=0.001)
+    cfg = Config(print_every=0, eval_every=0, bucket_mb=0.001, log_dir=tempfile.mkdtemp())
     opt = torch.optim.Adam(net.parameters(), lr=1e-3)
     loader = FakeLoader(n=6, seed=rank)   # non-IID: different shards
     t = Trainer(net, opt, FakeLoader(n=4), loader, None, 'cpu', cfg)
@@ -98,7 +100,8 @@ def _global_ema(rank, ws):
     from test_importance import FakeLoader, TinyNet
     torch.manual_seed(0)
     net = TinyNet()
-    cfg = Config(print_every=0, eval_every=0, global_ema=True, score='gradnorm')
+    cfg = Config(print_every=0, eval_every=0, global_ema=True, score='gradnorm',
+                 log_dir=tempfile.mkdtemp())
     t = Trainer(net, torch.optim.Adam(net.parameters(), lr=1e-3), FakeLoader(n=4),
                 FakeLoader(n=12, seed=rank), None, 'cpu', cfg)
     ema = EMAverage()
@@ -132,7 +135,8 @@ def _health(rank, ws):
     # the trainer checks every step and keeps training (replicas stay identical)
     torch.manual_seed(rank)
     net = TinyNet()
-    cfg = Config(print_every=0, eval_every=0, check_replicas_every=1)
+    cfg = Config(print_every=0, eval_every=0, check_replicas_every=1,
+                 log_dir=tempfile.mkdtemp())
     t = Trainer(net, torch.optim.Adam(net.parameters(), lr=1e-3), FakeLoader(n=3),
                 FakeLoader(n=6, seed=rank), None, 'cpu', cfg)
     t.fit(1)

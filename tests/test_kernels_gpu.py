@@ -665,3 +665,81 @@ def test_conv_pipelined_lds_dma(case, pipe):
             dx = torch.empty(N * H * W, spec.Cp, dtype=torch.bfloat16, device=DEV)
             ops.conv_dgrad(ops.to_nhwc(gy), wt, dx, spec, plan=plan, pipe=pipe)
             close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
+
+
+def conv_pro_direct(ops, x, wk, out, spec, slab, plan, pro):
+    """conv_fwd(pro=...) without the engine's pointwise-only policy (the kernel takes any
+    R x S; the policy is a speed choice)."""
+    from mercury_amd.ops import conv as cv
+    grp = spec.group_rows if spec.group_rows else spec.M
+    cv.lib().igemm_pro(cv.ptr(x), cv.ptr(wk), cv.ptr(out), spec.K, 0, 0, spec.K, grp,
+                       cv.ptr(slab) if plan[2] > 1 else 0, spec.H, spec.W, spec.Cp, spec.P, spec.Q,
+                       spec.R, spec.S, spec.stride, spec.pad, spec.R * spec.S * spec.Cp // 8,
+                       spec.K, spec.M, plan[0], plan[1], plan[2], cv.stream_ptr(),
+                       *cv._pro_args(pro, spec))
+
+
+@pytest.mark.parametrize('mode', ['train_keep', 'ghost', 'eval'])
+@pytest.mark.parametrize('case', [(8, 16, 16, 64, 64, 3, 3, 1, 1), (4, 8, 8, 128, 256, 1, 1, 1, 0),
+                                  (64, 4, 4, 64, 128, 3, 3, 2, 1)])
+def test_conv_fwd_bn_apply_prologue(case, mode):
+    """conv(act(bn(y))) with the BN-apply + ReLU done in the conv's operand load equals the
+    separate bn_apply pass followed by the plain conv, and an fp32 torch reference; in train
+    mode the kept activation equals bn_apply's output."""
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, pro_ok, slab_bytes
+    N, H, W, C, K, R, S, st, pd = case
+    if mode == 'train_keep' and st != 1:
+        pytest.skip('keep needs a stride-1 same conv')
+    g = torch.Generator(device='cpu').manual_seed(7)
+    yb = bf(torch.randn(N, C, H, W, generator=g) * 2 + 0.5).to(DEV)         # producer output
+    w = bf(torch.randn(K, C, R, S, generator=g) / math.sqrt(C * R * S)).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    yn = ops.to_nhwc(yb)
+    gimgs = N // 2 if mode == 'ghost' else 0     # two ghost groups
+    G = N // gimgs if gimgs else 1
+    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
+    if gimgs:
+        spec.group_rows = gimgs * spec.P * spec.Q
+    ycnt = (gimgs or N) * H * W
+    yg = yb.view(G, -1, C, H, W)
+    stats = torch.stack([yg.sum((1, 3, 4)), yg.pow(2).sum((1, 3, 4))], 1).contiguous()  # [G][2][C]
+    rmean = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    rvar = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    # reference activation (fp32 from the bf16 input), then bf16 as the kernels store it
+    if mode == 'eval':
+        mean = rmean.view(1, 1, C, 1, 1).expand(G, 1, C, 1, 1)
+        var = rvar.view(1, 1, C, 1, 1).expand(G, 1, C, 1, 1)
+    else:
+        mean = (stats[:, 0] / ycnt).view(G, 1, C, 1, 1)
+        var = (stats[:, 1] / ycnt).view(G, 1, C, 1, 1) - mean ** 2
+    a = torch.relu((yg - mean) / torch.sqrt(var + 1e-5) * gamma.view(1, 1, C, 1, 1)
+                   + beta.view(1, 1, C, 1, 1)).view(N, C, H, W)
+    ref = F.conv2d(bf(a), w, stride=st, padding=pd)
+    plan = fwd_plan(spec)
+    if R == 1:
+        assert pro_ok(spec, plan, keep=mode == 'train_keep')
+    wk, _ = ops.pack_conv_weight(w)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, K, *plan[:3]) // 4), device=DEV)
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    keep = torch.full_like(yn, float('nan')) if mode == 'train_keep' else None
+    pro = dict(gamma=gamma, beta=beta, act='relu', eps=1e-5, keep=keep)
+    if mode == 'eval':
+        pro.update(rmean=rmean, rvar=rvar)
+    else:
+        pro.update(stats=stats.reshape(-1), count=ycnt)
+    conv_pro_direct(ops, yn, wk, out, spec, slab, plan, pro)
+    got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2)
+    close(got, ref)
+    # unfused path: bn_apply pass, then the plain conv
+    an = torch.empty_like(yn)
+    ops.bn_apply(yn, None if mode == 'eval' else stats.reshape(-1), gamma, beta, an, N * H * W, C,
+                 group_rows=gimgs * H * W, act='relu',
+                 running=(rmean, rvar) if mode == 'eval' else None)
+    out2 = torch.empty_like(out)
+    ops.conv_fwd(an, wk, out2, spec, slab=slab, plan=plan)
+    close(out, out2, rtol=1e-2, atol=1e-2)
+    if keep is not None:
+        assert not torch.isnan(keep.float()).any()
+        close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
