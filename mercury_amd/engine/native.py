@@ -667,6 +667,9 @@ class NativeEngine(object):
             return
         ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label, sm.index,
                        self.P, self.B, self.seed, zero=sm.stats_arena)
+        # (the scoring convs keep their full occupancy: reserving extra LDS per scoring block
+        # so train blocks fit beside them measured 1.70-2.21 ms/step vs 1.65 -- in the
+        # concurrent step the GPU is throughput-bound, bench/ab_env.sh)
         x = self.forward(sm)
         self.head(sm, x, 'score')
         if self.table is not None:
