@@ -55,7 +55,7 @@ def main():
 
             def train():
                 e['tr0'].record(s0)
-                for g, _ in G['train']:
+                for g, _, _ in G['train']:
                     g.replay()
                 e['tr1'].record(s0)
             if order == 'score_first':

@@ -273,9 +273,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("optimizer", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t segs,
                         int nsegs, long long total, uintptr_t hyper, uintptr_t step, int algo,
-                        int zero_grad, uintptr_t st) {
+                        int zero_grad, uintptr_t st, long long start) {
     OptArgs a{P<float>(p), P<float>(g), P<float>(mm), P<float>(v), P<const OptSeg>(segs), nsegs,
-              total, P<const float>(hyper), P<const int64_t>(step), algo, zero_grad};
+              total, P<const float>(hyper), P<const int64_t>(step), algo, zero_grad, start};
     optimizer_launch(a, S(st));
     check_launch("optimizer");
   });

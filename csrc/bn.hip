@@ -88,6 +88,22 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
   const int c8 = i0 % C8, c = c8 * 8;
   const int g = blockIdx.y;
   const int row0 = g * a.group_rows, row1 = min(a.M, row0 + a.group_rows);
+  const int rpi = stride / C8;
+  // U rows per trip with every load issued before the first use (clamped rows, unconditional
+  // loads); the first trip's rows are requested BEFORE the per-channel constants, so a small
+  // launch pays one memory latency up front instead of two
+  constexpr int U = 4;
+  bf16x8 y[U], r[U];
+  auto load = [&](int rb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = (size_t)min(rb + u * rpi, row1 - 1) * a.C + c;
+      y[u] = *(const bf16x8*)(a.y + off);
+      if (a.res_mode) r[u] = *(const bf16x8*)(a.res + off);
+    }
+  };
+  int row = row0 + i0 / C8;
+  if (row < row1) load(row);
   const float inv = 1.f / (float)(row1 - row0);
   const bool run = a.use_running != 0;
   float sc[8], sh[8], sc2[8], sh2[8];
@@ -101,21 +117,21 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
     const float* s1 = run ? a.rvar2 + c : s0 + a.C;
     scale_shift8(s0, s1, run, inv, a.eps, a.gamma2 + c, a.beta2 + c, sc2, sh2);
   }
-  const int rpi = stride / C8;
-  for (int row = row0 + i0 / C8; row < row1; row += rpi) {
-    const size_t off = (size_t)row * a.C + c;
-    const bf16x8 y = *(const bf16x8*)(a.y + off);
-    bf16x8 r;
-    if (a.res_mode) r = *(const bf16x8*)(a.res + off);
-    bf16x8 o;
+  for (; row < row1; row += U * rpi) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float v = bf2f(y[k]) * sc[k] + sh[k];
-      if (a.res_mode == 1) v += bf2f(r[k]);
-      else if (a.res_mode == 2) v += bf2f(r[k]) * sc2[k] + sh2[k];
-      o[k] = f2bf(act_fwd(v, a.act));
+    for (int u = 0; u < U; ++u) {
+      if (row + u * rpi >= row1) break;
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = bf2f(y[u][k]) * sc[k] + sh[k];
+        if (a.res_mode == 1) v += bf2f(r[u][k]);
+        else if (a.res_mode == 2) v += bf2f(r[u][k]) * sc2[k] + sh2[k];
+        o[k] = f2bf(act_fwd(v, a.act));
+      }
+      *(bf16x8*)(a.out + (size_t)(row + u * rpi) * a.C + c) = o;
     }
-    *(bf16x8*)(a.out + off) = o;
+    if (row + U * rpi < row1) load(row + U * rpi);
   }
 }
 
@@ -198,6 +214,19 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const int i0 = blockIdx.x * NT + threadIdx.x;
   if (i0 >= stride) return;
   const int c8 = i0 % C8, c = c8 * 8;
+  const int rpi = stride / C8;
+  // the next row's tensors are requested before this row's math (and the first row's before
+  // the per-channel constants): one exposed memory latency per launch, not per row
+  bf16x8 d, o, y, y2;
+  auto load = [&](int rw) {
+    const size_t off = (size_t)rw * a.C + c;
+    d = *(const bf16x8*)(a.dout + off);
+    o = *(const bf16x8*)(a.out + off);
+    y = *(const bf16x8*)(a.y + off);
+    if (two) y2 = *(const bf16x8*)(a.y2 + off);
+  };
+  int row = i0 / C8;
+  if (row < a.M) load(row);
   float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
   mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
   load8(a.gamma + c, gm);
@@ -219,21 +248,18 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
       q2[k] = sx2[k] * inv;
     }
   }
-  const int rpi = stride / C8;
-  for (int row = i0 / C8; row < a.M; row += rpi) {
+  for (; row < a.M; row += rpi) {
+    const bf16x8 dc = d, oc = o, yc = y, y2c = y2;
+    if (row + rpi < a.M) load(row + rpi);
     const size_t off = (size_t)row * a.C + c;
-    const bf16x8 d = *(const bf16x8*)(a.dout + off);
-    const bf16x8 o = *(const bf16x8*)(a.out + off);
-    const bf16x8 y = *(const bf16x8*)(a.y + off);
-    bf16x8 y2, dy, dy2, dzo;
-    if (two) y2 = *(const bf16x8*)(a.y2 + off);
+    bf16x8 dy, dy2, dzo;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float dz = bf2f(d[k]) * act_mask(bf2f(o[k]), a.act);
-      const float xh = (bf2f(y[k]) - mean[k]) * rstd[k];
+      const float dz = bf2f(dc[k]) * act_mask(bf2f(oc[k]), a.act);
+      const float xh = (bf2f(yc[k]) - mean[k]) * rstd[k];
       dy[k] = f2bf(k1[k] * (dz - k2[k] - xh * q1[k]));
       if (two) {
-        const float xh2 = (bf2f(y2[k]) - mean2[k]) * rstd2[k];
+        const float xh2 = (bf2f(y2c[k]) - mean2[k]) * rstd2[k];
         dy2[k] = f2bf(k3[k] * (dz - k2[k] - xh2 * q2[k]));
       }
       dzo[k] = f2bf(dz);

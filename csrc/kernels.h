@@ -188,11 +188,12 @@ struct OptArgs {
   float* v;
   const OptSeg* segs;
   int nsegs;
-  long long total;               // padded flat length
+  long long total;               // end of the swept range (padded flat length for a full step)
   const float* hyper;            // device: [0] lr [1] beta1 [2] beta2 [3] eps [4] wd
   const int64_t* step;           // device step counter (t, already incremented)
   int algo;                      // 0 adam, 1 sgd(momentum)
   int zero_grad;
+  long long start;               // first element of the swept range (4-aligned segment start)
 };
 void optimizer_launch(const OptArgs& a, hipStream_t st);
 void step_begin_launch(int64_t* ctrl, float* z0, int n0, float* z1, int n1, hipStream_t st);

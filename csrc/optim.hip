@@ -1,7 +1,8 @@
 // Fused flat-buffer optimizer.
 //
-// One launch sweeps the whole flat fp32 parameter buffer (11.17M elements for
-// ResNet-18): Adam (torch.optim.Adam semantics, bias-corrected, L2 weight decay
+// One launch sweeps the flat fp32 parameter buffer (11.17M elements for ResNet-18), or a
+// [start, end) range of whole segments when the step is split (the engine updates the last
+// blocks' parameters while earlier blocks are still in backward): Adam (torch.optim.Adam semantics, bias-corrected, L2 weight decay
 // folded into the gradient) or SGD with momentum, then -- in the same pass --
 // writes the bf16 operand copies the MFMA kernels consume:
 //   conv weight (master layout [K][R][S][C]) -> [K][R][S][Cpad] bf16 (fwd/wgrad B)
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void transpose_weights_kernel(const OptSeg* se
 
 __global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
   const long long i4 = (long long)blockIdx.x * NT + threadIdx.x;
-  const long long e = i4 * 4;
+  const long long e = a.start + i4 * 4;
   if (e >= a.total) return;
   const int si = find_seg(a.segs, a.nsegs, e);
   const OptSeg sg = a.segs[si];
@@ -145,7 +146,8 @@ __global__ __launch_bounds__(256) void step_begin_kernel(int64_t* ctrl, float* z
 }  // namespace
 
 void optimizer_launch(const OptArgs& a, hipStream_t st) {
-  const long long n4 = (a.total + 3) / 4;
+  if (a.total <= a.start) return;
+  const long long n4 = (a.total - a.start + 3) / 4;
   hipLaunchKernelGGL(optimizer_kernel, dim3((unsigned)((n4 + NT - 1) / NT)), dim3(NT), 0, st, a);
 }
 

@@ -116,6 +116,11 @@ class NativeEngine(object):
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
         self.roctx = False               # per-phase roctx ranges around the step's host calls
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
+        # the last blocks' optimizer update on the scoring stream during the earlier blocks'
+        # backward (see _early_block).  Off by default: measured neutral on MI355X (ResNet-18
+        # 1.660 vs 1.655 ms/step) -- in the overlapped step the GPU is throughput-bound, so
+        # moving the update off the tail only moves its HBM traffic under the backward
+        self.early_opt = os.environ.get('MERCURY_EARLY_OPT', '0') == '1'
         # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
         self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
         self.sampler = sampler
@@ -242,7 +247,13 @@ class NativeEngine(object):
                 m.spec[u.name] = sp
                 if not u.depthwise:
                     # measured-best plans from the tuning cache (ops/tune.py) when present
-                    m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(sp, fwd_plan(sp))
+                    # the scoring pass runs beside the latency-bound train chain: fewer, larger
+                    # tiles leave the train kernels more room (measured, ResNet-18: 128-block
+                    # target 1.656 vs 256-block 1.667 ms/step; split-K or 512 blocks slower)
+                    mb = int(os.environ.get('MERCURY_SCORE_MIN_BLOCKS', '128')) \
+                        if group_imgs else 0
+                    m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(
+                        sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
                     if train:
                         if u.need_dgrad and sp.K % 8 == 0:
@@ -734,35 +745,69 @@ class NativeEngine(object):
                 torch.cuda.current_stream().wait_stream(self.s_wgrad)
 
         cuts = self.bucket_plan()
+        sb = self._early_block()
         cur = [fwd_head]
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
             cur.append(lambda bi=bi: self.backward_block(tm, bi))
-            if bi in cuts:
-                segs.append((cur + [join_wgrad], cuts[bi]))
+            if bi in cuts or bi == sb:
+                segs.append((cur + [join_wgrad], cuts.get(bi), bi == sb))
                 cur = []
         if cur:
-            segs.append((cur + [join_wgrad], None))
+            segs.append((cur + [join_wgrad], None, False))
         return segs
 
-    def bucket_plan(self):
-        """{block index: (flat_start, flat_end)} -- a bucket closes after that block's backward."""
-        if self.world_size == 1:
-            return {}
+    def _block_starts(self):
         starts = []
         for bi, blk in enumerate(self.lw.blocks):
             us = blk.units + ([blk.shortcut] if blk.shortcut else [])
             starts.append(min(min(s.off for s in (u.w_seg, u.g_seg, u.beta_seg)) for u in us))
+        return starts
+
+    def _early_block(self):
+        """First block of the parameter suffix the early optimizer updates (None: off).
+
+        The last blocks hold most of the parameters (ResNet-18: layer4 + fc = 75 %) and finish
+        their backward first.  Once they have (and the scoring forward, which reads every
+        weight, is done), their Adam update and bf16/transposed weight copies run on the
+        scoring stream while the train stream is still in the earlier blocks' backward, so the
+        step's tail only updates the remaining prefix."""
+        if not self.early_opt or len(self.lw.blocks) < 2:
+            return None
+        starts = self._block_starts()
+        total = self.lw.total
+        for bi in range(len(self.lw.blocks) - 1, 0, -1):
+            if (total - starts[bi]) * 2 >= total:
+                return bi
+        return None
+
+    @property
+    def _early_start(self):
+        sb = self._early_block()
+        return None if sb is None else self._block_starts()[sb]
+
+    def bucket_plan(self):
+        """{block index: (flat_start, flat_end)} -- a bucket closes after that block's backward
+        (always at the early optimizer's block, so its parameters' buckets end there)."""
+        if self.world_size == 1:
+            return {}
+        starts = self._block_starts()
+        sb = self._early_block()
         cuts = {}
         end = self.lw.total
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
-            if bi == 0 or (end - starts[bi]) * 4 >= self.bucket_bytes:
+            if bi == 0 or bi == sb or (end - starts[bi]) * 4 >= self.bucket_bytes:
                 cuts[bi] = (0 if bi == 0 else starts[bi], end)
                 end = starts[bi]
         return cuts
 
+    def early_tail(self):
+        """Score-stream part of the optimizer step: the parameter suffix (``_early_block``)."""
+        self.opt.step(self.ctrl[2:3], start=self._early_start)
+
     def tail(self):
         (self.bn_table if self.scoring else self.bn_table_uniform).launch(0.1)
-        self.opt.step(self.ctrl[2:3])
+        es = self._early_start
+        self.opt.step(self.ctrl[2:3], end=es)     # es None: the whole buffer
         self._mlp_refresh()
         self.gather_batch()
 
@@ -780,9 +825,12 @@ class NativeEngine(object):
         self.graphs = {
             'score': self._capture(self.score_forward if self._split_score else self.score_branch,
                                    cap),
-            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b) for fs, b in segs],
+            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b, e)
+                      for fs, b, e in segs],
             'tail': self._capture(self.tail, cap),
         }
+        if self._early_start is not None:
+            self.graphs['early'] = self._capture(self.early_tail, cap)
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
         self._graph_scoring = self.scoring
@@ -824,11 +872,10 @@ class NativeEngine(object):
         if rx:
             prof.pop()
             prof.push('train')
-        ev_score = torch.cuda.Event()
-        ev_score.record(self.s_score)
         works = []
         segs = graphs['train'] if graphs else self.train_segments()
-        for g, bucket in segs:
+        early = False
+        for g, bucket, cut in segs:
             if graphs:
                 g.replay()
             else:
@@ -836,15 +883,31 @@ class NativeEngine(object):
                     f()
             if bucket is not None and self.world_size > 1:
                 s, e = bucket
-                works.append((dist.all_reduce(self.opt.g[s:e], op=self._avg_op,
-                                              async_op=True), s, e))
+                works.append([dist.all_reduce(self.opt.g[s:e], op=self._avg_op,
+                                              async_op=True), s, e, False])
+            if cut:
+                # the parameter suffix is final on this rank once its buckets are reduced:
+                # update it on the scoring stream, behind the scoring forward that reads it
+                early = True
+                ev_bwd = torch.cuda.Event()
+                ev_bwd.record(s0)
+                with torch.cuda.stream(self.s_score):
+                    self.s_score.wait_event(ev_bwd)
+                    for wk in works:
+                        self._finish_work(wk)
+                    if graphs:
+                        graphs['early'].replay()
+                    else:
+                        self.early_tail()
+        ev_score = torch.cuda.Event()
+        ev_score.record(self.s_score)
         if rx:
             prof.pop()
             prof.push('allreduce')
-        for w, s, e in works:
-            w.wait()
-            if self._avg_op != dist.ReduceOp.AVG:   # gloo has no AVG
-                self.opt.g[s:e].mul_(1.0 / self.world_size)
+        for wk in works:
+            self._finish_work(wk)
+        if not early and self._early_start is not None:
+            raise RuntimeError('early optimizer cut not reached')
         s0.wait_event(ev_score)
         if rx:
             prof.pop()
@@ -855,6 +918,15 @@ class NativeEngine(object):
             self.tail()
         if rx:
             prof.pop()
+
+    def _finish_work(self, wk):
+        """Make the current stream wait for a bucket all-reduce (once per stream is harmless;
+        the gloo SUM -> mean scaling runs once)."""
+        w, s, e, done = wk
+        w.wait()
+        if not done and self._avg_op != dist.ReduceOp.AVG:   # gloo has no AVG
+            self.opt.g[s:e].mul_(1.0 / self.world_size)
+        wk[3] = True
 
     # ------------------------------------------------------------------ misc API
     def reset_ema(self):

@@ -94,9 +94,9 @@ def slab_bytes(M, Ncols, bm, bn, splits):
     return SEM_BYTES + splits * math.ceil(M / bm) * math.ceil(Ncols / bn) * bm * bn * 4
 
 
-def fwd_plan(spec: ConvSpec):
+def fwd_plan(spec: ConvSpec, min_blocks=CU):
     kchunks = spec.R * spec.S * spec.Cp // 8
-    return pick_tiles(spec.M, spec.K, kchunks, spec.group_rows)
+    return pick_tiles(spec.M, spec.K, kchunks, spec.group_rows, min_blocks=min_blocks)
 
 
 def dgrad_plan(spec: ConvSpec):

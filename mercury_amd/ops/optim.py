@@ -34,6 +34,7 @@ class FlatOptimizer(object):
             rows.append([s['off'], s['numel'], s['kind'], s.get('K', 0), s.get('R', 1),
                          s.get('S', 1), s.get('C', 1), s.get('Cpad', 1),
                          ptr(s.get('w_krsc')), ptr(s.get('w_crsk'))])
+        self._seg_starts = set(int(s['off']) for s in segments)
         packed = lib().pack_opt_segs(rows)
         self.segbuf = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(device)
         self.nsegs = len(rows)
@@ -46,12 +47,18 @@ class FlatOptimizer(object):
                         for c0 in range(0, s['C'], 64):
                             jobs.append((i, rs, k0, c0))
         self.njobs = len(jobs)
+        # jobs are ordered by segment, hence by flat offset: a range's jobs are a slice
+        self._job_off = [segments[j[0]]['off'] for j in jobs]
         self.jobs = torch.tensor(jobs if jobs else [(0, 0, 0, 0)], dtype=torch.int32,
                                  device=device).contiguous()
 
-    def _transpose(self):
-        if self.njobs:
-            lib().transpose_weights(ptr(self.segbuf), ptr(self.jobs), self.njobs, stream_ptr())
+    def _transpose(self, start=0, end=None):
+        end = self.total if end is None else end
+        j0 = next((i for i, o in enumerate(self._job_off) if o >= start), self.njobs)
+        j1 = next((i for i, o in enumerate(self._job_off) if o >= end), self.njobs)
+        if j1 > j0:
+            lib().transpose_weights(ptr(self.segbuf), ptr(self.jobs) + 16 * j0, j1 - j0,
+                                    stream_ptr())
 
     @property
     def lr(self):
@@ -60,12 +67,18 @@ class FlatOptimizer(object):
     def set_lr(self, lr):
         self.hyper[0].fill_(float(lr))
 
-    def step(self, step_counter, zero_grad=True):
-        """``step_counter``: device int64 scalar tensor/view holding t (already incremented)."""
+    def step(self, step_counter, zero_grad=True, start=0, end=None):
+        """``step_counter``: device int64 scalar tensor/view holding t (already incremented).
+        ``start``/``end``: update only the flat range [start, end) -- both must be segment
+        starts (or ``total``); two range steps equal one full step."""
+        end = self.total if end is None else end
+        for b in (start, end):
+            if b != self.total and b not in self._seg_starts:
+                raise ValueError('optimizer range bound %d is not a segment start' % b)
         lib().optimizer(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), ptr(self.segbuf),
-                        self.nsegs, self.total, ptr(self.hyper), ptr(step_counter), self.algo,
-                        int(zero_grad), stream_ptr())
-        self._transpose()
+                        self.nsegs, end, ptr(self.hyper), ptr(step_counter), self.algo,
+                        int(zero_grad), stream_ptr(), start)
+        self._transpose(start, end)
 
     def pack_weights(self):
         """Write the bf16 conv-weight copies from the fp32 master (after init / load)."""

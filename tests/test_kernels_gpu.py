@@ -552,12 +552,19 @@ def test_fused_adam_matches_torch_and_writes_bf16_copies():
         opt.g[:conv.numel()] = g1.permute(0, 2, 3, 1).reshape(-1)
         opt.g[off2:off2 + 10] = g2
         step += 1
-        opt.step(step)
+        if t % 2:
+            opt.step(step)
+        else:   # split step (the engine's early optimizer): suffix first, then the prefix
+            opt.step(step, start=off2)
+            assert opt.g[:conv.numel()].abs().max().item() > 0   # prefix untouched so far
+            opt.step(step, end=off2)
         assert opt.g.abs().max().item() == 0  # gradient consumed and zeroed
     close(opt.p[:conv.numel()].view(k, r, s, c).permute(0, 3, 1, 2), ref[0].detach(), 1e-5, 1e-6)
     close(opt.p[off2:off2 + 10], ref[1].detach(), 1e-5, 1e-6)
     close(krsc.float(), ref[0].detach().permute(0, 2, 3, 1), 1e-2, 1e-3)
     close(crsk.float(), ref[0].detach().permute(1, 2, 3, 0), 1e-2, 1e-3)
+    with pytest.raises(ValueError):
+        opt.step(step, start=3)          # not a segment start
 
 
 def test_quantize_pool_dwconv():
