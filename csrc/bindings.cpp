@@ -13,6 +13,7 @@
 
 #include "kernels.h"
 
+int igemm_read_stamps(unsigned long long* host, int n);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
@@ -115,6 +116,11 @@ PYBIND11_MODULE(_C, m) {
     std::vector<uint32_t> mask((size_t)words, 0u);
     (void)hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(st), (uint32_t)words, mask.data());
     return mask;
+  });
+  m.def("igemm_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
+    std::vector<unsigned long long> v((size_t)n * 4, 0ull);
+    if (!igemm_read_stamps(v.data(), n)) v.clear();
+    return v;
   });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};

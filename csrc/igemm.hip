@@ -48,6 +48,22 @@ __device__ __attribute__((aligned(16))) bf16 g_zero_page[64];
 
 MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
+#ifdef MERCURY_STAMPS
+// Diagnostic build only (-DMERCURY_STAMPS): per-block s_memtime at the phase boundaries of the
+// register-staged body -- entry, first stage staged, main loop done, epilogue done -- written
+// by thread 0 into a buffer no other code reads (bench/stamp_conv.py).
+__device__ unsigned long long g_stamps[8192][4];
+#define MA_STAMP(i)                                                                         \
+  do {                                                                                      \
+    if (threadIdx.x == 0) {                                                                 \
+      const int b_ = blockIdx.x + blockIdx.y * gridDim.x;                                   \
+      if (b_ < 8192) g_stamps[b_][i] = __builtin_amdgcn_s_memtime();                       \
+    }                                                                                       \
+  } while (0)
+#else
+#define MA_STAMP(i) (void)0
+#endif
+
 template <int BM, int BN>
 struct Smem {
   static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
@@ -457,6 +473,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   const int ntn = (g.Ncols + BN - 1) / BN;
   const int mt = bx / ntn, nt = bx - mt * ntn;
   const int m0 = mt * BM, n0 = nt * BN;
+  MA_STAMP(0);
   const int ktiles = (g.Kc + 7) / 8;
   const int kt0 = by * ktiles_per_split;
   const int kt1 = min(ktiles, kt0 + ktiles_per_split);
@@ -580,6 +597,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     load_stage(kt0);
     store_stage(0);
     __syncthreads();
+    MA_STAMP(1);
     int buf = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
@@ -591,7 +609,9 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       buf ^= 1;
     }
   }
+  MA_STAMP(2);
   finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, bx, by, gx, gy);
+  MA_STAMP(3);
 }
 
 template <int BM, int BN, bool TRANS>
@@ -786,6 +806,17 @@ void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, in
 }
 
 }  // namespace
+
+int igemm_read_stamps(unsigned long long* host, int n) {
+#ifdef MERCURY_STAMPS
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * n) ==
+         hipSuccess;
+#else
+  (void)host;
+  (void)n;
+  return 0;
+#endif
+}
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   const size_t mtiles = (g.M + bm - 1) / bm, ntiles = (g.Ncols + bn - 1) / bn;
