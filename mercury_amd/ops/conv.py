@@ -155,6 +155,12 @@ def pro_ok(spec: ConvSpec, plan, keep=False):
     # (bench/pro_bench.py, MI355X: B=320 64->64 3x3 135 us vs 53 + 20 us)
     if spec.R != 1 or spec.S != 1:
         return False
+    # every N-tile of the consumer redoes the normalisation of its A rows: worth it for one
+    # tile, or a few at train-batch sizes (MobileNetV2 4.33 -> 4.26 ms/step), not for the wide
+    # ResNet-50 expansions at large batch (53.6 -> 55.4 ms/step with every 1x1 fused)
+    ntn = -(-spec.K // plan[1])
+    if ntn > 1 and (ntn > 4 or spec.M > 32768):
+        return False
     if spec.group_rows and spec.group_rows < spec.M and spec.group_rows % bm:
         return False
     if keep and not (spec.stride == 1 and spec.R == spec.S and spec.R % 2 == 1
