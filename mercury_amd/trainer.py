@@ -141,6 +141,14 @@ class Trainer(object):
 
         Returns ``(weights = N*p[idx], data[idx], label[idx], index[idx], pool_mean)``."""
         alpha = self.cfg.alpha if alpha is None else alpha
+        if not self.cfg.importance and self.score_exchange is None:
+            # uniform-sampling baseline (the native engine's too): the next loader batch with
+            # unit weights -- no presample pool is scored
+            idx, data, label = self.get_next()
+            data = data.to(self.device, non_blocking=True)
+            label = torch.as_tensor(label).to(self.device, non_blocking=True)
+            return (torch.ones(data.shape[0], device=self.device), data, label,
+                    torch.as_tensor(idx), torch.zeros((), device=self.device))
         losses, labels, datas, index = [], [], [], []
         cnt = 0
         with torch.no_grad():
