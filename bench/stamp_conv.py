@@ -35,7 +35,7 @@ def main():
     ops.conv_fwd(x, wk, y, sp, stats=stats, slab=slab, plan=plan)
     torch.cuda.synchronize()
     nb = (sp.M + plan[0] - 1) // plan[0] * ((K + plan[1] - 1) // plan[1]) * plan[2]
-    v = np.array(ops.lib().igemm_stamps(min(nb, 8192)), dtype=np.int64).reshape(-1, 4)
+    v = np.array(ops.lib().igemm_stamps(min(nb, 8192)), dtype=np.int64).reshape(-1, 8)
     if v.size == 0:
         print('not a stamps build')
         return
@@ -46,6 +46,8 @@ def main():
     print('  prologue  med/p90 %s' % f(pro))
     print('  mainloop  med/p90 %s' % f(loop))
     print('  epilogue  med/p90 %s' % f(epi))
+    print('  main-loop split (median cycles summed over stages): load-issue %d  mfma %d  '
+          'store(+load wait) %d  barrier %d' % tuple(np.median(v[:, 4 + q]) for q in range(4)))
     print('  block start spread med/p90/max %d %d %d, kernel span %d' % (
         np.median(t0), np.percentile(t0, 90), t0.max(), v[:, 3].max() - v[:, 0].min()))
 

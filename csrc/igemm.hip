@@ -52,7 +52,7 @@ MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 // Diagnostic build only (-DMERCURY_STAMPS): per-block s_memtime at the phase boundaries of the
 // register-staged body -- entry, first stage staged, main loop done, epilogue done -- written
 // by thread 0 into a buffer no other code reads (bench/stamp_conv.py).
-__device__ unsigned long long g_stamps[8192][4];
+__device__ unsigned long long g_stamps[8192][8];
 #define MA_STAMP(i)                                                                         \
   do {                                                                                      \
     if (threadIdx.x == 0) {                                                                 \
@@ -60,8 +60,17 @@ __device__ unsigned long long g_stamps[8192][4];
       if (b_ < 8192) g_stamps[b_][i] = __builtin_amdgcn_s_memtime();                       \
     }                                                                                       \
   } while (0)
+// per-phase cycle sums over the main loop (thread 0): [4] load issue, [5] MFMA phase,
+// [6] stage store (incl. the wait for its loads), [7] barrier
+#define MA_LAP(slot, t)                                                                     \
+  do {                                                                                      \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                            \
+    lap[slot] += n_ - t;                                                                    \
+    t = n_;                                                                                 \
+  } while (0)
 #else
 #define MA_STAMP(i) (void)0
+#define MA_LAP(slot, t) (void)0
 #endif
 
 template <int BM, int BN>
@@ -318,6 +327,33 @@ MA_DEV int row_at(const ConvGeom& g, int off, int h, int w, int r, int s, int c8
   return ok ? o : -1;
 }
 
+// Register-staged loop addressing (see igemm_nt_body): element offset of the row's source
+// pixel at tap (0, 0), the uniform offset of tap (r, s) from it, and the tap's bounds test.
+// forward: +(r*SW + s); dgrad stride 1: -(r*SW + s); dgrad stride 2: -((r>>1)*SW + (s>>1)),
+// valid only when the row's parity matches the tap's (then (h - r) >> 1 == (h >> 1) - (r >> 1)).
+template <bool TRANS>
+MA_DEV int row_base(const ConvGeom& g, int off, int h, int w) {
+  if (TRANS && g.stride == 2) return (off + (h >> 1) * g.SW + (w >> 1)) * g.SC;
+  return (off + h * g.SW + w) * g.SC;
+}
+
+template <bool TRANS>
+MA_DEV int tap_offset(const ConvGeom& g, int r, int s) {
+  if (!TRANS) return (r * g.SW + s) * g.SC;
+  if (g.stride == 2) return -((r >> 1) * g.SW + (s >> 1)) * g.SC;
+  return -(r * g.SW + s) * g.SC;
+}
+
+template <bool TRANS>
+MA_DEV bool tap_ok(const ConvGeom& g, int h, int w, int r, int s) {
+  if (!TRANS) return (unsigned)(h + r) < (unsigned)g.SH && (unsigned)(w + s) < (unsigned)g.SW;
+  const int hp = h - r, wp = w - s;
+  if (g.stride == 2)   // kernel-uniform: scalar branch
+    return ((hp | wp) & 1) == 0 && (unsigned)(hp >> 1) < (unsigned)g.SH &&
+           (unsigned)(wp >> 1) < (unsigned)g.SW;
+  return (unsigned)hp < (unsigned)g.SH && (unsigned)wp < (unsigned)g.SW;
+}
+
 // k-chunk -> (r, s, c8) cursor.  When C/8 is a multiple of 8 a 64-deep stage lies in one
 // filter tap, so the tap advances incrementally (no division in the loop).  Otherwise the
 // stage base is decoded once (uniform) and each lane steps its <= 7 extra chunks forward;
@@ -480,9 +516,18 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   const int Kelems = g.Kc * 8;
   const int cc = tid & 7;
 
-  int aoff[AR], ah[AR], aw[AR];
+  // A rows: the source offset of tap (0, 0) is computed once per row (abase), so a stage's
+  // gather is  abase + uniform tap offset  plus two bounds tests -- no per-row multiplies
+  // (stamps: the per-row multiply-heavy row_at was ~45 % of each stage's cycles).  A row
+  // past M gets an out-of-range h, so its bounds test always fails.
+  int abase[AR], ah[AR], aw[AR];
 #pragma unroll
-  for (int i = 0; i < AR; ++i) row_init<TRANS>(g, m0 + (tid >> 3) + 32 * i, aoff[i], ah[i], aw[i]);
+  for (int i = 0; i < AR; ++i) {
+    int off;
+    row_init<TRANS>(g, m0 + (tid >> 3) + 32 * i, off, ah[i], aw[i]);
+    abase[i] = row_base<TRANS>(g, off, ah[i], aw[i]);
+    if (off < 0) ah[i] = -(1 << 28);
+  }
   int boff[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
@@ -524,14 +569,15 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       keep = pro.keep != nullptr && nt == 0 && kval && r * g.S + s == pro.keep_tap;
       pz = 0;
     }
+    const int toff = tap_offset<TRANS>(g, r, s) + c8 * 8;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      int o = row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8);
-      o = kval ? o : -1;                       // select, not a branch around the gather
-      ra[i] = *(const u32x4*)(o >= 0 ? src + o : zp);
+      const bool ok = kval && tap_ok<TRANS>(g, ah[i], aw[i], r, s);
+      const int o = abase[i] + toff;
+      ra[i] = *(const u32x4*)(ok ? src + o : zp);   // select, not a branch around the gather
       if constexpr (PRO) {
-        pz |= (o < 0 ? 1 : 0) << i;
-        pko[i] = keep ? o : -1;
+        pz |= (ok ? 0 : 1) << i;
+        pko[i] = keep && ok ? o : -1;
       }
     }
 #pragma unroll
@@ -598,16 +644,31 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     store_stage(0);
     __syncthreads();
     MA_STAMP(1);
+#ifdef MERCURY_STAMPS
+    unsigned long long lap[4] = {0, 0, 0, 0};
+    unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
     int buf = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) load_stage(kt + 1);
+      MA_LAP(0, tl);
       const bf16* a = sA + buf * Smem<BM, BN>::STAGE;
       mma_stage<BM, BN>(a, a + BM * BK, acc, lane, wm, wn);
+      MA_LAP(1, tl);
       if (more) store_stage(buf ^ 1);
+      MA_LAP(2, tl);
       __syncthreads();
+      MA_LAP(3, tl);
       buf ^= 1;
     }
+#ifdef MERCURY_STAMPS
+    if (threadIdx.x == 0) {
+      const int b_ = blockIdx.x + blockIdx.y * gridDim.x;
+      if (b_ < 8192)
+        for (int q = 0; q < 4; ++q) g_stamps[b_][4 + q] = lap[q];
+    }
+#endif
   }
   MA_STAMP(2);
   finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, bx, by, gx, gy);
@@ -809,7 +870,7 @@ void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, in
 
 int igemm_read_stamps(unsigned long long* host, int n) {
 #ifdef MERCURY_STAMPS
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * n) ==
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n) ==
          hipSuccess;
 #else
   (void)host;
