@@ -122,6 +122,7 @@ PYBIND11_MODULE(_C, m) {
     if (!igemm_read_stamps(v.data(), n)) v.clear();
     return v;
   });
+  m.def("igemm_set_halo", &igemm_set_halo);
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};
     g.M = M;

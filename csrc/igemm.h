@@ -65,6 +65,8 @@ struct ProParams {
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
+// halo-tile 3x3 forward on/off for subsequent launches (default: MERCURY_HALO env, off)
+void igemm_set_halo(int on);
 // pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages.
 // pro != null: BN-apply prologue (forward, pipe 0 only).
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,

@@ -490,6 +490,214 @@ MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& 
   epilogue<BM, BN>(acc, smem, e, M, N, m0, n0);
 }
 
+// ---------------------------------------------------------------- halo-tile 3x3 forward
+// Stride-1 3x3 "same" conv with C % 64 == 0 (the ResNet 3x3 body convs).  The generic loop
+// re-gathers every input pixel once per tap, so each 64-deep stage moves (BM + BN) x 128 B
+// through the CU's vector-memory path; in-kernel stamps put about half of a stage in load
+// issue.  Here a block's output rows are whole image rows (TR rows of one image, or IMG
+// whole images), so the input it needs for one 64-channel chunk is a (TR+2) x (Q+2) halo
+// tile: loaded ONCE into LDS and read by all 9 taps.  A stage (one tap of one channel chunk)
+// then only streams its BN x 64 weight tile; the next chunk's halo is prefetched into
+// registers from tap 0 and written at tap 8.  A fragments are read from the halo at the
+// lane's pixel + the uniform tap offset; the halo is XOR-swizzled by pixel (chunk c of pixel
+// p at slot c ^ (p & 7)), so 16 consecutive pixels read 16 distinct bank groups.
+struct HaloGeom {
+  int TR, IMG;        // tile = IMG images x TR output rows (TR == P when IMG > 1)
+  int HT, HW;         // halo rows (TR + 2) and columns (Q + 2) per image
+  int NHC;            // halo 16-B chunks per 64-channel slice = IMG * HT * HW * 8
+};
+
+template <int BM, int BN, int HMAX>
+struct HaloSmem {
+  static constexpr int HALO = HMAX * 16;              // bytes (max halo chunks)
+  static constexpr int BSTAGE = BN * BK * 2;          // bytes per weight stage
+  static constexpr int MAIN = HALO + 2 * BSTAGE;
+  static constexpr int RED = 4 * BN * 4 + BM * (BN + 8) * 2;
+  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
+};
+
+template <int BM, int BN, int HMAX>
+__global__ __launch_bounds__(NT, 2) void igemm_halo_kernel(const bf16* __restrict__ src,
+                                                            const bf16* __restrict__ wt,
+                                                            ConvGeom g, EpiParams e, HaloGeom hg) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int BR = BN / 32;
+  constexpr int HR = (HMAX + NT - 1) / NT;            // halo chunks per thread
+  using SM = HaloSmem<BM, BN, HMAX>;
+  __shared__ __attribute__((aligned(16))) char smem[SM::BYTES];
+  char* halo = smem;
+  bf16* sB = (bf16*)(smem + SM::HALO);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = (g.Ncols + BN - 1) / BN;
+  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int cc = tid & 7;
+  const int Kelems = g.Kc * 8;
+  const int PQ = g.RP * g.RQ;
+  // tile origin: image n0i, output row p0 (rows of one image, or whole images)
+  const int n0i = m0 / PQ;
+  const int p0 = (m0 - n0i * PQ) / g.RQ;
+
+  // halo slots of this thread: source element offset (channel chunk 0) or -1, LDS byte offset
+  int hsrc[HR], hdst[HR];
+#pragma unroll
+  for (int i = 0; i < HR; ++i) {
+    const int id = tid + i * NT;
+    hsrc[i] = -1;
+    hdst[i] = -1;
+    if (id < hg.NHC) {
+      const int pix = id >> 3, c8 = id & 7;
+      const int per = hg.HT * hg.HW;
+      const int img = pix / per, rem = pix - img * per;
+      const int hr = rem / hg.HW, hc = rem - hr * hg.HW;
+      const int h = p0 + hr - 1, ww = hc - 1, n = n0i + img;
+      if ((unsigned)h < (unsigned)g.SH && (unsigned)ww < (unsigned)g.SW && n * PQ < g.M)
+        hsrc[i] = ((n * g.SH + h) * g.SW + ww) * g.SC + c8 * 8;
+      hdst[i] = (pix * 8 + (c8 ^ (pix & 7))) * 16;
+    }
+  }
+  // lane's A pixel (halo index at tap (0,0)) for each of its TM fragment rows
+  int apix[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int row = wm * (BM / 2) + tm * 16 + (lane & 15);   // tile-local output pixel
+    const int img = row / (hg.TR * g.RQ), rem = row - img * hg.TR * g.RQ;
+    const int tr = rem / g.RQ, q = rem - tr * g.RQ;
+    apix[tm] = (img * hg.HT + tr) * hg.HW + q;
+  }
+  int boff[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    boff[i] = n < g.Ncols ? n * Kelems : -1;
+  }
+  const bf16* zp = g.zero;
+  const int ncb = g.SC >> 6;              // 64-channel chunks
+  const int nsteps = ncb * 9;
+
+  u32x4 rh[HR], rb[BR];
+  auto load_halo = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < HR; ++i)
+      rh[i] = *(const u32x4*)(hsrc[i] >= 0 ? src + hsrc[i] + cb * 64 : zp);
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int i = 0; i < HR; ++i)
+      if (hdst[i] >= 0) *(u32x4*)(halo + hdst[i]) = rh[i];
+  };
+  auto load_b = [&](int s) {
+    const int cb = s / 9, tap = s - cb * 9;
+    const int k = tap * g.SC + cb * 64 + cc * 8;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *(const u32x4*)(boff[i] >= 0 ? wt + boff[i] + k : zp);
+  };
+  auto store_b = [&](int buf) {
+    bf16* b = sB + buf * (BN * BK);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *(u32x4*)(b + row * BK + swz(row, cc) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_halo(0);
+  load_b(0);
+  store_halo();
+  store_b(0);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cb = s / 9, tap = s - cb * 9;
+    const bool more = s + 1 < nsteps;
+    const bool next_chunk = cb + 1 < ncb;
+    if (more) load_b(s + 1);
+    if (tap == 0 && next_chunk) load_halo(cb + 1);
+    // MFMAs of this tap: A from the halo at (pixel + tap offset), B from the weight stage
+    const int toff = (tap / 3) * hg.HW + (tap - (tap / 3) * 3);
+    const bf16* b = sB + (s & 1) * (BN * BK);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int p = apix[tm] + toff;
+        fa[tm] = *(const bf16x8*)(halo + (p * 8 + (chunk ^ (p & 7))) * 16);
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wn * (BN / 2) + tn * 16 + (lane & 15);
+        fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
+    }
+    if (tap == 8 && next_chunk) {
+      __syncthreads();                 // every wave is done with this chunk's halo
+      store_halo();
+    }
+    if (more) store_b((s + 1) & 1);
+    __syncthreads();
+  }
+  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, blockIdx.x, 0, gridDim.x, 1);
+}
+
+// Can the halo kernel run this forward conv with a BM x BN tile?  Fills hg.
+static bool halo_geom(const ConvGeom& g, int bm, HaloGeom& hg, int hmax) {
+  if (g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || (g.SC & 63) ||
+      g.SH != g.RP || g.SW != g.RQ)
+    return false;
+  const int PQ = g.RP * g.RQ;
+  if (bm <= PQ) {
+    if (PQ % bm || bm % g.RQ) return false;
+    hg.TR = bm / g.RQ;
+    hg.IMG = 1;
+  } else {
+    if (bm % PQ) return false;
+    hg.TR = g.RP;
+    hg.IMG = bm / PQ;
+  }
+  hg.HT = hg.TR + 2;
+  hg.HW = g.RQ + 2;
+  hg.NHC = hg.IMG * hg.HT * hg.HW * 8;
+  return hg.NHC <= hmax && g.M % bm == 0;
+}
+
+// Opt-in (MERCURY_HALO=1).  Measured on MI355X: 3-7 % faster per scoring-batch 3x3 conv in
+// isolation (bench/kernel_sweep.py), unchanged at the train batch, and the overlapped ResNet-18
+// step 1.9 % SLOWER (1.646 vs 1.616 ms) -- the per-stage time is not set by the gather's load
+// volume (profiles/ab_experiments_r1c.json).
+static int g_halo = -1;
+
+template <int BM, int BN>
+bool launch_halo(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, hipStream_t st) {
+  // largest halo of a BM-row tile over the ResNet CIFAR/ImageNet shapes (16-B chunks):
+  // BM 256: 10 x 34 px; 128: 8 images x 6 x 6 px; 64: 4 images x 6 x 6 px
+  constexpr int HMAX = BM >= 256 ? 2816 : (BM >= 128 ? 2304 : 1152);
+  if (g_halo < 0) {
+    const char* v = getenv("MERCURY_HALO");
+    g_halo = (v && v[0] == '1') ? 1 : 0;
+  }
+  HaloGeom hg;
+  if (!g_halo || !halo_geom(g, BM, hg, HMAX)) return false;
+  e.slab = nullptr;
+  const int grid = (g.M / BM) * ((g.Ncols + BN - 1) / BN);
+  hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, HMAX>), dim3(grid), dim3(NT), 0, st, src, wt, g, e,
+                     hg);
+  return true;
+}
+
 // ---------------------------------------------------------------- register-staged loop
 // One (tile bx, K-split by) of the NT GEMM; gx tiles x gy splits in the launch.
 // PRO: BN-apply + activation of the A operand between the global load and the LDS write
@@ -827,6 +1035,7 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
                        per, *pro);
     return;
   }
+  if (!TRANS && pipe == 0 && gy == 1 && launch_halo<BM, BN>(src, wt, g, e, st)) return;
   launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), pipe, st);
 }
 
@@ -878,6 +1087,8 @@ int igemm_read_stamps(unsigned long long* host, int n) {
   return 0;
 #endif
 }
+
+void igemm_set_halo(int on) { g_halo = on ? 1 : 0; }
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   const size_t mtiles = (g.M + bm - 1) / bm, ntiles = (g.Ncols + bn - 1) / bn;
