@@ -33,7 +33,7 @@ SHAPES = [  # C, K, H, R, stride, pad
 def fwd_cands(sp, pipes):
     kt = math.ceil(sp.R * sp.S * sp.Cp / 64)
     out = []
-    for bm, bn in ((256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
+    for bm, bn in ((256, 128), (256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
         if sp.group_rows and sp.group_rows < bm:
             continue
         if bn == 128 and sp.K <= 64:

@@ -48,6 +48,12 @@ __device__ __attribute__((aligned(16))) bf16 g_zero_page[64];
 
 MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
+// 256 x 128 tiles (the B = 320 scoring convs): 128 fp32 accumulators per lane and 96 KB of
+// stages -- one block per CU, every register available to it
+template <int BM, int BN>
+constexpr int nt_occ() { return BM * BN >= 256 * 128 ? 1 : 2; }
+
+
 #ifdef MERCURY_STAMPS
 // Diagnostic build only (-DMERCURY_STAMPS): per-block s_memtime at the phase boundaries of the
 // register-staged body -- entry, first stage staged, main loop done, epilogue done -- written
@@ -111,13 +117,18 @@ MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, 
   }
 }
 
-// acc[tm][tn][j] = OUT[m0 + wm*(BM/2) + tm*16 + (lane&15)][n0 + wn*(BN/2) + tn*16 + 4*(lane>>4) + j]
-template <int BM, int BN>
-MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
+// Waves are laid out WM x WN (WM * WN = 4): 2 x 2 for the LDS-staged loops, 4 x 1 for the
+// direct-A loop.  acc[tm][tn][j] =
+//   OUT[m0 + wm*(BM/WM) + tm*16 + (lane&15)][n0 + wn*(BN/WN) + tn*16 + 4*(lane>>4) + j]
+template <int BM, int BN, int WM>
+using AccT = f32x4[BM / (16 * WM)][BN * WM / 64];
+
+template <int BM, int BN, int WM = 2>
+MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int M, int N,
                      int m0, int n0) {
-  constexpr int TM = BM / 32, TN = BN / 32, LDT = BN + 8;
+  constexpr int WN = 4 / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
   const bool stats = e.stats != nullptr;
   const bool bw = e.bw_sums != nullptr;
   float* red = (float*)smem;   // [2][2][BN] (group, sum|sumsq)  |  [3][BN] bwd sums
@@ -136,21 +147,21 @@ MA_DEV void epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams
   if (e.bias) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const int nb = n0 + wn * (BN / 2) + tn * 16 + 4 * (lane >> 4);
+      const int nb = n0 + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
       bias[tn] = *(const float4*)(e.bias + (nb < N ? nb : N - 4));
     }
   }
   __syncthreads();
-  const int mrow = m0 + wm * (BM / 2) + (lane & 15);
+  const int mrow = m0 + wm * (BM / WM) + (lane & 15);
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
-    const int nl = wn * (BN / 2) + tn * 16 + 4 * (lane >> 4);
+    const int nl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
     float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
     float s2[4] = {0.f, 0.f, 0.f, 0.f}, ss2[4] = {0.f, 0.f, 0.f, 0.f};
     const float bb[4] = {bias[tn].x, bias[tn].y, bias[tn].z, bias[tn].w};
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
-      const int ml = wm * (BM / 2) + tm * 16 + (lane & 15);
+      const int ml = wm * (BM / WM) + tm * 16 + (lane & 15);
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j] + bb[j]);
@@ -444,10 +455,10 @@ MA_DEV void mma_stage(const bf16* a, const bf16* b, f32x4 (&acc)[BM / 32][BN / 3
 // counter is reset by the last arriver (slabs are zero-initialised at allocation).
 constexpr int SEM_INTS = 1024;   // tile counters at the head of the slab (4 KB)
 
-template <int BM, int BN>
-MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& e, int M, int N,
+template <int BM, int BN, int WM = 2>
+MA_DEV void finish(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int M, int N,
                    int m0, int n0, int bx, int by, int gx, int gy) {
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int TM = BM / (16 * WM), TN = BN * WM / 64;
   if (e.slab) {
     const int ntiles = gx;
     const int splits = gy;
@@ -487,7 +498,7 @@ MA_DEV void finish(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const EpiParams& 
     }
     __syncthreads();   // flag read by every wave before the epilogue reuses smem
   }
-  epilogue<BM, BN>(acc, smem, e, M, N, m0, n0);
+  epilogue<BM, BN, WM>(acc, smem, e, M, N, m0, n0);
 }
 
 // ---------------------------------------------------------------- halo-tile 3x3 forward
@@ -517,7 +528,7 @@ struct HaloSmem {
 };
 
 template <int BM, int BN, int HMAX>
-__global__ __launch_bounds__(NT, 2) void igemm_halo_kernel(const bf16* __restrict__ src,
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_halo_kernel(const bf16* __restrict__ src,
                                                             const bf16* __restrict__ wt,
                                                             ConvGeom g, EpiParams e, HaloGeom hg) {
   constexpr int TM = BM / 32, TN = BN / 32;
@@ -883,8 +894,148 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   MA_STAMP(3);
 }
 
+// ---------------------------------------------------------------- direct-A loop (pipe 1)
+// The LDS-staged loops move every A byte through LDS twice: a ds_write_b128 (13 cycles per
+// wave-instruction, ~79 B/clk/CU -- MI355X_MICROARCH.md §LDS) and, with 2 x 2 waves, two
+// ds_read_b128s.  Per 64-deep stage of a 256 x 64 tile that is ~840 LDS cycles per block
+// against ~256 MFMA cycles per wave, and two co-resident blocks make the CU's LDS the bound.
+// Here the 4 waves are stacked along M (4 x 1), so no A row is shared between waves: each lane
+// gathers its A fragments straight from global memory in MFMA operand layout (row lane&15,
+// k-group lane>>4 -> chunks lg and 4 + lg of the stage) into registers, double-buffered one
+// stage ahead.  Only the BN x 64 weight tile goes through LDS (written once, read by the 4
+// waves): ~230 LDS cycles per block-stage.
 template <int BM, int BN, bool TRANS>
-__global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict__ src,
+MA_DEV void igemm_da_body(const bf16* __restrict__ src, const bf16* __restrict__ wt,
+                          const ConvGeom& g, const EpiParams& e, int ktiles_per_split, char* smem,
+                          int bx, int by, int gx, int gy) {
+  constexpr int TM = BM / 64, TN = BN / 16;
+  constexpr int BR = BN / 32;
+  bf16* sB = (bf16*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ntn = (g.Ncols + BN - 1) / BN;
+  const int mt = bx / ntn, nt = bx - mt * ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (g.Kc + 7) / 8;
+  const int kt0 = by * ktiles_per_split;
+  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
+  const int Kelems = g.Kc * 8;
+  const int cc = tid & 7;
+  const int lg = lane >> 4;
+
+  int abase[TM], ah[TM], aw[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int off;
+    row_init<TRANS>(g, m0 + w * (BM / 4) + i * 16 + (lane & 15), off, ah[i], aw[i]);
+    abase[i] = row_base<TRANS>(g, off, ah[i], aw[i]);
+    if (off < 0) ah[i] = -(1 << 28);
+  }
+  int boff[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    boff[i] = n < g.Ncols ? n * Kelems : -1;
+  }
+  KCursor kc;
+  kc.init(g, kt0);
+  const bf16* zp = g.zero;
+
+  u32x4 rb[BR];
+  auto load = [&](int kt, u32x4 (&ra)[2 * TM]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      int r, s, c8;
+      bool kval;
+      kc.decode(g, kt, kk * 4 + lg, r, s, c8, kval);
+      const int toff = tap_offset<TRANS>(g, r, s) + c8 * 8;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool ok = kval && tap_ok<TRANS>(g, ah[i], aw[i], r, s);
+        ra[kk * TM + i] = *(const u32x4*)(ok ? src + abase[i] + toff : zp);
+      }
+    }
+    kc.advance(g);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const bool ok = kt * 8 + cc < g.Kc && boff[i] >= 0;
+      rb[i] = *(const u32x4*)(ok ? wt + boff[i] + (kt * 8 + cc) * 8 : zp);
+    }
+  };
+  auto store_b = [&](int buf) {
+    bf16* b = sB + buf * (BN * BK);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *(u32x4*)(b + row * BK + swz(row, cc) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const u32x4 (&ra)[2 * TM], int buf) {
+    const bf16* b = sB + buf * (BN * BK);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lg;
+      bf16x8 fb[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = tn * 16 + (lane & 15);
+        fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const bf16x8 fa = __builtin_bit_cast(bf16x8, ra[kk * TM + tm]);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
+      }
+    }
+  };
+
+  if (kt0 < kt1) {
+    u32x4 r0[2 * TM], r1[2 * TM];
+    load(kt0, r0);
+    store_b(0);
+    __syncthreads();
+    // two stages per trip so the two A register sets keep fixed names (no copies)
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      const int buf = (kt - kt0) & 1;
+      if (kt + 1 < kt1) load(kt + 1, r1);
+      mma(r0, buf);
+      if (kt + 1 >= kt1) break;
+      store_b(buf ^ 1);
+      __syncthreads();
+      if (kt + 2 < kt1) load(kt + 2, r0);
+      mma(r1, buf ^ 1);
+      if (kt + 2 < kt1) store_b(buf);
+      __syncthreads();
+    }
+  }
+  finish<BM, BN, 4>(acc, smem, e, g.M, g.Ncols, m0, n0, bx, by, gx, gy);
+}
+
+template <int BM, int BN>
+struct DaSmem {
+  static constexpr int MAIN = 2 * BN * BK * 2;
+  static constexpr int BYTES = MAIN > Smem<BM, BN>::RED_BYTES ? MAIN : Smem<BM, BN>::RED_BYTES;
+};
+
+template <int BM, int BN, bool TRANS>
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_da_kernel(const bf16* __restrict__ src,
+                                                          const bf16* __restrict__ wt,
+                                                          ConvGeom g, EpiParams e,
+                                                          int ktiles_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[DaSmem<BM, BN>::BYTES];
+  igemm_da_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x, blockIdx.y,
+                               gridDim.x, gridDim.y);
+}
+
+template <int BM, int BN, bool TRANS>
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const bf16* __restrict__ src,
                                                           const bf16* __restrict__ wt,
                                                           ConvGeom g, EpiParams e,
                                                           int ktiles_per_split) {
@@ -896,7 +1047,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_nt_kernel(const bf16* __restrict_
 
 // forward conv with the BN-apply prologue on its input (ProParams)
 template <int BM, int BN>
-__global__ __launch_bounds__(NT, 2) void igemm_pro_kernel(const bf16* __restrict__ src,
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_pro_kernel(const bf16* __restrict__ src,
                                                            const bf16* __restrict__ wt,
                                                            ConvGeom g, EpiParams e,
                                                            int ktiles_per_split, ProParams pro) {
@@ -1006,6 +1157,8 @@ void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiPa
   if (pipe >= 4)
     hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, (BM + BN > 256 ? 3 : 4), TRANS>), grid, dim3(NT),
                        0, st, src, wt, g, e, per);
+  else if (pipe == 1)
+    hipLaunchKernelGGL((igemm_da_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
   else if (pipe == 3)
     hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, 3, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e,
                        per);
@@ -1121,6 +1274,7 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const E
   MA_CASE(64, 128)
   MA_CASE(64, 64)
   MA_CASE(256, 64)
+  MA_CASE(256, 128)
 #undef MA_CASE
 }
 

@@ -120,7 +120,7 @@ def _time(fn, iters=15):
 def _fwd_candidates(sp):
     kt = math.ceil(sp.R * sp.S * sp.Cp / 64)
     out = []
-    for bm, bn in ((256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
+    for bm, bn in ((256, 128), (256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
         if sp.group_rows and sp.group_rows < bm:
             continue
         if bn == 128 and sp.K <= 64:

@@ -74,7 +74,7 @@ def test_conv_fwd_and_stats(case):
 
 
 @pytest.mark.parametrize('bm_bn_split', [(128, 128, 1), (64, 64, 3), (128, 64, 2), (64, 128, 1),
-                                         (256, 64, 1)])
+                                         (256, 64, 1), (256, 128, 1), (256, 128, 3)])
 def test_conv_fwd_all_tiles(bm_bn_split):
     ops = _ops()
     from mercury_amd.ops.conv import ConvSpec, slab_bytes
@@ -646,10 +646,11 @@ def test_depthwise_strips_ghost_stats(case):
     close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize('pipe', [3, 4])
+@pytest.mark.parametrize('pipe', [1, 3, 4])
 @pytest.mark.parametrize('case', CONV_CASES)
 def test_conv_pipelined_lds_dma(case, pipe):
-    """LDS-DMA ring variant of the NT implicit GEMM: forward, stats, dgrad, all tile shapes."""
+    """Main-loop variants of the NT implicit GEMM -- direct-A registers (1), LDS-DMA ring (3, 4):
+    forward, stats, split-K, dgrad, all tile shapes."""
     ops = _ops()
     from mercury_amd.ops.conv import ConvSpec, slab_bytes
     N, H, W, C, K, R, S, st, pd = case
@@ -658,7 +659,8 @@ def test_conv_pipelined_lds_dma(case, pipe):
     xn = ops.to_nhwc(x)
     wk, wt = ops.pack_conv_weight(w)
     ref = F.conv2d(x, w, stride=st, padding=pd)
-    for plan in [(128, 128, 1), (64, 128, 2), (128, 64, 1), (64, 64, 3), (256, 64, 1)]:
+    for plan in [(128, 128, 1), (64, 128, 2), (128, 64, 1), (64, 64, 3), (256, 64, 1),
+                 (256, 128, 2)]:
         out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
         stats = torch.zeros(2, K, device=DEV)
         ops.conv_fwd(xn, wk, out, spec, stats=stats, plan=plan, pipe=pipe)
