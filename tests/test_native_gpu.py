@@ -244,3 +244,33 @@ def test_tiny_shard_smaller_than_batch_cycles():
     assert int(idx.min()) >= 0 and int(idx.max()) < 10
     assert sorted(set(idx[:10].tolist())) == list(range(10))    # one batch = a permutation, wrapped
     assert np.isfinite(eng.read_meters()['loss_sum'])
+
+
+def test_step_tuner_keeps_engine_consistent():
+    """In-situ plan tuner (ops/step_tune.py): every coordinate is a real plan of the engine,
+    tuned plans land in its plan table, and the re-captured step still trains."""
+    from mercury_amd.models import ResNet18
+    from mercury_amd.ops import step_tune, tune
+    torch.manual_seed(0)
+    net = ResNet18(10).to(DEV)
+    eng = _engine(net)
+    eng.use_graphs = True
+    eng.prime()
+    eng.step()
+    eng.build_graphs()
+    coords = step_tune.coordinates(eng)
+    kinds = {k for k, _, _ in coords}
+    assert kinds == {'fwd', 'bwd'}
+    res, base, final = step_tune.tune_step(eng, steps=2, chunks=1, budget_s=3.0,
+                                           log=lambda s: None)
+    assert res and base > 0 and final > 0
+    for kind, key, users in coords:
+        if key in res:
+            m, name, _ = users[0]
+            got = step_tune._get(kind, users)
+            want = tuple(res[key]) if kind == 'fwd' else tuple(tuple(p) for p in res[key])
+            assert got == want
+    for _ in range(3):
+        eng.step()
+    assert math.isfinite(float(eng.read_meters()['loss_sum']))
+    assert tune._key('fwd', coords[0][2][0][2]).startswith('fwd|')
