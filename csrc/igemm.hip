@@ -1034,6 +1034,16 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_da_kernel(const 
                                gridDim.x, gridDim.y);
 }
 
+
+// XCD-aware tile order.  The dispatcher places workgroup b on XCD b % 8 and each XCD has its
+// own 4 MB L2, so with tile = blockIdx.x, neighbouring output tiles -- which share the 3x3
+// halo rows of their input and, across N tiles, the same input rows entirely -- land on
+// different L2s.  Renumber so XCD x runs one contiguous range of tiles (bijective on [0, n)).
+MA_DEV int xcd_tile(int b, int n) {
+  const int per = n >> 3, rem = n & 7, x = b & 7;
+  return x * per + min(x, rem) + (b >> 3);
+}
+
 template <int BM, int BN, bool TRANS>
 __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const bf16* __restrict__ src,
                                                           const bf16* __restrict__ wt,
@@ -1041,7 +1051,8 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const 
                                                           int ktiles_per_split) {
   __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
   const ProParams none{};
-  igemm_nt_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x, blockIdx.y,
+  const int bx = gridDim.y == 1 ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  igemm_nt_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, bx, blockIdx.y,
                                gridDim.x, gridDim.y, none);
 }
 
@@ -1052,7 +1063,8 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_pro_kernel(const
                                                            ConvGeom g, EpiParams e,
                                                            int ktiles_per_split, ProParams pro) {
   __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
-  igemm_nt_body<BM, BN, false, true>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x,
+  const int bx = gridDim.y == 1 ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  igemm_nt_body<BM, BN, false, true>(src, wt, g, e, ktiles_per_split, smem, bx,
                                      blockIdx.y, gridDim.x, gridDim.y, pro);
 }
 
@@ -1213,6 +1225,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict_
   } else {
     const int d = b - nw;
     const ProParams none{};
+    // (no XCD renumbering here: measured +1 % step time -- the pair's wgrad blocks come first,
+    // so the dgrad tiles' XCD placement is already rotated and interleaved with them)
     igemm_nt_body<DBM, DBN, true>(dy, wt, g, e, dper, smem, d % dgx, d / dgx, dgx, dgy, none);
   }
 }
