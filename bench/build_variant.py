@@ -2,6 +2,7 @@
 
     python bench/build_variant.py REV OUT.so csrc/igemm.hip csrc/igemm.h csrc/bindings.cpp
     MERCURY_EXT_PATH=OUT.so python bench.py ...
+    MERCURY_VARIANT_FLAGS=-DMERCURY_STAMPS python bench/build_variant.py HEAD OUT.so   # + flags
 
 Files not named come from the working tree.  Kernel timings differ by several percent
 between MI355X devices, so variants are compared on the same box in one GPU call.
@@ -29,6 +30,7 @@ def main():
             fh.write(data)
     _build.CSRC, _build.OBJ, _build.TARGET = src, os.path.join(tmp, 'obj'), out
     _build.HIP_FLAGS = [f if not f.startswith('-I') else '-I' + src for f in _build.HIP_FLAGS]
+    _build.HIP_FLAGS += os.environ.get('MERCURY_VARIANT_FLAGS', '').split()
     _build.build(verbose=True)
     print(out)
 

@@ -35,7 +35,7 @@ def main():
     ops.conv_fwd(x, wk, y, sp, stats=stats, slab=slab, plan=plan)
     torch.cuda.synchronize()
     nb = (sp.M + plan[0] - 1) // plan[0] * ((K + plan[1] - 1) // plan[1]) * plan[2]
-    v = np.array(ops.lib().igemm_stamps(min(nb, 8192)), dtype=np.int64).reshape(-1, 8)
+    v = np.array(ops.lib().igemm_stamps(min(nb, 8192)), dtype=np.int64).reshape(-1, 12)
     if v.size == 0:
         print('not a stamps build')
         return
@@ -48,6 +48,9 @@ def main():
     print('  epilogue  med/p90 %s' % f(epi))
     print('  main-loop split (median cycles summed over stages): load-issue %d  mfma %d  '
           'store(+load wait) %d  barrier %d' % tuple(np.median(v[:, 4 + q]) for q in range(4)))
+    e = lambda a, b: np.median(v[:, b] - v[:, a])
+    print('  epilogue split (median): split-K/setup %d  acc->LDS tile + stats %d  '
+          'sync + stats atomics %d  row stores %d' % (e(2, 8), e(8, 9), e(9, 10), e(10, 3)))
     print('  block start spread med/p90/max %d %d %d, kernel span %d' % (
         np.median(t0), np.percentile(t0, 90), t0.max(), v[:, 3].max() - v[:, 0].min()))
 

@@ -118,7 +118,7 @@ PYBIND11_MODULE(_C, m) {
     return mask;
   });
   m.def("igemm_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
-    std::vector<unsigned long long> v((size_t)n * 8, 0ull);
+    std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!igemm_read_stamps(v.data(), n)) v.clear();
     return v;
   });

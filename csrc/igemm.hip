@@ -58,7 +58,7 @@ constexpr int nt_occ() { return BM * BN >= 256 * 128 ? 1 : 2; }
 // Diagnostic build only (-DMERCURY_STAMPS): per-block s_memtime at the phase boundaries of the
 // register-staged body -- entry, first stage staged, main loop done, epilogue done -- written
 // by thread 0 into a buffer no other code reads (bench/stamp_conv.py).
-__device__ unsigned long long g_stamps[8192][8];
+__device__ unsigned long long g_stamps[8192][12];   // [8..10]: epilogue sub-phases
 #define MA_STAMP(i)                                                                         \
   do {                                                                                      \
     if (threadIdx.x == 0) {                                                                 \
@@ -152,6 +152,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
     }
   }
   __syncthreads();
+  MA_STAMP(8);
   const int mrow = m0 + wm * (BM / WM) + (lane & 15);
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
@@ -211,6 +212,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       }
     }
   }
+  MA_STAMP(9);
   __syncthreads();
   if (stats) {
     for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
@@ -238,6 +240,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
     bn_mean_rstd8(e.bw_stats + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean, rstd);
     if (two) bn_mean_rstd8(e.bw_stats2 + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean2, rstd2);
   }
+  MA_STAMP(10);
   for (int i = tid; i < BM * CPR; i += NT) {
     const int rl = i / CPR;
     const int row = m0 + rl, col = colc;
@@ -1246,7 +1249,7 @@ void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, in
 
 int igemm_read_stamps(unsigned long long* host, int n) {
 #ifdef MERCURY_STAMPS
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n) ==
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 12 * n) ==
          hipSuccess;
 #else
   (void)host;
