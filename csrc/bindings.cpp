@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -46,6 +47,8 @@ PYBIND11_MODULE(_C, m) {
                     int pipe, uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
                     uintptr_t bw_stats2, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
                     int bw_act) {
+    if (stats && bw_sums)   // the epilogue reduces both through one LDS scratch
+      throw std::invalid_argument("igemm: forward BN stats and backward BN sums are exclusive");
     ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
     EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows,
                 accumulate, P<float>(slab), P<const bf16>(bw_out), P<const bf16>(bw_y),

@@ -82,7 +82,7 @@ __device__ unsigned long long g_stamps[8192][12];   // [8..10]: epilogue sub-pha
 template <int BM, int BN>
 struct Smem {
   static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
-  static constexpr int RED_BYTES = 4 * BN * 4 + BM * (BN + 8) * 2;   // stats + staged tile
+  static constexpr int RED_BYTES = 16 * BN * 4 + BM * (BN + 8) * 2;  // stats + staged tile
   static constexpr int bytes(int stages) {
     return stages * STAGE * 2 > RED_BYTES ? stages * STAGE * 2 : RED_BYTES;
   }
@@ -131,10 +131,12 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
   const int wm = w / WN, wn = w % WN;
   const bool stats = e.stats != nullptr;
   const bool bw = e.bw_sums != nullptr;
-  float* red = (float*)smem;   // [2][2][BN] (group, sum|sumsq)  |  [3][BN] bwd sums
-  bf16* tile = (bf16*)(smem + 4 * BN * 4);         // [BM][LDT] staged output
-  if (stats || bw) {
-    for (int i = tid; i < 4 * BN; i += NT) red[i] = 0.f;
+  // stats: [WM][4][BN] per-wave-row partials (sum | sumsq | group-2 sum | group-2 sumsq),
+  // each slot written by exactly one lane -- no LDS atomics, no zeroing; bw: [3][BN] sums
+  float* red = (float*)smem;
+  bf16* tile = (bf16*)(smem + 16 * BN * 4);        // [BM][LDT] staged output
+  if (bw) {
+    for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
   }
   // ghost-BN groups: a tile may straddle ONE group boundary (groups are >= BM rows), e.g. when
   // the per-image pixel count is odd (speech VGG 101x161); rows >= bnd go to group g + 1
@@ -168,20 +170,31 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j] + bb[j]);
       *(bf16x4*)(tile + ml * LDT + nl) = o;   // one 8-byte LDS write per lane
       const int row = mrow + tm * 16;
-      if (stats && row < M) {
-        if (!straddle || row < bnd) {
+      if (stats) {
+        if (!straddle) {
+          // rows past M masked by a multiply, not an exec-mask branch per fragment
+          const float msk = row < M ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]);
+            const float f = bf2f(o[j]) * msk;
             s[j] += f;
             ss[j] += f * f;
           }
-        } else {
+        } else if (row < M) {
+          if (row < bnd) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]);
-            s2[j] += f;
-            ss2[j] += f * f;
+            for (int j = 0; j < 4; ++j) {
+              const float f = bf2f(o[j]);
+              s[j] += f;
+              ss[j] += f * f;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float f = bf2f(o[j]);
+              s2[j] += f;
+              ss2[j] += f * f;
+            }
           }
         }
       }
@@ -200,14 +213,12 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
         }
       }
       if ((lane & 15) == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          atomicAdd(&red[nl + j], s[j]);
-          atomicAdd(&red[BN + nl + j], ss[j]);
-          if (straddle) {
-            atomicAdd(&red[2 * BN + nl + j], s2[j]);
-            atomicAdd(&red[3 * BN + nl + j], ss2[j]);
-          }
+        float* r = red + wm * 4 * BN + nl;
+        *(float4*)r = make_float4(s[0], s[1], s[2], s[3]);
+        *(float4*)(r + BN) = make_float4(ss[0], ss[1], ss[2], ss[3]);
+        if (straddle) {
+          *(float4*)(r + 2 * BN) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+          *(float4*)(r + 3 * BN) = make_float4(ss2[0], ss2[1], ss2[2], ss2[3]);
         }
       }
     }
@@ -220,8 +231,14 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       for (int i = tid; i < BN; i += NT) {
         const int col = n0 + i;
         if (col < N) {
-          atomicAdd(dst + col, red[2 * BN * gi + i]);
-          atomicAdd(dst + e.stats_ld + col, red[2 * BN * gi + BN + i]);
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int q = 0; q < WM; ++q) {
+            a += red[(q * 4 + 2 * gi) * BN + i];
+            b += red[(q * 4 + 2 * gi + 1) * BN + i];
+          }
+          atomicAdd(dst + col, a);
+          atomicAdd(dst + e.stats_ld + col, b);
         }
       }
     }
@@ -526,7 +543,7 @@ struct HaloSmem {
   static constexpr int HALO = HMAX * 16;              // bytes (max halo chunks)
   static constexpr int BSTAGE = BN * BK * 2;          // bytes per weight stage
   static constexpr int MAIN = HALO + 2 * BSTAGE;
-  static constexpr int RED = 4 * BN * 4 + BM * (BN + 8) * 2;
+  static constexpr int RED = Smem<BM, BN>::RED_BYTES;
   static constexpr int BYTES = MAIN > RED ? MAIN : RED;
 };
 
