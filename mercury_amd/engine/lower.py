@@ -1,8 +1,8 @@
 """Lower a reference-architecture ``nn.Module`` to the native engine's unit graph.
 
 The engine does not trace anything: it walks the known module trees of the
-model zoo (``models/resnet.py`` = `pytorch_model.py:14-113`, and
-``models/mobilenetv2.py``) and emits
+model zoo (``models/resnet.py`` = `pytorch_model.py:14-113`, ``models/vgg.py`` =
+`pytorch_model.py:117-153`, and ``models/mobilenetv2.py``) and emits
 
 * ``Unit``  -- one conv (implicit-GEMM or depthwise) + its BatchNorm + activation;
 * ``Block`` -- main-path units, an optional shortcut unit or identity skip, the
