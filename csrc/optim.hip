@@ -46,10 +46,16 @@ MA_DEV void write_copies(const OptSeg& sg, long long local, float v) {
 }
 
 // One 64(k) x 64(c) tile of one (segment, r*S+s) per workgroup: coalesced 2-byte reads
-// along c from the KRSC copy, LDS transpose, coalesced writes along k to CRSK.
+// along c from the KRSC copy, LDS transpose, coalesced writes along k to CRSK.  The tile
+// holds one value per dword (bf16 -> fp32 -> bf16 is exact) with a 65-dword row stride, so
+// the column read tile[tx][r] hits bank (tx + r) mod 64 -- a 2-byte tile with a 65-element
+// stride put two lanes in every dword and measured one bank conflict per LDS instruction
+// (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 1.0, profiles/pmc_step_r1f.txt).  Conflicts are now 0
+// but the kernel time is unchanged (20.6 -> 21.0 us): it is bound by its 2-byte global
+// accesses, so the next step is 16-byte (bf16x8) loads and stores.
 __global__ __launch_bounds__(256) void transpose_weights_kernel(const OptSeg* segs,
                                                                 const int* jobs) {
-  __shared__ bf16 tile[64][65];
+  __shared__ float tile[64][65];
   const int* j = jobs + blockIdx.x * 4;
   const OptSeg sg = segs[j[0]];
   const int rs = j[1], k0 = j[2], c0 = j[3];
@@ -57,12 +63,12 @@ __global__ __launch_bounds__(256) void transpose_weights_kernel(const OptSeg* se
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, c = c0 + tx;
-    tile[r][tx] = (k < sg.K && c < sg.C) ? sg.w_krsc[((size_t)k * RS + rs) * sg.Cpad + c] : f2bf(0.f);
+    tile[r][tx] = (k < sg.K && c < sg.C) ? bf2f(sg.w_krsc[((size_t)k * RS + rs) * sg.Cpad + c]) : 0.f;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
     const int c = c0 + r, k = k0 + tx;
-    if (c < sg.C && k < sg.K) sg.w_crsk[((size_t)c * RS + rs) * sg.K + k] = tile[tx][r];
+    if (c < sg.C && k < sg.K) sg.w_crsk[((size_t)c * RS + rs) * sg.K + k] = f2bf(tile[tx][r]);
   }
 }
 
