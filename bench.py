@@ -51,6 +51,45 @@ PRESETS = {
 }
 
 
+def diagnostics(eng, steps, ws):
+    """Untimed steps AFTER the timed loop: device-phase times (HIP events on each stream),
+    the DP communicator's view (ranks, bucket bytes, all-reduce device time, the part of it
+    not hidden under backward / scoring) and a final replica check across ranks."""
+    import torch
+    import torch.distributed as dist
+    acc = {}
+    for _ in range(steps):
+        eng.timer.on = True
+        eng.step()
+        eng.timer.on = False
+        ph = eng.timer.collect()
+        for k, v in ph.items():
+            if not isinstance(v, list):
+                acc.setdefault(k, []).append(v)
+    med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in acc.items()}
+    plan = eng.bucket_plan()
+    out = {'device_phase_ms': {k: med[k] for k in ('step', 'critical', 'score', 'train', 'wait',
+                                                   'tail') if k in med}}
+    dp = {'backend': dist.get_backend() if dist.is_initialized() else None,
+          'comm': 'rccl' if eng.comm is not None else ('pg' if eng.dp else None),
+          'comm_ranks': eng.comm.size if eng.comm is not None else
+          (dist.get_world_size() if dist.is_initialized() else 1),
+          'buckets_bytes': [4 * (e - s) for s, e in sorted(plan.values(), reverse=True)],
+          'wire': 'bf16' if eng.wire_bf16 else 'fp32',
+          'allreduce_ms_per_step': med.get('comm'), 'comm_exposed_ms': med.get('comm_exposed'),
+          'overlap_frac': med.get('overlap')}
+    torch.cuda.synchronize()
+    if ws > 1:
+        from mercury_amd.parallel.health import check_replicas
+        ok, spread = check_replicas(eng.opt.p)
+        dp['replicas_identical'] = bool(ok)
+        dp['replica_spread'] = float(spread)
+    if eng.check_order:
+        dp['order_violations'] = eng.order_violations()[0]
+    out['dp'] = dp
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -61,6 +100,14 @@ def main():
     ap.add_argument('--pool-batches', type=int, default=10)
     ap.add_argument('--no-overhead', action='store_true')
     ap.add_argument('--no-graphs', action='store_true')
+    ap.add_argument('--force-buckets', action='store_true',
+                    help='issue the RCCL bucket all-reduces even at one GPU (path check)')
+    ap.add_argument('--comm', default='auto', choices=('auto', 'rccl', 'pg'),
+                    help='DP all-reduce: own RCCL communicator on a comm stream, or the torch '
+                         'ProcessGroup')
+    ap.add_argument('--wire-bf16', action='store_true', help='bf16 gradients on the wire')
+    ap.add_argument('--diag-steps', type=int, default=5,
+                    help='untimed steps after the timed loop with device-phase events')
     args = ap.parse_args()
     pre = PRESETS[args.config]
     args.batch = args.batch or pre['batch']
@@ -69,7 +116,7 @@ def main():
     import torch
     import torch.distributed as dist
     from mercury_amd.parallel import dist as pdist
-    rank, ws, device = pdist.init_from_env()
+    rank, ws, device = pdist.init_from_env(force=args.force_buckets)
     if ws != args.gpus and rank == 0:
         print('[bench] warning: WORLD_SIZE=%d but --gpus=%d' % (ws, args.gpus), file=sys.stderr)
 
@@ -96,7 +143,9 @@ def main():
     def make(importance):
         eng = NativeEngine(net, device, args.batch, args.pool_batches, optimizer='adam',
                            lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
-                           use_graphs=not args.no_graphs, image_hw=hw)
+                           use_graphs=not args.no_graphs, image_hw=hw,
+                           force_buckets=args.force_buckets, comm=args.comm,
+                           wire_bf16=args.wire_bf16)
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)
@@ -127,6 +176,7 @@ def main():
     eng = make(True)
     t_is = run(eng, args.steps, args.warmup)
     m = eng.read_meters()
+    diag = diagnostics(eng, args.diag_steps, ws)
     ms = t_is * 1e3 / args.steps
     value = ws * args.batch * args.steps / t_is
     overhead = None
@@ -155,8 +205,9 @@ def main():
                        'sampler': 'importance (loss + 0.5*EMA), with replacement'},
             'final_train_loss': round(m['loss_sum'] / max(m['count'], 1), 4),
         }
+        out.update(diag)
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

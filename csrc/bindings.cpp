@@ -25,6 +25,9 @@ void comm_allgather(uintptr_t c, uintptr_t send, uintptr_t recv, long long count
 void comm_broadcast(uintptr_t c, uintptr_t buf, long long count, int dtype, int root, uintptr_t st);
 void comm_ring_allreduce(uintptr_t c, uintptr_t buf, long long count, uintptr_t work, int avg,
                          uintptr_t st);
+void add_f32(float* dst, const float* src, long long n, hipStream_t s);
+void order_check_launch(int* o, int slot, int ref, int mult, int add, int ge, int tick, int at,
+                        hipStream_t st);
 
 namespace py = pybind11;
 
@@ -106,26 +109,21 @@ PYBIND11_MODULE(_C, m) {
     comm_ring_allreduce(c, buf, count, work, avg, st);
     check_launch("comm_ring_allreduce");
   });
-  // a HIP stream whose kernels may only use the CUs set in `mask` (bit i = CU i); wrapped on
-  // the Python side with torch.cuda.ExternalStream
-  m.def("cu_mask_stream", [](std::vector<uint32_t> mask) {
-    hipStream_t st = nullptr;
-    const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
-    if (e != hipSuccess)
-      throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
-    return reinterpret_cast<uintptr_t>(st);
+  m.def("add_f32", [](uintptr_t dst, uintptr_t src, long long n, uintptr_t st) {
+    add_f32(P<float>(dst), P<const float>(src), n, S(st));
+    check_launch("add_f32");
   });
-  m.def("cu_mask_of", [](uintptr_t st, int words) {
-    std::vector<uint32_t> mask((size_t)words, 0u);
-    (void)hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(st), (uint32_t)words, mask.data());
-    return mask;
+  // stream-order race detector (runtime.hip)
+  m.def("order_check", [](uintptr_t o, int slot, int ref, int mult, int add, int ge, int tick,
+                          int at, uintptr_t st) {
+    order_check_launch(P<int>(o), slot, ref, mult, add, ge, tick, at, S(st));
+    check_launch("order_check");
   });
   m.def("igemm_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!igemm_read_stamps(v.data(), n)) v.clear();
     return v;
   });
-  m.def("igemm_set_halo", &igemm_set_halo);
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
     ConvGeom g{};
     g.M = M;

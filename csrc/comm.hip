@@ -23,20 +23,26 @@
 
 namespace {
 
+// dst += src.  VEC: both pointers 16-byte aligned (checked by the launcher) -> one f32x4 per
+// thread for the body; the < 4 tail elements go to the first threads of the grid, in parallel.
+template <bool VEC>
 __global__ __launch_bounds__(256) void add_f32_kernel(float* __restrict__ dst,
                                                       const float* __restrict__ src, long long n) {
-  const long long i4 = ((long long)blockIdx.x * 256 + threadIdx.x);
-  const long long n4 = n >> 2;
-  if (i4 < n4) {
-    f32x4 a = ((const f32x4*)dst)[i4];
-    const f32x4 b = ((const f32x4*)src)[i4];
-    a += b;
-    ((f32x4*)dst)[i4] = a;
-  }
-  if (i4 == 0) {
-    for (long long j = n4 * 4; j < n; ++j) dst[j] += src[j];
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (VEC) {
+    const long long n4 = n >> 2;
+    if (i < n4) {
+      f32x4 a = ((const f32x4*)dst)[i];
+      a += ((const f32x4*)src)[i];
+      ((f32x4*)dst)[i] = a;
+    }
+    const long long j = n4 * 4 + i;
+    if (i < 4 && j < n) dst[j] += src[j];
+  } else if (i < n) {
+    dst[i] += src[i];
   }
 }
+
 
 __global__ __launch_bounds__(256) void scale_f32_kernel(float* __restrict__ x, float s, long long n) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -59,6 +65,15 @@ ncclDataType_t dtype_of(int code) {
 }
 
 }  // namespace
+
+void add_f32(float* dst, const float* src, long long n, hipStream_t s) {
+  if (n <= 0) return;
+  const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const long long work = vec ? (n >> 2) + 1 : n;
+  const unsigned blocks = (unsigned)((work + 255) / 256);
+  if (vec) hipLaunchKernelGGL(add_f32_kernel<true>, dim3(blocks), dim3(256), 0, s, dst, src, n);
+  else hipLaunchKernelGGL(add_f32_kernel<false>, dim3(blocks), dim3(256), 0, s, dst, src, n);
+}
 
 std::string comm_unique_id() {
   ncclUniqueId id;
@@ -110,8 +125,13 @@ void comm_ring_allreduce(uintptr_t c, uintptr_t buf, long long count, uintptr_t 
   float* x = reinterpret_cast<float*>(buf);
   float* tmp = reinterpret_cast<float*>(work);
   if (W > 1) {
-    // chunk k = [off(k), off(k+1)), sizes differ by at most one element
-    auto off = [&](int k) { return (long long)k * count / W; };
+    // chunk k = [off(k), off(k+1)): boundaries are multiples of 4 elements (16 bytes), so with
+    // a 16-byte aligned buffer every chunk of x and the workspace takes the vector add; the
+    // last chunk absorbs the remainder
+    auto off = [&](int k) {
+      if (k >= W) return count;
+      return ((long long)k * count / W) & ~3LL;
+    };
     const int right = (r + 1) % W, left = (r + W - 1) % W;
     for (int step = 0; step < W - 1; ++step) {            // reduce-scatter
       const int sc = ((r - step) % W + W) % W, rc = ((r - step - 1) % W + W) % W;
@@ -120,9 +140,7 @@ void comm_ring_allreduce(uintptr_t c, uintptr_t buf, long long count, uintptr_t 
       nccl_check(ncclSend(x + off(sc), (size_t)sn, ncclFloat32, right, comm, s), "ncclSend");
       nccl_check(ncclRecv(tmp, (size_t)rn, ncclFloat32, left, comm, s), "ncclRecv");
       nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-      const long long blocks = ((rn >> 2) + 255) / 256 + 1;
-      hipLaunchKernelGGL(add_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x + off(rc), tmp,
-                         rn);
+      add_f32(x + off(rc), tmp, rn, s);
     }
     for (int step = 0; step < W - 1; ++step) {            // all-gather
       const int sc = ((r + 1 - step) % W + W) % W, rc = ((r - step) % W + W) % W;

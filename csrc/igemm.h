@@ -65,8 +65,6 @@ struct ProParams {
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
-// halo-tile 3x3 forward on/off for subsequent launches (default: MERCURY_HALO env, off)
-void igemm_set_halo(int on);
 // pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages.
 // pro != null: BN-apply prologue (forward, pipe 0 only).
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
@@ -87,3 +85,49 @@ void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, 
 int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
                          int bm, int bn, int splits, const bf16* x, const WgradGeom& wg, float* dw,
                          int wbm, int wbn, int wsplits, hipStream_t st);
+
+// ---------------------------------------------------------------------------- halo conv
+// Forward convolution whose A operand is a HALO TILE in LDS (hconv.hip): a block's output
+// tile is IMG whole images or TR whole output rows of one image, so the input it reads for
+// one 64-channel slice is a small rectangle, staged into LDS ONCE and read by every tap.
+// While staging, the producer's BatchNorm (+ residual / shortcut BN) + activation is applied
+// (HconvPro), so normalised activations never make a separate HBM round trip.
+struct HconvGeom {
+  int N, H, W, C;        // input NHWC (C padded to a multiple of 64)
+  int P, Q, K;           // output pixels per image and channels
+  int R, stride, pad;    // R in {1, 3}
+  int IMG, TR;           // tile = IMG images x TR output rows (TR == P when IMG > 1)
+  int HT, HWd;           // halo rows / columns per image
+  int HWP, HALF;         // LDS pitch (pixels per halo row); stride-2 3x3: even columns first,
+                         // odd columns from HALF on (0 otherwise) -- both bank-conflict choices
+  int HS, SR;            // input step per halo pixel; halo step per output pixel
+  int HPIX;              // halo pixels per tile = IMG * HT * HWP
+  int chunks_per_split;  // 64-channel input slices per K-split
+  const bf16* zero;      // 16-byte zero page (set by the launcher)
+};
+
+struct HconvPro {
+  int mode;              // 0 plain, 1 act(bn(y)), 2 act(bn(y) + res), 3 act(bn(y) + bn2(y2))
+  const float* stats;    // [G][2][C] batch / ghost-group sums of y, or null -> running stats
+  const float* rmean;
+  const float* rvar;
+  const float* gamma;
+  const float* beta;
+  const bf16* res;       // mode 2: residual, same NHWC shape as the input
+  const bf16* y2;        // mode 3: shortcut conv output, same shape
+  const float* stats2;
+  const float* rmean2;
+  const float* rvar2;
+  const float* gamma2;
+  const float* beta2;
+  bf16* keep;            // optional: the computed activation (same shape), written once
+  int group_imgs;        // images per statistics group
+  float inv_count;       // 1 / pixels per statistics group
+  float eps;
+  int act;               // 0 none, 1 relu, 2 relu6
+};
+
+// returns 0 when (bm, bn) is not instantiated
+int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                 const HconvPro& pro, int bm, int bn, int splits, hipStream_t st);
+const bf16* conv_zero_page();

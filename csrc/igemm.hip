@@ -35,14 +35,12 @@
 // a zero page.  Split-K writes fp32 partial tiles in fragment order (16 B per lane,
 // fully coalesced); the last-arriving slice of each tile reduces them and runs the
 // same epilogue inside the launch (see finish()).
-#include "common.h"
-#include "igemm.h"
+
+#include "conv_epi.h"
 #include "wgrad_body.h"
 
 namespace {
 
-constexpr int BK = 64;          // k elements per stage (8 chunks of 8)
-constexpr int NT = 256;         // threads
 
 __device__ __attribute__((aligned(16))) bf16 g_zero_page[64];
 
@@ -53,269 +51,6 @@ MA_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 template <int BM, int BN>
 constexpr int nt_occ() { return BM * BN >= 256 * 128 ? 1 : 2; }
 
-
-#ifdef MERCURY_STAMPS
-// Diagnostic build only (-DMERCURY_STAMPS): per-block s_memtime at the phase boundaries of the
-// register-staged body -- entry, first stage staged, main loop done, epilogue done -- written
-// by thread 0 into a buffer no other code reads (bench/stamp_conv.py).
-__device__ unsigned long long g_stamps[8192][12];   // [8..10]: epilogue sub-phases
-#define MA_STAMP(i)                                                                         \
-  do {                                                                                      \
-    if (threadIdx.x == 0) {                                                                 \
-      const int b_ = blockIdx.x + blockIdx.y * gridDim.x;                                   \
-      if (b_ < 8192) g_stamps[b_][i] = __builtin_amdgcn_s_memtime();                       \
-    }                                                                                       \
-  } while (0)
-// per-phase cycle sums over the main loop (thread 0): [4] load issue, [5] MFMA phase,
-// [6] stage store (incl. the wait for its loads), [7] barrier
-#define MA_LAP(slot, t)                                                                     \
-  do {                                                                                      \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                            \
-    lap[slot] += n_ - t;                                                                    \
-    t = n_;                                                                                 \
-  } while (0)
-#else
-#define MA_STAMP(i) (void)0
-#define MA_LAP(slot, t) (void)0
-#endif
-
-template <int BM, int BN>
-struct Smem {
-  static constexpr int STAGE = (BM + BN) * BK;              // bf16 elements
-  static constexpr int RED_BYTES = 16 * BN * 4 + BM * (BN + 8) * 2;  // stats + staged tile
-  static constexpr int bytes(int stages) {
-    return stages * STAGE * 2 > RED_BYTES ? stages * STAGE * 2 : RED_BYTES;
-  }
-};
-
-// DPP sum over the 16 lanes of a row (quad xor1, quad xor2, half-mirror, mirror)
-MA_DEV float row16_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-  return v;
-}
-
-// ---------------------------------------------------------------- epilogue
-// BN-backward helpers (same arithmetic as bn.hip so fused and standalone reductions agree)
-MA_DEV float bn_act_mask(float out, int act) {
-  if (act == 1) return out > 0.f ? 1.f : 0.f;
-  if (act == 2) return (out > 0.f && out < 6.f) ? 1.f : 0.f;
-  return 1.f;
-}
-MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, float (&mean)[8],
-                          float (&rstd)[8]) {
-  const float4 a = *(const float4*)stats, b = *(const float4*)(stats + 4);
-  const float4 c = *(const float4*)(stats + ld), d = *(const float4*)(stats + ld + 4);
-  const float s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  const float ss[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    mean[k] = s[k] * inv_cnt;
-    rstd[k] = rsqrtf(fmaxf(ss[k] * inv_cnt - mean[k] * mean[k], 0.f) + eps);
-  }
-}
-
-// Waves are laid out WM x WN (WM * WN = 4): 2 x 2 for the LDS-staged loops, 4 x 1 for the
-// direct-A loop.  acc[tm][tn][j] =
-//   OUT[m0 + wm*(BM/WM) + tm*16 + (lane&15)][n0 + wn*(BN/WN) + tn*16 + 4*(lane>>4) + j]
-template <int BM, int BN, int WM>
-using AccT = f32x4[BM / (16 * WM)][BN * WM / 64];
-
-template <int BM, int BN, int WM = 2>
-MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int M, int N,
-                     int m0, int n0) {
-  constexpr int WN = 4 / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w / WN, wn = w % WN;
-  const bool stats = e.stats != nullptr;
-  const bool bw = e.bw_sums != nullptr;
-  // stats: [WM][4][BN] per-wave-row partials (sum | sumsq | group-2 sum | group-2 sumsq),
-  // each slot written by exactly one lane -- no LDS atomics, no zeroing; bw: [3][BN] sums
-  float* red = (float*)smem;
-  bf16* tile = (bf16*)(smem + 16 * BN * 4);        // [BM][LDT] staged output
-  if (bw) {
-    for (int i = tid; i < 3 * BN; i += NT) red[i] = 0.f;
-  }
-  // ghost-BN groups: a tile may straddle ONE group boundary (groups are >= BM rows), e.g. when
-  // the per-image pixel count is odd (speech VGG 101x161); rows >= bnd go to group g + 1
-  const int g0 = stats ? m0 / e.group_rows : 0;
-  const int bnd = stats ? (g0 + 1) * e.group_rows : 0;
-  const bool straddle = stats && bnd < m0 + BM && bnd < M;
-  float4 bias[TN];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) bias[tn] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e.bias) {
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int nb = n0 + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
-      bias[tn] = *(const float4*)(e.bias + (nb < N ? nb : N - 4));
-    }
-  }
-  __syncthreads();
-  MA_STAMP(8);
-  const int mrow = m0 + wm * (BM / WM) + (lane & 15);
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int nl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
-    float s2[4] = {0.f, 0.f, 0.f, 0.f}, ss2[4] = {0.f, 0.f, 0.f, 0.f};
-    const float bb[4] = {bias[tn].x, bias[tn].y, bias[tn].z, bias[tn].w};
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      const int ml = wm * (BM / WM) + tm * 16 + (lane & 15);
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j] + bb[j]);
-      *(bf16x4*)(tile + ml * LDT + nl) = o;   // one 8-byte LDS write per lane
-      const int row = mrow + tm * 16;
-      if (stats) {
-        if (!straddle) {
-          // rows past M masked by a multiply, not an exec-mask branch per fragment
-          const float msk = row < M ? 1.f : 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]) * msk;
-            s[j] += f;
-            ss[j] += f * f;
-          }
-        } else if (row < M) {
-          if (row < bnd) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float f = bf2f(o[j]);
-              s[j] += f;
-              ss[j] += f * f;
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float f = bf2f(o[j]);
-              s2[j] += f;
-              ss2[j] += f * f;
-            }
-          }
-        }
-      }
-    }
-    if (stats) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s[j] = row16_sum(s[j]);
-        ss[j] = row16_sum(ss[j]);
-      }
-      if (straddle) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s2[j] = row16_sum(s2[j]);
-          ss2[j] = row16_sum(ss2[j]);
-        }
-      }
-      if ((lane & 15) == 0) {
-        float* r = red + wm * 4 * BN + nl;
-        *(float4*)r = make_float4(s[0], s[1], s[2], s[3]);
-        *(float4*)(r + BN) = make_float4(ss[0], ss[1], ss[2], ss[3]);
-        if (straddle) {
-          *(float4*)(r + 2 * BN) = make_float4(s2[0], s2[1], s2[2], s2[3]);
-          *(float4*)(r + 3 * BN) = make_float4(ss2[0], ss2[1], ss2[2], ss2[3]);
-        }
-      }
-    }
-  }
-  MA_STAMP(9);
-  __syncthreads();
-  if (stats) {
-    for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
-      float* dst = e.stats + (size_t)(g0 + gi) * 2 * e.stats_ld;
-      for (int i = tid; i < BN; i += NT) {
-        const int col = n0 + i;
-        if (col < N) {
-          float a = 0.f, b = 0.f;
-#pragma unroll
-          for (int q = 0; q < WM; ++q) {
-            a += red[(q * 4 + 2 * gi) * BN + i];
-            b += red[(q * 4 + 2 * gi + 1) * BN + i];
-          }
-          atomicAdd(dst + col, a);
-          atomicAdd(dst + e.stats_ld + col, b);
-        }
-      }
-    }
-  }
-  // coalesced 16-byte row stores from the staged tile.  NT is a multiple of CPR, so every
-  // thread keeps ONE 8-column chunk for the whole loop (its BN constants load once).
-  constexpr int CPR = BN / 8;
-  const int ch = tid % CPR;
-  const int colc = n0 + ch * 8;
-  float mean[8], rstd[8], mean2[8], rstd2[8], sdz[8], sx[8], sx2[8];
-  const bool two = bw && e.bw_y2 != nullptr;
-  if (bw) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = sx2[k] = mean2[k] = 0.f, rstd2[k] = 1.f;
-    const int cc = colc < N ? colc : 0;
-    bn_mean_rstd8(e.bw_stats + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean, rstd);
-    if (two) bn_mean_rstd8(e.bw_stats2 + cc, e.ldo, e.bw_inv_count, e.bw_eps, mean2, rstd2);
-  }
-  MA_STAMP(10);
-  for (int i = tid; i < BM * CPR; i += NT) {
-    const int rl = i / CPR;
-    const int row = m0 + rl, col = colc;
-    if (row >= M || col >= N) continue;
-    bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
-    const size_t off = (size_t)row * e.ldo + col;
-    bf16* dst = e.out + off;
-    if (e.accumulate) {
-      const bf16x8 o = *(const bf16x8*)dst;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = f2bf(bf2f(v[k]) + bf2f(o[k]));
-    }
-    *(bf16x8*)dst = v;
-    if (bw) {
-      const bf16x8 ao = *(const bf16x8*)(e.bw_out + off);
-      const bf16x8 ay = *(const bf16x8*)(e.bw_y + off);
-      bf16x8 ay2;
-      if (two) ay2 = *(const bf16x8*)(e.bw_y2 + off);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float dz = bf2f(v[k]) * bn_act_mask(bf2f(ao[k]), e.bw_act);
-        sdz[k] += dz;
-        sx[k] += dz * (bf2f(ay[k]) - mean[k]) * rstd[k];
-        if (two) sx2[k] += dz * (bf2f(ay2[k]) - mean2[k]) * rstd2[k];
-      }
-    }
-  }
-  if (bw) {
-    // lanes ch, ch+CPR, ... of a wave share the chunk: butterfly, then one LDS atomic per
-    // (wave, column), then one global atomic per column per block
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        sdz[k] += __shfl_xor(sdz[k], o, 64);
-        sx[k] += __shfl_xor(sx[k], o, 64);
-        if (two) sx2[k] += __shfl_xor(sx2[k], o, 64);
-      }
-    }
-    if (lane < CPR) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        atomicAdd(&red[ch * 8 + k], sdz[k]);
-        atomicAdd(&red[BN + ch * 8 + k], sx[k]);
-        if (two) atomicAdd(&red[2 * BN + ch * 8 + k], sx2[k]);
-      }
-    }
-    __syncthreads();
-    for (int i = tid; i < BN; i += NT) {
-      const int col = n0 + i;
-      if (col < N) {
-        atomicAdd(e.bw_sums + col, red[i]);
-        atomicAdd(e.bw_sums + e.ldo + col, red[BN + i]);
-        if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, red[2 * BN + i]);
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------- A-row gather helpers
 // (plain scalars per row -- a struct holding the per-row arrays was demoted to scratch
@@ -463,270 +198,6 @@ MA_DEV void mma_stage(const bf16* a, const bf16* b, f32x4 (&acc)[BM / 32][BN / 3
       for (int tn = 0; tn < TN; ++tn)
         acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
   }
-}
-
-// Split-K: every K-slice block writes its fp32 partial tile (fragment order, 16 B per lane,
-// fully coalesced) behind the slab's tile-counter header; the LAST block to arrive on a tile
-// sums all slices and runs the epilogue in the same launch (no reducer kernel, no extra launch
-// in the step graph).  Hand-off (cdna_hip_programming.md §6 Guideline 16, R1 form): partials are
-// stored write-through (buffer store, sc1) and drained by every wave before the workgroup
-// barrier, one lane takes a relaxed agent-scope ticket; the last arriver reads the other slices
-// with sc1 loads only -- no L2 write-back fence per block, correct for any XCD placement.  The
-// counter is reset by the last arriver (slabs are zero-initialised at allocation).
-constexpr int SEM_INTS = 1024;   // tile counters at the head of the slab (4 KB)
-
-template <int BM, int BN, int WM = 2>
-MA_DEV void finish(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int M, int N,
-                   int m0, int n0, int bx, int by, int gx, int gy) {
-  constexpr int TM = BM / (16 * WM), TN = BN * WM / 64;
-  if (e.slab) {
-    const int ntiles = gx;
-    const int splits = gy;
-    int* sem = (int*)e.slab;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(e.slab + SEM_INTS), 0, 0x7fffffff,
-                                                      0x00020000);
-    const int tile_bytes = TM * TN * NT * 16;
-    const int mine = (by * ntiles + bx) * tile_bytes + threadIdx.x * 16;
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[tm][tn]), rs,
-                                               mine + (tm * TN + tn) * NT * 16, 0, 16 /*sc1*/);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
-    int* flag = (int*)smem;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(&sem[bx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == splits - 1;
-      if (last) __hip_atomic_store(&sem[bx], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the ticket
-    for (int sp = 0; sp < splits; ++sp) {
-      if (sp == by) continue;
-      const int base = (sp * ntiles + bx) * tile_bytes + threadIdx.x * 16;
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] += __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (tm * TN + tn) * NT * 16, 0,
-                                                           16 /*sc1*/));
-    }
-    __syncthreads();   // flag read by every wave before the epilogue reuses smem
-  }
-  epilogue<BM, BN, WM>(acc, smem, e, M, N, m0, n0);
-}
-
-// ---------------------------------------------------------------- halo-tile 3x3 forward
-// Stride-1 3x3 "same" conv with C % 64 == 0 (the ResNet 3x3 body convs).  The generic loop
-// re-gathers every input pixel once per tap, so each 64-deep stage moves (BM + BN) x 128 B
-// through the CU's vector-memory path; in-kernel stamps put about half of a stage in load
-// issue.  Here a block's output rows are whole image rows (TR rows of one image, or IMG
-// whole images), so the input it needs for one 64-channel chunk is a (TR+2) x (Q+2) halo
-// tile: loaded ONCE into LDS and read by all 9 taps.  A stage (one tap of one channel chunk)
-// then only streams its BN x 64 weight tile; the next chunk's halo is prefetched into
-// registers from tap 0 and written at tap 8.  A fragments are read from the halo at the
-// lane's pixel + the uniform tap offset; the halo is XOR-swizzled by pixel (chunk c of pixel
-// p at slot c ^ (p & 7)), so 16 consecutive pixels read 16 distinct bank groups.
-struct HaloGeom {
-  int TR, IMG;        // tile = IMG images x TR output rows (TR == P when IMG > 1)
-  int HT, HW;         // halo rows (TR + 2) and columns (Q + 2) per image
-  int NHC;            // halo 16-B chunks per 64-channel slice = IMG * HT * HW * 8
-};
-
-template <int BM, int BN, int HMAX>
-struct HaloSmem {
-  static constexpr int HALO = HMAX * 16;              // bytes (max halo chunks)
-  static constexpr int BSTAGE = BN * BK * 2;          // bytes per weight stage
-  static constexpr int MAIN = HALO + 2 * BSTAGE;
-  static constexpr int RED = Smem<BM, BN>::RED_BYTES;
-  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
-};
-
-template <int BM, int BN, int HMAX>
-__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_halo_kernel(const bf16* __restrict__ src,
-                                                            const bf16* __restrict__ wt,
-                                                            ConvGeom g, EpiParams e, HaloGeom hg) {
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int BR = BN / 32;
-  constexpr int HR = (HMAX + NT - 1) / NT;            // halo chunks per thread
-  using SM = HaloSmem<BM, BN, HMAX>;
-  __shared__ __attribute__((aligned(16))) char smem[SM::BYTES];
-  char* halo = smem;
-  bf16* sB = (bf16*)(smem + SM::HALO);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int ntn = (g.Ncols + BN - 1) / BN;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int cc = tid & 7;
-  const int Kelems = g.Kc * 8;
-  const int PQ = g.RP * g.RQ;
-  // tile origin: image n0i, output row p0 (rows of one image, or whole images)
-  const int n0i = m0 / PQ;
-  const int p0 = (m0 - n0i * PQ) / g.RQ;
-
-  // halo slots of this thread: source element offset (channel chunk 0) or -1, LDS byte offset
-  int hsrc[HR], hdst[HR];
-#pragma unroll
-  for (int i = 0; i < HR; ++i) {
-    const int id = tid + i * NT;
-    hsrc[i] = -1;
-    hdst[i] = -1;
-    if (id < hg.NHC) {
-      const int pix = id >> 3, c8 = id & 7;
-      const int per = hg.HT * hg.HW;
-      const int img = pix / per, rem = pix - img * per;
-      const int hr = rem / hg.HW, hc = rem - hr * hg.HW;
-      const int h = p0 + hr - 1, ww = hc - 1, n = n0i + img;
-      if ((unsigned)h < (unsigned)g.SH && (unsigned)ww < (unsigned)g.SW && n * PQ < g.M)
-        hsrc[i] = ((n * g.SH + h) * g.SW + ww) * g.SC + c8 * 8;
-      hdst[i] = (pix * 8 + (c8 ^ (pix & 7))) * 16;
-    }
-  }
-  // lane's A pixel (halo index at tap (0,0)) for each of its TM fragment rows
-  int apix[TM];
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int row = wm * (BM / 2) + tm * 16 + (lane & 15);   // tile-local output pixel
-    const int img = row / (hg.TR * g.RQ), rem = row - img * hg.TR * g.RQ;
-    const int tr = rem / g.RQ, q = rem - tr * g.RQ;
-    apix[tm] = (img * hg.HT + tr) * hg.HW + q;
-  }
-  int boff[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
-    boff[i] = n < g.Ncols ? n * Kelems : -1;
-  }
-  const bf16* zp = g.zero;
-  const int ncb = g.SC >> 6;              // 64-channel chunks
-  const int nsteps = ncb * 9;
-
-  u32x4 rh[HR], rb[BR];
-  auto load_halo = [&](int cb) {
-#pragma unroll
-    for (int i = 0; i < HR; ++i)
-      rh[i] = *(const u32x4*)(hsrc[i] >= 0 ? src + hsrc[i] + cb * 64 : zp);
-  };
-  auto store_halo = [&]() {
-#pragma unroll
-    for (int i = 0; i < HR; ++i)
-      if (hdst[i] >= 0) *(u32x4*)(halo + hdst[i]) = rh[i];
-  };
-  auto load_b = [&](int s) {
-    const int cb = s / 9, tap = s - cb * 9;
-    const int k = tap * g.SC + cb * 64 + cc * 8;
-#pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = *(const u32x4*)(boff[i] >= 0 ? wt + boff[i] + k : zp);
-  };
-  auto store_b = [&](int buf) {
-    bf16* b = sB + buf * (BN * BK);
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *(u32x4*)(b + row * BK + swz(row, cc) * 8) = rb[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  load_halo(0);
-  load_b(0);
-  store_halo();
-  store_b(0);
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int cb = s / 9, tap = s - cb * 9;
-    const bool more = s + 1 < nsteps;
-    const bool next_chunk = cb + 1 < ncb;
-    if (more) load_b(s + 1);
-    if (tap == 0 && next_chunk) load_halo(cb + 1);
-    // MFMAs of this tap: A from the halo at (pixel + tap offset), B from the weight stage
-    const int toff = (tap / 3) * hg.HW + (tap - (tap / 3) * 3);
-    const bf16* b = sB + (s & 1) * (BN * BK);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int p = apix[tm] + toff;
-        fa[tm] = *(const bf16x8*)(halo + (p * 8 + (chunk ^ (p & 7))) * 16);
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int row = wn * (BN / 2) + tn * 16 + (lane & 15);
-        fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
-      }
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
-    }
-    if (tap == 8 && next_chunk) {
-      __syncthreads();                 // every wave is done with this chunk's halo
-      store_halo();
-    }
-    if (more) store_b((s + 1) & 1);
-    __syncthreads();
-  }
-  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, blockIdx.x, 0, gridDim.x, 1);
-}
-
-// Can the halo kernel run this forward conv with a BM x BN tile?  Fills hg.
-static bool halo_geom(const ConvGeom& g, int bm, HaloGeom& hg, int hmax) {
-  if (g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || (g.SC & 63) ||
-      g.SH != g.RP || g.SW != g.RQ)
-    return false;
-  const int PQ = g.RP * g.RQ;
-  if (bm <= PQ) {
-    if (PQ % bm || bm % g.RQ) return false;
-    hg.TR = bm / g.RQ;
-    hg.IMG = 1;
-  } else {
-    if (bm % PQ) return false;
-    hg.TR = g.RP;
-    hg.IMG = bm / PQ;
-  }
-  hg.HT = hg.TR + 2;
-  hg.HW = g.RQ + 2;
-  hg.NHC = hg.IMG * hg.HT * hg.HW * 8;
-  return hg.NHC <= hmax && g.M % bm == 0;
-}
-
-// Opt-in (MERCURY_HALO=1).  Measured on MI355X: 3-7 % faster per scoring-batch 3x3 conv in
-// isolation (bench/kernel_sweep.py), unchanged at the train batch, and the overlapped ResNet-18
-// step 1.9 % SLOWER (1.646 vs 1.616 ms) -- the per-stage time is not set by the gather's load
-// volume (profiles/ab_experiments_r1c.json).
-static int g_halo = -1;
-
-template <int BM, int BN>
-bool launch_halo(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, hipStream_t st) {
-  // largest halo of a BM-row tile over the ResNet CIFAR/ImageNet shapes (16-B chunks):
-  // BM 256: 10 x 34 px; 128: 8 images x 6 x 6 px; 64: 4 images x 6 x 6 px
-  constexpr int HMAX = BM >= 256 ? 2816 : (BM >= 128 ? 2304 : 1152);
-  if (g_halo < 0) {
-    const char* v = getenv("MERCURY_HALO");
-    g_halo = (v && v[0] == '1') ? 1 : 0;
-  }
-  HaloGeom hg;
-  if (!g_halo || !halo_geom(g, BM, hg, HMAX)) return false;
-  e.slab = nullptr;
-  const int grid = (g.M / BM) * ((g.Ncols + BN - 1) / BN);
-  hipLaunchKernelGGL((igemm_halo_kernel<BM, BN, HMAX>), dim3(grid), dim3(NT), 0, st, src, wt, g, e,
-                     hg);
-  return true;
 }
 
 // ---------------------------------------------------------------- register-staged loop
@@ -914,155 +385,6 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   MA_STAMP(3);
 }
 
-// ---------------------------------------------------------------- direct-A loop (pipe 1)
-// The LDS-staged loops move every A byte through LDS twice: a ds_write_b128 (13 cycles per
-// wave-instruction, ~79 B/clk/CU -- MI355X_MICROARCH.md §LDS) and, with 2 x 2 waves, two
-// ds_read_b128s.  Per 64-deep stage of a 256 x 64 tile that is ~840 LDS cycles per block
-// against ~256 MFMA cycles per wave, and two co-resident blocks make the CU's LDS the bound.
-// Here the 4 waves are stacked along M (4 x 1), so no A row is shared between waves: each lane
-// gathers its A fragments straight from global memory in MFMA operand layout (row lane&15,
-// k-group lane>>4 -> chunks lg and 4 + lg of the stage) into registers, double-buffered one
-// stage ahead.  Only the BN x 64 weight tile goes through LDS (written once, read by the 4
-// waves): ~230 LDS cycles per block-stage.
-template <int BM, int BN, bool TRANS>
-MA_DEV void igemm_da_body(const bf16* __restrict__ src, const bf16* __restrict__ wt,
-                          const ConvGeom& g, const EpiParams& e, int ktiles_per_split, char* smem,
-                          int bx, int by, int gx, int gy) {
-  constexpr int TM = BM / 64, TN = BN / 16;
-  constexpr int BR = BN / 32;
-  bf16* sB = (bf16*)smem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ntn = (g.Ncols + BN - 1) / BN;
-  const int mt = bx / ntn, nt = bx - mt * ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int ktiles = (g.Kc + 7) / 8;
-  const int kt0 = by * ktiles_per_split;
-  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
-  const int Kelems = g.Kc * 8;
-  const int cc = tid & 7;
-  const int lg = lane >> 4;
-
-  int abase[TM], ah[TM], aw[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    int off;
-    row_init<TRANS>(g, m0 + w * (BM / 4) + i * 16 + (lane & 15), off, ah[i], aw[i]);
-    abase[i] = row_base<TRANS>(g, off, ah[i], aw[i]);
-    if (off < 0) ah[i] = -(1 << 28);
-  }
-  int boff[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
-    boff[i] = n < g.Ncols ? n * Kelems : -1;
-  }
-  KCursor kc;
-  kc.init(g, kt0);
-  const bf16* zp = g.zero;
-
-  u32x4 rb[BR];
-  auto load = [&](int kt, u32x4 (&ra)[2 * TM]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      int r, s, c8;
-      bool kval;
-      kc.decode(g, kt, kk * 4 + lg, r, s, c8, kval);
-      const int toff = tap_offset<TRANS>(g, r, s) + c8 * 8;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bool ok = kval && tap_ok<TRANS>(g, ah[i], aw[i], r, s);
-        ra[kk * TM + i] = *(const u32x4*)(ok ? src + abase[i] + toff : zp);
-      }
-    }
-    kc.advance(g);
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const bool ok = kt * 8 + cc < g.Kc && boff[i] >= 0;
-      rb[i] = *(const u32x4*)(ok ? wt + boff[i] + (kt * 8 + cc) * 8 : zp);
-    }
-  };
-  auto store_b = [&](int buf) {
-    bf16* b = sB + buf * (BN * BK);
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *(u32x4*)(b + row * BK + swz(row, cc) * 8) = rb[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const u32x4 (&ra)[2 * TM], int buf) {
-    const bf16* b = sB + buf * (BN * BK);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + lg;
-      bf16x8 fb[TN];
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int row = tn * 16 + (lane & 15);
-        fb[tn] = *(const bf16x8*)(b + row * BK + swz(row, chunk) * 8);
-      }
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const bf16x8 fa = __builtin_bit_cast(bf16x8, ra[kk * TM + tm]);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
-      }
-    }
-  };
-
-  if (kt0 < kt1) {
-    u32x4 r0[2 * TM], r1[2 * TM];
-    load(kt0, r0);
-    store_b(0);
-    __syncthreads();
-    // two stages per trip so the two A register sets keep fixed names (no copies)
-    for (int kt = kt0; kt < kt1; kt += 2) {
-      const int buf = (kt - kt0) & 1;
-      if (kt + 1 < kt1) load(kt + 1, r1);
-      mma(r0, buf);
-      if (kt + 1 >= kt1) break;
-      store_b(buf ^ 1);
-      __syncthreads();
-      if (kt + 2 < kt1) load(kt + 2, r0);
-      mma(r1, buf ^ 1);
-      if (kt + 2 < kt1) store_b(buf);
-      __syncthreads();
-    }
-  }
-  finish<BM, BN, 4>(acc, smem, e, g.M, g.Ncols, m0, n0, bx, by, gx, gy);
-}
-
-template <int BM, int BN>
-struct DaSmem {
-  static constexpr int MAIN = 2 * BN * BK * 2;
-  static constexpr int BYTES = MAIN > Smem<BM, BN>::RED_BYTES ? MAIN : Smem<BM, BN>::RED_BYTES;
-};
-
-template <int BM, int BN, bool TRANS>
-__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_da_kernel(const bf16* __restrict__ src,
-                                                          const bf16* __restrict__ wt,
-                                                          ConvGeom g, EpiParams e,
-                                                          int ktiles_per_split) {
-  __shared__ __attribute__((aligned(16))) char smem[DaSmem<BM, BN>::BYTES];
-  igemm_da_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, blockIdx.x, blockIdx.y,
-                               gridDim.x, gridDim.y);
-}
-
-
-// XCD-aware tile order.  The dispatcher places workgroup b on XCD b % 8 and each XCD has its
-// own 4 MB L2, so with tile = blockIdx.x, neighbouring output tiles -- which share the 3x3
-// halo rows of their input and, across N tiles, the same input rows entirely -- land on
-// different L2s.  Renumber so XCD x runs one contiguous range of tiles (bijective on [0, n)).
-MA_DEV int xcd_tile(int b, int n) {
-  const int per = n >> 3, rem = n & 7, x = b & 7;
-  return x * per + min(x, rem) + (b >> 3);
-}
 
 template <int BM, int BN, bool TRANS>
 __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const bf16* __restrict__ src,
@@ -1189,8 +511,6 @@ void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiPa
   if (pipe >= 4)
     hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, (BM + BN > 256 ? 3 : 4), TRANS>), grid, dim3(NT),
                        0, st, src, wt, g, e, per);
-  else if (pipe == 1)
-    hipLaunchKernelGGL((igemm_da_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
   else if (pipe == 3)
     hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, 3, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e,
                        per);
@@ -1220,7 +540,6 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
                        per, *pro);
     return;
   }
-  if (!TRANS && pipe == 0 && gy == 1 && launch_halo<BM, BN>(src, wt, g, e, st)) return;
   launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), pipe, st);
 }
 
@@ -1275,14 +594,16 @@ int igemm_read_stamps(unsigned long long* host, int n) {
 #endif
 }
 
-void igemm_set_halo(int on) { g_halo = on ? 1 : 0; }
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   const size_t mtiles = (g.M + bm - 1) / bm, ntiles = (g.Ncols + bn - 1) / bn;
   return SEM_INTS * 4 + (size_t)splits * mtiles * ntiles * bm * bn * 4;
 }
 
-static const bf16* zero_page() {
+const bf16* conv_zero_page();
+static const bf16* zero_page() { return conv_zero_page(); }
+
+const bf16* conv_zero_page() {
   static const bf16* zp = nullptr;
   if (!zp) {
     void* p = nullptr;

@@ -191,7 +191,7 @@ struct OptArgs {
   long long total;               // end of the swept range (padded flat length for a full step)
   const float* hyper;            // device: [0] lr [1] beta1 [2] beta2 [3] eps [4] wd
   const int64_t* step;           // device step counter (t, already incremented)
-  int algo;                      // 0 adam, 1 sgd(momentum)
+  int algo;                      // 0 adam (L2 in the gradient), 1 sgd(momentum), 2 adamw
   int zero_grad;
   long long start;               // first element of the swept range (4-aligned segment start)
 };

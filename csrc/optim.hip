@@ -83,16 +83,18 @@ __global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
   float4 g = *(const float4*)(a.g + e);
   float4 m = *(const float4*)(a.m + e);
   float pv[4] = {p.x, p.y, p.z, p.w}, gv[4] = {g.x, g.y, g.z, g.w}, mv[4] = {m.x, m.y, m.z, m.w};
-  if (a.algo == 0) {
+  if (a.algo == 0 || a.algo == 2) {
     float4 v = *(const float4*)(a.v + e);
     float vv[4] = {v.x, v.y, v.z, v.w};
     const float t = (float)(*a.step);
     const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
     const float step_size = lr / bc1, rbc2 = rsqrtf(bc2);
+    const bool decoupled = a.algo == 2;   // AdamW: p *= 1 - lr*wd before the Adam update
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gv[k];
-      if (wd != 0.f) gk += wd * pv[k];
+      if (decoupled) pv[k] *= 1.f - lr * wd;
+      else if (wd != 0.f) gk += wd * pv[k];
       mv[k] = b1 * mv[k] + (1.f - b1) * gk;
       vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
       const float denom = sqrtf(vv[k]) * rbc2 + eps;

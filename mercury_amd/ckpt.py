@@ -38,7 +38,8 @@ def _plain(x):
 def checkpoint_dict(trainer, ema=None, sampler=None, net_dataidx_map=None):
     sd = trainer.state_dict()
     out = {'format': 'mercury_amd/1', 'model': sd['model'], 'optimizer': sd['optimizer'],
-           'scheduler': sd.get('scheduler'), 'step': int(sd['step']), 'epoch': int(sd['epoch'])}
+           'scheduler': sd.get('scheduler'), 'step': int(sd['step']), 'epoch': int(sd['epoch']),
+           'epoch_step': int(sd.get('epoch_step', 0))}
     if ema is not None:
         out['ema'] = ema.state_dict()
     if sampler is not None:
@@ -59,6 +60,17 @@ def save_checkpoint(trainer, path, ema=None, sampler=None, net_dataidx_map=None)
     torch.save(checkpoint_dict(trainer, ema, sampler, net_dataidx_map), tmp)
     os.replace(tmp, path)  # atomic: a crash never leaves a torn checkpoint
     return path
+
+
+def resume_path(spec, rank):
+    """Per-rank checkpoint file for ``Config.resume``: a path containing ``{rank}`` is
+    formatted, a directory resolves to its ``ckpt_rank<r>.pt`` (the name ``Trainer`` writes),
+    anything else is used as given (every rank loads the same file)."""
+    if '{rank}' in spec:
+        return spec.format(rank=rank)
+    if os.path.isdir(spec):
+        return os.path.join(spec, 'ckpt_rank%d.pt' % rank)
+    return spec
 
 
 def load_checkpoint(trainer, path, ema=None, sampler=None):

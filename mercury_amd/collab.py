@@ -30,6 +30,8 @@ def make_optimizer(cfg, params, world_size):
     if cfg.optimizer == 'sgd':
         return torch.optim.SGD(params, lr=lr, momentum=cfg.momentum,
                                weight_decay=cfg.weight_decay)
+    if cfg.optimizer == 'adamw':
+        return torch.optim.AdamW(params, lr=lr, weight_decay=cfg.weight_decay)
     return torch.optim.Adam(params, lr=lr, weight_decay=cfg.weight_decay)
 
 
@@ -48,11 +50,18 @@ def make_trainer(cfg, net, optimizer, train_loader, presam_loader, test_loader, 
     from .trainer import Trainer
     if cfg.engine in ('native', 'auto') and torch.device(device).type == 'cuda':
         from .engine import native_supported, NativeTrainer
-        if native_supported(net):
+        from .ops.optim import optimizer_spec
+        try:
+            optimizer_spec(optimizer)
+            why = None if native_supported(net) else 'model not supported by the native engine'
+        except ValueError as e:
+            why = str(e)
+        if why is None:
             return NativeTrainer(net, optimizer, train_loader, presam_loader, test_loader,
                                  device, cfg)
         if cfg.engine == 'native':
-            raise RuntimeError('model not supported by the native engine')
+            raise RuntimeError(why)
+        print('[mercury_amd] eager engine: %s' % why, flush=True)
     return Trainer(net, optimizer, train_loader, presam_loader, test_loader, device, cfg)
 
 

@@ -51,6 +51,12 @@ class Config:
     wire_bf16: bool = False         # bf16 gradient all-reduce
     overlap: bool = True            # scoring of step t+1 overlaps backward/all-reduce of step t
     use_graphs: bool = True
+    comm: str = 'auto'              # native DP all-reduce: 'rccl' (own communicator + comm stream),
+                                    # 'pg' (torch ProcessGroup), 'auto' (rccl on nccl backends)
+    force_buckets: bool = False     # issue the bucket all-reduces even at world size 1
+    # debug / race detection
+    debug: bool = False             # serialise streams, no graphs, sync + check after every phase
+    check_order: bool = False       # device-side stream-order assertions every step
     # logging
     print_every: int = 100
     eval_every: int = 200           # 0 disables evaluation inside train()

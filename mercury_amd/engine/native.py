@@ -67,7 +67,8 @@ class NativeEngine(object):
                  weight_decay=0.0, momentum=0.9, seed=0, alpha=0.5, ema_alpha=0.9,
                  importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
                  sampler='alias', exchange_scores=False, global_table=True, score='loss',
-                 global_ema=False, autotune=None):
+                 global_ema=False, autotune=None, force_buckets=False, comm='auto',
+                 wire_bf16=False, debug=False, check_order=False):
         ops.lib()
         if autotune is not None:
             tune.enable(autotune)
@@ -82,11 +83,27 @@ class NativeEngine(object):
         self.seed = seed
         self.alpha, self.ema_alpha, self.importance = alpha, ema_alpha, importance
         self.world_size = world_size
-        self.use_graphs = use_graphs
+        self.use_graphs = use_graphs and not debug
+        self.debug = debug
+        # data-parallel gradient path.  ``force_buckets`` runs the real bucketed all-reduces
+        # even at W = 1 (the one-GPU box exercises the RCCL code path; AVG over one rank is the
+        # identity, so results are bit-identical to the unbucketed step)
+        self.dp = world_size > 1 or (force_buckets and dist.is_initialized())
         self._avg_op = None
-        if world_size > 1:
-            self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == 'nccl'
-                            else dist.ReduceOp.SUM)
+        self.comm = None                 # own RCCL communicator (csrc/comm.hip)
+        self.s_comm = None               # ... and the stream its bucket all-reduces run on
+        self.wire_bf16 = wire_bf16
+        if self.dp:
+            nccl = dist.get_backend() == 'nccl'
+            self._avg_op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM
+            if comm == 'auto':
+                comm = 'rccl' if nccl else 'pg'
+            if comm == 'rccl':
+                from ..parallel.rccl import RcclComm
+                self.comm = RcclComm()
+                self.s_comm = torch.cuda.Stream(self.device)
+            elif comm != 'pg':
+                raise ValueError("comm must be 'auto', 'rccl' or 'pg'")
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
         self.units = []
         for blk in self.lw.blocks:
@@ -99,28 +116,17 @@ class NativeEngine(object):
         self.ema = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.meters = torch.zeros(8, dtype=torch.float32, device=self.device)
         self.eval_meters = torch.zeros(8, dtype=torch.float32, device=self.device)
-        # optional stream priorities (train high, scoring low).  Off by default: measured on
-        # MI355X it cost 2.4 % (1.897 vs 1.852 ms/step, ResNet-18) -- the extra stream hop
-        # outweighs any dispatch-order gain
-        prio = os.environ.get('MERCURY_STREAM_PRIO', '0') == '1'
-        self.s_score = self._score_stream()
-        self.s_train = torch.cuda.Stream(self.device, priority=-1) if prio else None
-        # Optional side stream for weight gradients.  Off by default: measured on MI355X
-        # (bench/host_overhead.py) a fork/join per conv inside a captured graph is spread
-        # over several hardware queues and each cross-queue edge costs ~15 us, which made
-        # the train graph 1.8 ms vs 1.5 ms single-stream.
-        self.s_wgrad = None
+        # (stream priorities, a CU-masked scoring stream, a weight-gradient side stream and an
+        # early optimizer split were all measured neutral or slower on MI355X and removed:
+        # profiles/ab_experiments_r1c.json)
+        self.s_score = torch.cuda.Stream(self.device)
         self.graphs = None
         self.shard = None
+        self.primed = False              # a scored pool / drawn batch is pending
         self.scoring = True
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
         self.roctx = False               # per-phase roctx ranges around the step's host calls
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
-        # the last blocks' optimizer update on the scoring stream during the earlier blocks'
-        # backward (see _early_block).  Off by default: measured neutral on MI355X (ResNet-18
-        # 1.660 vs 1.655 ms/step) -- in the overlapped step the GPU is throughput-bound, so
-        # moving the update off the tail only moves its HBM traffic under the backward
-        self.early_opt = os.environ.get('MERCURY_EARLY_OPT', '0') == '1'
         # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
         self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
         self.sampler = sampler
@@ -131,29 +137,17 @@ class NativeEngine(object):
         self.table = None
         self.score_exchange = None
         self.global_ema = global_ema
-        if world_size > 1 and (exchange_scores or global_ema):
+        if self.dp and (exchange_scores or global_ema):
             from ..parallel.scores import ScoreExchange
-            self.score_exchange = ScoreExchange(self.P, self.device)
-
-    def _score_stream(self):
-        """The scoring stream.  ``MERCURY_SCORE_CU_FRAC`` (0 < f < 1) restricts it to that
-        fraction of the CUs (HIP CU-masked stream, every k-th CU kept so each XCD loses the
-        same share), so the latency-bound train kernels always find free CUs.  Off by default:
-        measured on MI355X the masked stream made the ResNet-18 step 2.54 ms at f = 0.5, 0.75
-        and 0.875 alike (1.65 ms unmasked) -- a fixed cost of the masked queue, not of the
-        CUs given up."""
-        frac = float(os.environ.get('MERCURY_SCORE_CU_FRAC', '1'))
-        if not 0.0 < frac < 1.0:
-            return torch.cuda.Stream(self.device, priority=0)
-        n = torch.cuda.get_device_properties(self.device).multi_processor_count
-        keep = [int(i * frac) != int((i + 1) * frac) for i in range(n)]   # evenly spread
-        words = [0] * ((n + 31) // 32)
-        for i, k in enumerate(keep):
-            if k:
-                words[i // 32] |= 1 << (i % 32)
-        ptr_ = ops.lib().cu_mask_stream(words)
-        self._cu_mask_words = words
-        return torch.cuda.ExternalStream(ptr_, device=self.device)
+            self.score_exchange = ScoreExchange(self.P, self.device, force=world_size == 1)
+        from .timing import StepTimer
+        self.timer = StepTimer(self.device)   # per-phase device timing (off until enabled)
+        self.wire = None
+        # race detection: device-side stream-order assertions (csrc/runtime.hip);
+        # debug mode also serialises the streams, runs eagerly and syncs after every phase
+        self.check_order = check_order or debug
+        self.order = torch.zeros(16, dtype=torch.int32, device=self.device)
+        self.debug_log = os.environ.get('MERCURY_DEBUG_LOG', '0') == '1'
 
     # ------------------------------------------------------------------ parameters
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
@@ -493,12 +487,11 @@ class NativeEngine(object):
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 
     def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None):
-        """Weight gradient (optionally on a side stream), then the data gradient.  ``bw``:
-        the dgrad epilogue also reduces the BN-backward sums of the unit feeding ``dx``
-        (returns True when it did, so the caller skips bn_bwd's reduce pass)."""
+        """Weight gradient, then the data gradient.  ``bw``: the dgrad epilogue also reduces
+        the BN-backward sums of the unit feeding ``dx`` (returns True when it did, so the
+        caller skips bn_bwd's reduce pass)."""
         sp = m.spec[u.name]
-        if (dx is not None and not u.depthwise and self.s_wgrad is None and self.pair_bwd
-                and sp.K % 8 == 0):
+        if (dx is not None and not u.depthwise and self.pair_bwd and sp.K % 8 == 0):
             if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
                 bw = None
             # dgrad + wgrad of this conv in ONE launch (they share dy and are independent)
@@ -506,15 +499,7 @@ class NativeEngine(object):
                          dplan=m.plan[u.name, 'dgrad'], wplan=m.plan[u.name, 'wgrad'],
                          slab=m.slab, accumulate=accumulate, bw=bw)
             return bw is not None
-        ws = self.s_wgrad
-        if ws is not None:
-            ev = torch.cuda.Event()
-            ev.record()
-            ws.wait_event(ev)
-            with torch.cuda.stream(ws):
-                self._wgrad(m, u, dy, x)
-        else:
-            self._wgrad(m, u, dy, x)
+        self._wgrad(m, u, dy, x)
         if u.depthwise:
             if dx is not None:
                 assert not accumulate
@@ -740,20 +725,19 @@ class NativeEngine(object):
             ops.head_bwd(tm.pooled, tm.dlogits, self._pview(self.lw.fc_w),
                          self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True),
                          tm.buf[last, 'dout'], self.B, tm.final_hw, tm.final_C, self.classes)
-        def join_wgrad():
-            if self.s_wgrad is not None:
-                torch.cuda.current_stream().wait_stream(self.s_wgrad)
-
         cuts = self.bucket_plan()
-        sb = self._early_block()
         cur = [fwd_head]
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
             cur.append(lambda bi=bi: self.backward_block(tm, bi))
-            if bi in cuts or bi == sb:
-                segs.append((cur + [join_wgrad], cuts.get(bi), bi == sb))
+            if bi in cuts:
+                segs.append((cur, cuts[bi]))
                 cur = []
         if cur:
-            segs.append((cur + [join_wgrad], None, False))
+            segs.append((cur, None))
+        if self.check_order:
+            # every train segment ticks o[2]; the comm stream checks it before reducing
+            for fs, _ in segs:
+                fs.append(lambda: self._order(tick=2, at=1))
         return segs
 
     def _block_starts(self):
@@ -763,53 +747,42 @@ class NativeEngine(object):
             starts.append(min(min(s.off for s in (u.w_seg, u.g_seg, u.beta_seg)) for u in us))
         return starts
 
-    def _early_block(self):
-        """First block of the parameter suffix the early optimizer updates (None: off).
-
-        The last blocks hold most of the parameters (ResNet-18: layer4 + fc = 75 %) and finish
-        their backward first.  Once they have (and the scoring forward, which reads every
-        weight, is done), their Adam update and bf16/transposed weight copies run on the
-        scoring stream while the train stream is still in the earlier blocks' backward, so the
-        step's tail only updates the remaining prefix."""
-        if not self.early_opt or len(self.lw.blocks) < 2:
-            return None
-        starts = self._block_starts()
-        total = self.lw.total
-        for bi in range(len(self.lw.blocks) - 1, 0, -1):
-            if (total - starts[bi]) * 2 >= total:
-                return bi
-        return None
-
-    @property
-    def _early_start(self):
-        sb = self._early_block()
-        return None if sb is None else self._block_starts()[sb]
-
     def bucket_plan(self):
         """{block index: (flat_start, flat_end)} -- a bucket closes after that block's backward
-        (always at the early optimizer's block, so its parameters' buckets end there)."""
-        if self.world_size == 1:
+        once it holds >= ``bucket_bytes`` of gradient (and always at block 0).  Parameters are
+        laid out in forward order, so backward finishes them from the end of the flat buffer."""
+        if not self.dp:
             return {}
         starts = self._block_starts()
-        sb = self._early_block()
         cuts = {}
         end = self.lw.total
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
-            if bi == 0 or bi == sb or (end - starts[bi]) * 4 >= self.bucket_bytes:
+            if bi == 0 or (end - starts[bi]) * 4 >= self.bucket_bytes:
                 cuts[bi] = (0 if bi == 0 else starts[bi], end)
                 end = starts[bi]
         return cuts
 
-    def early_tail(self):
-        """Score-stream part of the optimizer step: the parameter suffix (``_early_block``)."""
-        self.opt.step(self.ctrl[2:3], start=self._early_start)
-
     def tail(self):
+        if self.check_order:
+            # the tail consumes the scoring stream's draw and (DP) every reduced bucket: both
+            # must have finished this step -- o[0] / o[1] == steps completed + 1
+            self._order(slot=0, ref=3, mult=1, add=1, at=3)
+            if self.dp:
+                self._order(slot=1, ref=3, mult=1, add=1, at=4)
+            self._order(tick=3, at=5)
         (self.bn_table if self.scoring else self.bn_table_uniform).launch(0.1)
-        es = self._early_start
-        self.opt.step(self.ctrl[2:3], end=es)     # es None: the whole buffer
+        self.opt.step(self.ctrl[2:3])
         self._mlp_refresh()
         self.gather_batch()
+
+    def _order(self, slot=-1, ref=0, mult=0, add=0, ge=False, tick=-1, at=0):
+        ops.lib().order_check(ops.ptr(self.order), slot, ref, mult, add, int(ge), tick, at,
+                              ops.stream_ptr())
+
+    def order_violations(self):
+        """(count, first violation record) of the stream-order checks (``check_order``)."""
+        o = self.order.tolist()
+        return o[4], dict(slot=o[8], seen=o[9], want=o[10], at=o[11]) if o[4] else None
 
     # ------------------------------------------------------------------ graphs
     def _capture(self, fn, stream):
@@ -825,12 +798,9 @@ class NativeEngine(object):
         self.graphs = {
             'score': self._capture(self.score_forward if self._split_score else self.score_branch,
                                    cap),
-            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b, e)
-                      for fs, b, e in segs],
+            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b) for fs, b in segs],
             'tail': self._capture(self.tail, cap),
         }
-        if self._early_start is not None:
-            self.graphs['early'] = self._capture(self.early_tail, cap)
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
         self._graph_scoring = self.scoring
@@ -844,80 +814,139 @@ class NativeEngine(object):
             self._score_stream_work(None)
         s0.wait_stream(self.s_score)
         self.gather_batch()
+        self.primed = True
 
     def step(self):
-        """One importance-sampled DP step (all async; nothing syncs the host)."""
-        caller = torch.cuda.current_stream(self.device)
-        if self.s_train is None:
-            return self._step(caller)
-        # the train chain is the critical path: run it on the high-priority stream so its
-        # small B=32 kernels are dispatched ahead of the pool-scoring kernels' blocks
-        self.s_train.wait_stream(caller)
-        with torch.cuda.stream(self.s_train):
-            self._step(self.s_train)
-        caller.wait_stream(self.s_train)
+        """One importance-sampled DP step (all async; nothing syncs the host unless ``debug``).
 
-    def _step(self, s0):
-        ev_start = torch.cuda.Event()
-        ev_start.record(s0)
-        self.s_score.wait_event(ev_start)
+        Streams: the scoring stream (next pool) and the train stream (this batch) start
+        together; after each bucket segment of the backward the comm stream all-reduces that
+        bucket (RCCL, AVG) while later segments and the scoring keep computing; the tail on the
+        train stream waits for the scoring stream and the last bucket."""
+        s0 = torch.cuda.current_stream(self.device)
         graphs = self.graphs if self.use_graphs else None
         if graphs and self._graph_scoring != self.scoring:
             raise RuntimeError('scoring was toggled after build_graphs(); rebuild the graphs')
+        T = self.timer
+        T.begin_step()
+        T.mark('start', s0)
         rx = self.roctx
+        debug = self.debug
         if rx:
             prof.push('score')
-        with torch.cuda.stream(self.s_score):
-            self._score_stream_work(graphs)
+        if debug:
+            # serialised: scoring first, on the train stream, checked before training starts
+            self._score_stream_work(None)
+            if self.check_order:
+                self._order(tick=0, at=0)
+            self._debug_sync('score')
+        else:
+            ev_start = torch.cuda.Event()
+            ev_start.record(s0)
+            self.s_score.wait_event(ev_start)
+            with torch.cuda.stream(self.s_score):
+                T.mark('score0', self.s_score)
+                self._score_stream_work(graphs)
+                if self.check_order:
+                    self._order(tick=0, at=0)
+                T.mark('score1', self.s_score)
         if rx:
             prof.pop()
             prof.push('train')
         works = []
         segs = graphs['train'] if graphs else self.train_segments()
-        early = False
-        for g, bucket, cut in segs:
+        nb = 0
+        for si, (g, bucket) in enumerate(segs):
             if graphs:
                 g.replay()
             else:
                 for f in g:
                     f()
-            if bucket is not None and self.world_size > 1:
-                s, e = bucket
-                works.append([dist.all_reduce(self.opt.g[s:e], op=self._avg_op,
-                                              async_op=True), s, e, False])
-            if cut:
-                # the parameter suffix is final on this rank once its buckets are reduced:
-                # update it on the scoring stream, behind the scoring forward that reads it
-                early = True
-                ev_bwd = torch.cuda.Event()
-                ev_bwd.record(s0)
-                with torch.cuda.stream(self.s_score):
-                    self.s_score.wait_event(ev_bwd)
-                    for wk in works:
-                        self._finish_work(wk)
-                    if graphs:
-                        graphs['early'].replay()
-                    else:
-                        self.early_tail()
-        ev_score = torch.cuda.Event()
-        ev_score.record(self.s_score)
+            if debug:
+                self._debug_sync('train segment %d' % si)
+            if bucket is not None and self.dp:
+                works.append(self._reduce_bucket(s0, bucket, nb, si))
+                nb += 1
+        T.mark('train1', s0)
         if rx:
             prof.pop()
             prof.push('allreduce')
+        if self.s_comm is not None and nb:
+            if self.check_order:
+                with torch.cuda.stream(self.s_comm):
+                    self._order(tick=1, at=2)
+            ev_c = torch.cuda.Event()
+            ev_c.record(self.s_comm)
+            s0.wait_event(ev_c)
         for wk in works:
-            self._finish_work(wk)
-        if not early and self._early_start is not None:
-            raise RuntimeError('early optimizer cut not reached')
-        s0.wait_event(ev_score)
+            if wk is not None:
+                self._finish_work(wk)
+                if self.check_order and wk is works[-1]:
+                    self._order(tick=1, at=2)
+        if debug and self.dp:
+            self._debug_sync('allreduce')
+        if not debug:
+            ev_score = torch.cuda.Event()
+            ev_score.record(self.s_score)
+            s0.wait_event(ev_score)
         if rx:
             prof.pop()
             prof.push('tail')
+        T.mark('tail0', s0)
         if graphs:
             graphs['tail'].replay()
         else:
             self.tail()
+        T.mark('end', s0)
+        if debug:
+            self._debug_sync('tail')
         if rx:
             prof.pop()
+
+    def _reduce_bucket(self, s0, bucket, i, si):
+        """Issue bucket ``i``'s gradient all-reduce behind train segment ``si``."""
+        s, e = bucket
+        g = self.opt.g[s:e]
+        if self.s_comm is None:          # torch ProcessGroup (gloo / CPU tests)
+            return [dist.all_reduce(g, op=self._avg_op, async_op=True), s, e, False]
+        ev = torch.cuda.Event()
+        ev.record(s0)
+        self.s_comm.wait_event(ev)
+        with torch.cuda.stream(self.s_comm):
+            if self.check_order:
+                # the bucket's gradients are final: train segment si has ticked this step
+                self._order(slot=2, ref=3, mult=self._nseg, add=si + 1, ge=True, at=6)
+            self.timer.bucket(i, 0, self.s_comm)
+            if self.wire_bf16:
+                # bf16 on the wire: half the bytes over xGMI; the sum is rounded once per hop
+                if self.wire is None:
+                    self.wire = torch.empty(self.lw.total, dtype=torch.bfloat16,
+                                            device=self.device)
+                w = self.wire[s:e]
+                w.copy_(g)
+                self.comm.allreduce(w, avg=True)
+                g.copy_(w)
+            else:
+                self.comm.allreduce(g, avg=True)
+            self.timer.bucket(i, 1, self.s_comm)
+        return None
+
+    @property
+    def _nseg(self):
+        return len(self.bucket_plan()) + (0 if 0 in self.bucket_plan() else 1)
+
+    def _debug_sync(self, what):
+        """Debug mode: drain the device after every phase so a fault names its phase."""
+        try:
+            torch.cuda.synchronize(self.device)
+        except RuntimeError as e:
+            raise RuntimeError('device error after %s: %s' % (what, e)) from e
+        if self.check_order:
+            n, first = self.order_violations()
+            if n:
+                raise RuntimeError('stream-order violation after %s: %s' % (what, first))
+        if self.debug_log:
+            print('[mercury_amd debug] step phase done: %s' % what, flush=True)
 
     def _finish_work(self, wk):
         """Make the current stream wait for a bucket all-reduce (once per stream is harmless;
@@ -1001,6 +1030,7 @@ class NativeTrainer(Trainer):
         self.world_size = dist.get_world_size() if dist.is_initialized() else 1
         self.com_tensor = torch.ones(1)
         self.epoch, self.step, self.writer, self.scheduler = 0, 1, None, None
+        self.epoch_step = 0
         self.next_batch_iter = None
         self.computed_samples = {'index': [], 'prob': []}
         self.should_compute_importance = True
@@ -1013,18 +1043,19 @@ class NativeTrainer(Trainer):
         # the engine's fused kernel performs the optimizer step; tell the LR scheduler so it
         # does not warn that optimizer.step() was never called
         optimizer._opt_called = True
-        g = optimizer.param_groups[0]
-        algo = 'adam' if isinstance(optimizer, torch.optim.Adam) else 'sgd'
+        osp = ops.optimizer_spec(optimizer)       # raises on anything the kernel cannot run
         x, y = _dataset_arrays(presam_loader)
         self.engine = NativeEngine(
             net, self.device, self.batch_size, cfg.presample_batches, image_hw=x.shape[1:3],
-            optimizer=algo, lr=g['lr'], betas=g.get('betas', (0.9, 0.999)),
-            eps=g.get('eps', 1e-8), weight_decay=g.get('weight_decay', 0.0),
-            momentum=g.get('momentum', 0.9), seed=cfg.seed * 1000 + self.rank, alpha=cfg.alpha,
+            optimizer=osp['algo'], lr=osp['lr'], betas=osp['betas'], eps=osp['eps'],
+            weight_decay=osp['weight_decay'], momentum=osp['momentum'],
+            seed=cfg.seed * 1000 + self.rank, alpha=cfg.alpha,
             ema_alpha=cfg.ema_alpha, importance=cfg.importance, world_size=self.world_size,
             bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs,
             sampler=cfg.sampler, exchange_scores=cfg.exchange_scores,
-            score=cfg.score, global_ema=cfg.global_ema)
+            score=cfg.score, global_ema=cfg.global_ema, wire_bf16=cfg.wire_bf16,
+            comm=cfg.comm, debug=cfg.debug, check_order=cfg.check_order,
+            force_buckets=cfg.force_buckets)
         self.engine.set_shard(x, y)
         self.engine.roctx = cfg.roctx
         from ..utils.profiling import StepWindow
@@ -1047,9 +1078,14 @@ class NativeTrainer(Trainer):
         pass  # bucketed inside engine.step()
 
     def update_samples(self, ema_loss=None, alpha=None):
-        """API-compatible scoring call: returns (weights, data NCHW, label, index, pool_mean)."""
+        """API-compatible scoring call: returns (weights, data NCHW, label, index, pool_mean).
+
+        The native step scores the next pool inside ``step()``, so this is a read-only view of
+        the pending (already scored and drawn) batch; only before the first step does it score
+        a pool (``prime``)."""
         e = self.engine
-        e.prime()
+        if not e.primed:
+            e.prime()
         sm = e.score_mode
         idx = e.idx.long()
         data = sm.input[idx][..., :3].permute(0, 3, 1, 2).float()
@@ -1071,13 +1107,18 @@ class NativeTrainer(Trainer):
         e.meters[:3].zero_()
         self._sync_lr()
         e.prime()
-        if e.use_graphs and e.graphs is None:
-            e.step()                       # one eager step warms every kernel, then capture
-            self.step += 1
-            e.build_graphs()
         t0 = time.perf_counter()
-        for _ in range(self.steps_per_epoch):
-            e.step()
+        pe = self.cfg.print_every
+        for _ in range(max(0, self.steps_per_epoch - self.epoch_step)):
+            # device-phase timing for the steps that are printed (events cost host time)
+            e.timer.on = bool(pe) and self.step % pe == 0 and self.rank == 0
+            if e.use_graphs and e.graphs is None:
+                # the first step runs eagerly (warms every kernel), then the step is captured;
+                # it is a real training step and counts like every other one
+                e.step()
+                e.build_graphs()
+            else:
+                e.step()
             self._health()
             if self.cfg.print_every and self.step % self.cfg.print_every == 0:
                 self._log(t0)
@@ -1085,7 +1126,7 @@ class NativeTrainer(Trainer):
             if self.cfg.eval_every and self.step % self.cfg.eval_every == 0 and (
                     self.rank == 0 or self.cfg.eval_all_ranks):
                 self._eval_log()
-            self.step += 1
+            self._advance()
             if self._stop():
                 break
         m = e.read_meters()
@@ -1099,11 +1140,25 @@ class NativeTrainer(Trainer):
             return
         m = self.engine.read_meters()
         cnt = max(m['count'], 1)
+        ph = self.engine.timer.collect()
+        dev = ''
+        if ph:
+            # reference C27 fields (`pytorch_collab.py:129-178`), from device events: step, IS
+            # (scoring stream), ff+bp, sync (all-reduce, and the part not hidden), opt (tail)
+            dev = (', device ms: step {step:.3f} (critical path {critical:.3f}), IS {score:.3f}, '
+                   'ff+bp {train:.3f}, sync {comm:.3f} (exposed {exp:.3f}), wait {wait:.3f}, '
+                   'opt+tail {tail:.3f}, IS share {share:.1f}%').format(
+                       exp=ph.get('comm_exposed', 0.0), share=100.0 * ph['score'] / max(
+                           ph['score'] + ph['train'], 1e-9), **ph)
         print('step:{}, running train loss: {:.6f}, running train acc: {:.2f}%, '
-              'presam_ema_loss: {:.6f}, pool_mean: {:.4f}, {:.3f} ms/step'.format(
+              'presam_ema_loss: {:.6f}, pool_mean: {:.4f}, {:.3f} ms/step{}'.format(
                   self.step, m['loss_sum'] / cnt, 100 * m['correct'] / cnt, m['ema'],
-                  m['pool_mean'], (time.perf_counter() - t0) * 1e3 / self.cfg.print_every),
+                  m['pool_mean'], (time.perf_counter() - t0) * 1e3 / self.cfg.print_every, dev),
               flush=True)
+        if self.engine.check_order:
+            n, first = self.engine.order_violations()
+            if n:
+                raise RuntimeError('stream-order violation (%d): %s' % (n, first))
 
     def _eval_log(self):
         train_loss, train_acc, test_loss, test_acc = self.evaluate()
@@ -1140,7 +1195,7 @@ class NativeTrainer(Trainer):
         t = int(e.ctrl[2].item())
         for i, s in enumerate(e.lw.segs):
             st = {'step': torch.tensor(float(t)), 'exp_avg': e._to_torch_layout(s, e.opt.m).cpu()}
-            if e.opt.algo == 0:
+            if e.opt.algo in (0, 2):
                 st['exp_avg_sq'] = e._to_torch_layout(s, e.opt.v).cpu()
             else:
                 st = {'momentum_buffer': st['exp_avg']}
@@ -1149,7 +1204,7 @@ class NativeTrainer(Trainer):
         return {'model': {k: v.detach().cpu() for k, v in self.net.state_dict().items()},
                 'optimizer': ost,
                 'scheduler': self.scheduler.state_dict() if self.scheduler else None,
-                'step': self.step, 'epoch': self.epoch,
+                'step': self.step, 'epoch': self.epoch, 'epoch_step': self.epoch_step,
                 'engine': self._engine_state()}
 
     def _engine_state(self):
@@ -1170,7 +1225,7 @@ class NativeTrainer(Trainer):
             if i in st:
                 if 'exp_avg' in st[i]:
                     e._from_torch_layout(s, e.opt.m, st[i]['exp_avg'])
-                if 'exp_avg_sq' in st[i] and e.opt.algo == 0:
+                if 'exp_avg_sq' in st[i] and e.opt.algo in (0, 2):
                     e._from_torch_layout(s, e.opt.v, st[i]['exp_avg_sq'])
                 if 'momentum_buffer' in st[i]:
                     e._from_torch_layout(s, e.opt.m, st[i]['momentum_buffer'])
@@ -1178,12 +1233,22 @@ class NativeTrainer(Trainer):
             self.scheduler.load_state_dict(sd['scheduler'])
         self.optimizer.param_groups[0]['lr'] = sd['optimizer']['param_groups'][0]['lr']
         self.step, self.epoch = sd['step'], sd['epoch']
+        self.epoch_step = int(sd.get('epoch_step', 0))
         if 'engine' in sd:
-            e.ctrl.copy_(sd['engine']['ctrl'].to(e.device))
-            e.ema.copy_(sd['engine']['ema'].to(e.device))
-            if e.table is not None and 'importance' in sd['engine']:
-                e.table.importance.copy_(sd['engine']['importance'].to(e.device))
-                e.table.group.copy_(sd['engine']['group_indicator'].to(e.device, torch.int32))
+            es = sd['engine']
+            if e.table is not None and 'importance' in es:
+                n = es['importance'].numel()
+                if n != e.table.importance.numel():
+                    raise ValueError(
+                        'checkpoint importance table has %d entries but this rank\'s shard has '
+                        '%d: resume each rank from its own file (Config.resume = a directory of '
+                        'ckpt_rank<r>.pt files, or a path with {rank})'
+                        % (n, e.table.importance.numel()))
+            e.ctrl.copy_(es['ctrl'].to(e.device))
+            e.ema.copy_(es['ema'].to(e.device))
+            if e.table is not None and 'importance' in es:
+                e.table.importance.copy_(es['importance'].to(e.device))
+                e.table.group.copy_(es['group_indicator'].to(e.device, torch.int32))
 
 
 # ---------------------------------------------------------------------- smoke

@@ -3,9 +3,9 @@
 Each wrapper validates shapes / dtypes / devices / contiguity and then calls the
 raw launcher in ``mercury_amd._C`` on the *current* HIP stream (so every call
 is capturable into a HIP graph).  There is no silent fallback: on a machine
-with a GPU, a missing or stale extension raises; the pure-torch reference
-implementations live in ``mercury_amd.ops.reference`` and are used only by
-tests and by the CPU engine.
+with a GPU, a missing or stale extension raises.  The plain-PyTorch fp32
+oracles the kernels are tested against live in ``tests/refutil.py`` and in each
+GPU test; the CPU path is the eager ``mercury_amd.trainer.Trainer``.
 
 Layout conventions: activations NHWC bf16 with channels padded to a multiple
 of 8; conv weights bf16 [K][R][S][Cpad] (forward) and [C][R][S][K] (dgrad);
@@ -81,12 +81,12 @@ from .bn import bn_apply, bn_bwd, BnRunTable  # noqa: E402
 from .head import head_fwd, head_bwd  # noqa: E402
 from .importance import pool_build, is_sample, gather  # noqa: E402
 from .table import ImportanceTable  # noqa: E402
-from .optim import FlatOptimizer  # noqa: E402
+from .optim import FlatOptimizer, optimizer_spec  # noqa: E402
 from .misc import (quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad,  # noqa: E402
                    nchw_to_nhwc8)
 
 __all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
            'pack_conv_weight', 'to_nhwc', 'from_nhwc', 'bn_apply', 'bn_bwd', 'BnRunTable',
            'head_fwd', 'head_bwd', 'pool_build', 'is_sample', 'gather', 'ImportanceTable',
-           'FlatOptimizer', 'quantize', 'pool2d_fwd', 'maxpool2d_bwd',
+           'FlatOptimizer', 'optimizer_spec', 'quantize', 'pool2d_fwd', 'maxpool2d_bwd',
            'dwconv_fwd', 'dwconv_dgrad', 'dwconv_wgrad', 'nchw_to_nhwc8']

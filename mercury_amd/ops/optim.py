@@ -13,6 +13,49 @@ import torch
 
 from . import lib, ptr, stream_ptr
 
+# kernel algorithm codes (csrc/kernels.h OptArgs.algo)
+ALGOS = {'adam': 0, 'sgd': 1, 'adamw': 2}
+
+
+def optimizer_spec(optimizer):
+    """Map a ``torch.optim`` instance onto the fused kernel, or raise ``ValueError``.
+
+    Only exact types are accepted (``AdamW`` subclasses ``Adam`` in torch 2.x, so an
+    ``isinstance`` test would silently run it with coupled L2 decay), with one param group and
+    no option the kernel does not implement.  Returns the ``FlatOptimizer`` keyword arguments."""
+    groups = optimizer.param_groups
+    if len(groups) != 1:
+        raise ValueError('native optimizer: exactly one param group supported, got %d'
+                         % len(groups))
+    g = groups[0]
+    t = type(optimizer)
+    if g.get('maximize', False):
+        raise ValueError('native optimizer: maximize=True is not supported')
+    if g.get('differentiable', False):
+        raise ValueError('native optimizer: differentiable=True is not supported')
+    if t is torch.optim.Adam or t is torch.optim.AdamW:
+        if g.get('amsgrad', False):
+            raise ValueError('native optimizer: amsgrad=True is not supported')
+        algo = 'adamw' if (t is torch.optim.AdamW or g.get('decoupled_weight_decay', False)) \
+            else 'adam'
+        lr = g['lr']
+        if torch.is_tensor(lr):
+            lr = float(lr)
+        return dict(algo=algo, lr=lr, betas=tuple(g['betas']), eps=g['eps'],
+                    weight_decay=g['weight_decay'], momentum=0.9)
+    if t is torch.optim.SGD:
+        if g.get('nesterov', False):
+            raise ValueError('native optimizer: nesterov=True is not supported')
+        if g.get('dampening', 0) != 0:
+            raise ValueError('native optimizer: dampening != 0 is not supported')
+        if g.get('momentum', 0) == 0:
+            raise ValueError('native optimizer: SGD without momentum is not supported '
+                             '(the kernel keeps a momentum buffer)')
+        return dict(algo='sgd', lr=g['lr'], betas=(0.9, 0.999), eps=1e-8,
+                    weight_decay=g['weight_decay'], momentum=g['momentum'])
+    raise ValueError('native optimizer: %s is not supported (Adam, AdamW, SGD with momentum)'
+                     % t.__name__)
+
 
 class FlatOptimizer(object):
 
@@ -24,9 +67,12 @@ class FlatOptimizer(object):
         self.p = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.g = torch.zeros_like(self.p)
         self.m = torch.zeros_like(self.p)
-        self.v = torch.zeros_like(self.p) if algo == 'adam' else torch.zeros(4, device=device)
-        self.algo = 0 if algo == 'adam' else 1
-        b1 = betas[0] if algo == 'adam' else momentum
+        if algo not in ALGOS:
+            raise ValueError('FlatOptimizer algo must be one of %s, got %r' % (sorted(ALGOS), algo))
+        adam = algo in ('adam', 'adamw')
+        self.v = torch.zeros_like(self.p) if adam else torch.zeros(4, device=device)
+        self.algo = ALGOS[algo]
+        b1 = betas[0] if adam else momentum
         self.hyper = torch.tensor([lr, b1, betas[1], eps, weight_decay, 0, 0, 0],
                                   dtype=torch.float32, device=device)
         rows = []

@@ -49,10 +49,11 @@ def default_backend(device):
     return 'nccl' if torch.device(device).type == 'cuda' else 'gloo'
 
 
-def init_from_env(device=None, backend=None, timeout_s=DEFAULT_TIMEOUT_S):
+def init_from_env(device=None, backend=None, timeout_s=DEFAULT_TIMEOUT_S, force=False):
     """Initialise from torchrun env vars; returns ``(rank, world_size, device)``.
 
-    Works without any env (single process) -- then no process group is made."""
+    Works without any env (single process) -- then no process group is made unless ``force``
+    (a one-rank group, so the collective code paths run on one GPU)."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     rk = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', str(rk)))
@@ -62,7 +63,7 @@ def init_from_env(device=None, backend=None, timeout_s=DEFAULT_TIMEOUT_S):
     if device.type == 'cuda':
         torch.cuda.set_device(local)
         device = torch.device('cuda', local)
-    if ws > 1 and not is_initialized():
+    if (ws > 1 or force) and not is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29500')
         kw = {}

@@ -82,7 +82,7 @@ class RcclComm(object):
         if t.dtype != torch.float32:
             raise TypeError('ring_allreduce: fp32 only')
         self._code(t)
-        need = (t.numel() + self.size - 1) // self.size + 1
+        need = (t.numel() + self.size - 1) // self.size + 8   # 16-B aligned chunks (comm.hip)
         if self._work is None or self._work.numel() < need or self._work.device != t.device:
             self._work = torch.empty(need, dtype=torch.float32, device=t.device)
         lib().comm_ring_allreduce(self.handle, ptr(t), t.numel(), ptr(self._work), int(avg),

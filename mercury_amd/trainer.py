@@ -56,6 +56,7 @@ class Trainer(object):
         self.com_tensor = torch.ones(1)
         self.epoch = 0
         self.step = 1
+        self.epoch_step = 0       # steps completed in the current epoch (mid-epoch resume)
         self.writer = None
         self.next_batch_iter = None
         self.computed_samples = {'index': [], 'prob': []}
@@ -214,15 +215,27 @@ class Trainer(object):
         presam_ema_loss = EMAverage(self.cfg.ema_alpha)
         runing_train_acc = Accuracy()
         probs, i_data, i_label, _, _ = self.update_samples(presam_ema_loss)
-        for _ in range(self.steps_per_epoch):
+        for _ in range(max(0, self.steps_per_epoch - self.epoch_step)):
             t0 = time.perf_counter()
             (probs, i_data, i_label, _, _), _ = self.train_step(
                 probs, i_data, i_label, presam_ema_loss, running_train_loss, runing_train_acc)
             self._after_step(running_train_loss, runing_train_acc, presam_ema_loss, t0)
-            self.step += 1
+            self._advance()
             if self._stop():
                 break
         return running_train_loss, runing_train_acc, presam_ema_loss
+
+    def _advance(self):
+        """Count a finished step, then checkpoint on cadence: the saved state is exactly
+        "``epoch_step`` steps of epoch ``epoch`` done, ``step`` is the next step", so a resume
+        finishes the partial epoch before the LR scheduler advances (see ``fit``)."""
+        self.step += 1
+        self.epoch_step += 1
+        cfg = self.cfg
+        if cfg.checkpoint_dir and cfg.checkpoint_every and \
+                (self.step - 1) % cfg.checkpoint_every == 0:
+            from .ckpt import save_checkpoint
+            save_checkpoint(self, os.path.join(cfg.checkpoint_dir, 'ckpt_rank%d.pt' % self.rank))
 
     def _stop(self):
         return self.step * self.world_size > self.cfg.max_samples
@@ -244,9 +257,6 @@ class Trainer(object):
                 if cfg.on_divergence == 'raise':
                     raise ReplicaDivergence(msg)
                 print('[mercury_amd] WARNING ' + msg, flush=True)
-        if cfg.checkpoint_dir and cfg.checkpoint_every and self.step % cfg.checkpoint_every == 0:
-            from .ckpt import save_checkpoint
-            save_checkpoint(self, os.path.join(cfg.checkpoint_dir, 'ckpt_rank%d.pt' % self.rank))
 
     def _after_step(self, running_loss, running_acc, ema, t0):
         cfg = self.cfg
@@ -275,15 +285,26 @@ class Trainer(object):
                 self.world_size))
         self.scheduler = CosineAnnealingLR(self.optimizer, epochs)
         if self.cfg.resume:
-            from .ckpt import load_checkpoint
-            load_checkpoint(self, self.cfg.resume)
+            from .ckpt import load_checkpoint, resume_path
+            load_checkpoint(self, resume_path(self.cfg.resume, self.rank))
         self.average_model()
+        stopped = False
+        if self.epoch_step > 0:
+            # resumed inside epoch ``self.epoch``: finish it at that epoch's LR, then advance
+            if self.epoch_step < self.steps_per_epoch:
+                self.train()
+            stopped = self._stop()
+            if self.epoch_step >= self.steps_per_epoch:
+                self.scheduler.step()
         for epoch in range(self.epoch + 1, epochs + 1):
-            self.epoch = epoch
-            self.train()
-            self.scheduler.step()
-            if self._stop():
+            if stopped:
                 break
+            self.epoch = epoch
+            self.epoch_step = 0
+            self.train()
+            if self.epoch_step >= self.steps_per_epoch:
+                self.scheduler.step()
+            stopped = self._stop()
         self.profile_window.close()
         if self.writer is not None:
             self.writer.close()
@@ -313,7 +334,7 @@ class Trainer(object):
         return {'model': self.net.state_dict(),
                 'optimizer': self.optimizer.state_dict(),
                 'scheduler': self.scheduler.state_dict() if self.scheduler else None,
-                'step': self.step, 'epoch': self.epoch}
+                'step': self.step, 'epoch': self.epoch, 'epoch_step': self.epoch_step}
 
     def load_state_dict(self, sd):
         self.net.load_state_dict(sd['model'])
@@ -322,3 +343,4 @@ class Trainer(object):
             self.scheduler.load_state_dict(sd['scheduler'])
         self.step = sd['step']
         self.epoch = sd['epoch']
+        self.epoch_step = int(sd.get('epoch_step', 0))

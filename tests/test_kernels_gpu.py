@@ -754,25 +754,6 @@ def test_conv_fwd_bn_apply_prologue(case, mode):
         close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize('case,plan,gimgs', [
-    ((2, 32, 32, 64, 64, 3, 3, 1, 1), (256, 64, 1), 0),
-    ((2, 32, 32, 64, 64, 3, 3, 1, 1), (128, 64, 1), 1),
-    ((4, 16, 16, 128, 128, 3, 3, 1, 1), (128, 128, 1), 2),
-    ((8, 8, 8, 256, 256, 3, 3, 1, 1), (128, 128, 1), 4),      # 2 images per tile
-    ((16, 4, 4, 512, 512, 3, 3, 1, 1), (128, 128, 1), 8),     # 8 images per tile
-    ((16, 4, 4, 512, 512, 3, 3, 1, 1), (64, 128, 1), 0),      # 4 images per tile
-    ((4, 8, 8, 192, 64, 3, 3, 1, 1), (64, 64, 1), 0)])        # 3 channel slices of 64
-def test_conv_fwd_halo_tile(case, plan, gimgs):
-    """The halo-tile 3x3 forward (every 64-channel input slice loaded once per tile, read by
-    all 9 taps) against torch, incl. ghost-group BN statistics (the kernel is opt-in)."""
-    ops = _ops()
-    ops.lib().igemm_set_halo(1)
-    try:
-        _halo_case(ops, case, plan, gimgs)
-    finally:
-        ops.lib().igemm_set_halo(0)
-
-
 def _halo_case(ops, case, plan, gimgs):
     from mercury_amd.ops.conv import ConvSpec
     N, H, W, C, K, R, S, st, pd = case

@@ -186,7 +186,7 @@ def test_vgg_speech_native_matches_torch():
     tm.input.copy_(ops.to_nhwc(x))
     tm.label.copy_(y.int())
     eng.isw.copy_(w)
-    for fs, _, _ in eng.train_segments():
+    for fs, _ in eng.train_segments():
         for f in fs:
             f()
     torch.cuda.synchronize()
