@@ -100,7 +100,7 @@ class NativeEngine(object):
                 comm = 'rccl' if nccl else 'pg'
             if comm == 'rccl':
                 from ..parallel.rccl import RcclComm
-                self.comm = RcclComm()
+                self.comm = RcclComm.shared()
                 self.s_comm = torch.cuda.Stream(self.device)
             elif comm != 'pg':
                 raise ValueError("comm must be 'auto', 'rccl' or 'pg'")

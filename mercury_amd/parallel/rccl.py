@@ -15,6 +15,13 @@ block the host:
 This is independent of ``ProcessGroupNCCL``, so the engine can place a
 collective on any stream it owns (e.g. the score stream) without an extra
 ProcessGroup stream edge.
+
+Lifetime is explicit.  ``RcclComm.shared(group)`` hands out one communicator per
+torch.distributed group per process (engines share it); ``close()`` synchronises
+the device and destroys it.  Nothing is destroyed from ``__del__``: a garbage
+collection pass can run at any point (inside another engine's construction, with
+collectives in flight on a stream), and ncclCommDestroy there aborted the process
+on the GPU box -- an un-closed communicator is released at process exit.
 """
 from __future__ import annotations
 
@@ -28,6 +35,18 @@ _DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3
 
 
 class RcclComm(object):
+
+    _shared = {}
+
+    @classmethod
+    def shared(cls, group=None):
+        init = dist.is_initialized()
+        key = (id(group) if group is not None else None,
+               dist.get_rank(group) if init else 0, dist.get_world_size(group) if init else 1)
+        c = cls._shared.get(key)
+        if c is None or not c.handle:
+            c = cls._shared[key] = cls(group)
+        return c
 
     def __init__(self, group=None):
         self.group = group
@@ -45,14 +64,9 @@ class RcclComm(object):
 
     def close(self):
         if self.handle:
+            torch.cuda.synchronize()
             lib().comm_destroy(self.handle)
             self.handle = 0
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
     @staticmethod
     def _code(t):
