@@ -51,6 +51,13 @@ PRESETS = {
 }
 
 
+SAMPLER_DESC = {
+    'alias': 'importance (loss + 0.5*EMA), with replacement',
+    'cdf': 'importance (loss + 0.5*EMA), with replacement (inverse-CDF draws)',
+    'groupwise': 'global HBM importance table, current contiguous-slice group, p ~ loss + mean',
+}
+
+
 def diagnostics(eng, steps, ws):
     """Untimed steps AFTER the timed loop: device-phase times (HIP events on each stream),
     the DP communicator's view (ranks, bucket bytes, all-reduce device time, the part of it
@@ -106,6 +113,9 @@ def main():
                     help='DP all-reduce: own RCCL communicator on a comm stream, or the torch '
                          'ProcessGroup')
     ap.add_argument('--wire-bf16', action='store_true', help='bf16 gradients on the wire')
+    ap.add_argument('--sampler', default='alias', choices=('alias', 'cdf', 'groupwise'),
+                    help="pool draw kernel, or 'groupwise': draws from the HBM importance table "
+                         'over the current contiguous-slice group (Groupwise_Sampler)')
     ap.add_argument('--diag-steps', type=int, default=5,
                     help='untimed steps after the timed loop with device-phase events')
     args = ap.parse_args()
@@ -145,7 +155,7 @@ def main():
                            lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
                            use_graphs=not args.no_graphs, image_hw=hw,
                            force_buckets=args.force_buckets, comm=args.comm,
-                           wire_bf16=args.wire_bf16)
+                           wire_bf16=args.wire_bf16, sampler=args.sampler)
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)
@@ -202,7 +212,7 @@ def main():
                        'global_batch': ws * args.batch, 'per_gpu_batch': args.batch,
                        'presample_pool': args.batch * args.pool_batches, 'seq_len': None,
                        'optimizer': 'adam', 'parallelism': 'dp%d' % ws,
-                       'sampler': 'importance (loss + 0.5*EMA), with replacement'},
+                       'sampler': SAMPLER_DESC[args.sampler]},
             'final_train_loss': round(m['loss_sum'] / max(m['count'], 1), 4),
         }
         out.update(diag)

@@ -1,0 +1,102 @@
+"""Halo-tile conv (hconv) vs the generic implicit GEMM (igemm), timed by HIP-graph replay.
+
+    python bench/hconv_sweep.py [--batch 320] [--reps 12]
+
+Per ResNet-18 CIFAR conv shape with >= 64 input channels, one JSON line:
+  igemm_us       generic implicit GEMM at its heuristic plan (plain input)
+  bn_apply_us    the standalone BN + ReLU pass over the conv input that igemm needs first
+  hconv_us       halo conv, plain input, best plan over tiles x 64-channel splits
+  hconv_bn_us    halo conv with the producer's BN + ReLU applied while staging (+ the kept
+                 activation where the halos tile the input) -- replaces bn_apply + igemm
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+from gtime import gtime  # noqa: E402
+
+SHAPES = [  # C, K, H, R, stride
+    (64, 64, 32, 3, 1), (64, 128, 32, 3, 2), (128, 128, 16, 3, 1), (128, 256, 16, 3, 2),
+    (256, 256, 8, 3, 1), (256, 512, 8, 3, 2), (512, 512, 4, 3, 1)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=320)
+    ap.add_argument('--no-bn', action='store_true')
+    ap.add_argument('--reps', type=int, default=12)
+    args = ap.parse_args()
+    import torch
+    from mercury_amd import ops
+    from mercury_amd.ops import hconv as H
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes
+    dev = 'cuda'
+    N = args.batch
+    gimgs = 32 if N > 32 else 0
+    G = N // gimgs if gimgs else 1
+    tot = dict(igemm=0.0, bn_apply=0.0, hconv=0.0, hconv_bn=0.0)
+    for (C, K, Hh, R, st) in SHAPES:
+        sp = ConvSpec(N, Hh, Hh, C, K, R, R, st, R // 2)
+        if gimgs:
+            sp.group_rows = gimgs * sp.P * sp.Q
+        torch.manual_seed(0)
+        y = ops.to_nhwc(torch.randn(N, C, Hh, Hh, device=dev))
+        a = torch.empty_like(y)
+        wk, _ = ops.pack_conv_weight(torch.randn(K, C, R, R, device=dev) * 0.05)
+        out = torch.empty(sp.M * K, dtype=torch.bfloat16, device=dev)
+        stats = torch.zeros(G * 2 * K, device=dev)
+        ystats = torch.rand(G * 2 * C, device=dev) + 1.0
+        gamma = torch.ones(C, device=dev)
+        beta = torch.zeros(C, device=dev)
+        cands = []
+        for bm, bn, _ in H.TILES:
+            g = H.geometry_cached(sp, bm, bn)
+            if g is None:
+                continue
+            for s in (1, 2, 4):
+                if s <= C // 64 and H.lds_bytes(g, bm, bn, s) <= H.LDS_MAX:
+                    cands.append((bm, bn, s))
+        hp = H.plan(sp)
+        ip = fwd_plan(sp)
+        slab = torch.zeros(max([slab_bytes(sp.M, K, *c) for c in cands + [ip]] + [4]) // 4 + 1,
+                           device=dev)
+        ti = gtime(lambda: ops.conv_fwd(y, wk, out, sp, stats=stats, slab=slab, plan=ip),
+                   reps=args.reps)
+        tb = gtime(lambda: ops.bn_apply(y, ystats, gamma, beta, a, N * Hh * Hh, C,
+                                        group_rows=(gimgs or N) * Hh * Hh, act='relu'),
+                   reps=args.reps)
+        res = {}
+        for c in cands:
+            res[c] = gtime(lambda: H.hconv_fwd(y, wk, out, sp, c, stats=stats, slab=slab),
+                           reps=args.reps)
+        best = min(res, key=res.get)
+        pro = dict(stats=ystats, gamma=gamma, beta=beta, act='relu', count=(gimgs or N) * Hh * Hh,
+                   group_imgs=gimgs or N, keep=a if H.keep_ok(sp) else None)
+        tbn = -1.0 if args.no_bn else gtime(
+            lambda: H.hconv_fwd(y, wk, out, sp, best, stats=stats, slab=slab, pro=pro),
+            reps=args.reps)
+        row = dict(shape=[N, C, K, Hh, R, st], igemm_plan=list(ip), igemm_us=round(ti, 2),
+                   igemm_tflops=round(sp.flops() / ti / 1e6, 1), bn_apply_us=round(tb, 2),
+                   hconv_heur=list(hp) if hp else None,
+                   hconv_heur_us=round(res.get(tuple(hp), -1), 2) if hp else None,
+                   hconv_best=list(best), hconv_us=round(res[best], 2),
+                   hconv_tflops=round(sp.flops() / res[best] / 1e6, 1),
+                   hconv_bn_us=round(tbn, 2),
+                   all={'%dx%d/%d' % c: round(t, 2) for c, t in res.items()})
+        print(json.dumps(row), flush=True)
+        tot['igemm'] += ti
+        tot['bn_apply'] += tb
+        tot['hconv'] += res[best]
+        tot['hconv_bn'] += tbn
+    print(json.dumps({'batch': N, 'totals_us': {k: round(v, 1) for k, v in tot.items()}}),
+          flush=True)
+
+
+if __name__ == '__main__':
+    main()

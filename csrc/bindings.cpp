@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 int igemm_read_stamps(unsigned long long* host, int n);
+int hconv_read_stamps(unsigned long long* host, int n);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
@@ -77,6 +78,32 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, false, S(st), 0, &pr);
     check_launch("igemm_pro");
   });
+  // halo-tile forward conv (hconv.hip) with the producer's BN (+ residual / shortcut BN) +
+  // activation applied while staging its input
+  m.def("hconv", [](uintptr_t src, uintptr_t wt, uintptr_t out, uintptr_t bias, uintptr_t stats,
+                    int group_rows, uintptr_t slab, const std::vector<int>& geo, int bm, int bn,
+                    int splits, uintptr_t st, int mode, uintptr_t p_stats, uintptr_t p_rmean,
+                    uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, uintptr_t p_res,
+                    uintptr_t p_y2, uintptr_t p_stats2, uintptr_t p_rmean2, uintptr_t p_rvar2,
+                    uintptr_t p_gamma2, uintptr_t p_beta2, uintptr_t p_keep, int p_group_imgs,
+                    float p_inv_count, float p_eps, int p_act) {
+    if (geo.size() != 19) throw std::invalid_argument("hconv: geometry needs 19 ints");
+    HconvGeom g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9],
+                geo[10], geo[11], geo[12], geo[13], geo[14], geo[15], geo[16], geo[17], geo[18],
+                0, nullptr};
+    const int K = geo[6];
+    EpiParams e{P<bf16>(out), K, P<const float>(bias), P<float>(stats), K, group_rows, 0,
+                P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
+    HconvPro pr{mode, P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
+                P<const float>(p_gamma), P<const float>(p_beta), P<const bf16>(p_res),
+                P<const bf16>(p_y2), P<const float>(p_stats2), P<const float>(p_rmean2),
+                P<const float>(p_rvar2), P<const float>(p_gamma2), P<const float>(p_beta2),
+                P<bf16>(p_keep), p_group_imgs, p_inv_count, p_eps, p_act};
+    const int ok = hconv_launch(P<const bf16>(src), P<const bf16>(wt), g, e, pr, bm, bn, splits,
+                                S(st));
+    if (!ok) throw std::invalid_argument("hconv: tile not instantiated");
+    check_launch("hconv");
+  });
   m.def("conv_bwd_pair", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int ldo, int accumulate,
                             uintptr_t slab, int SH, int SW, int SC, int RP, int RQ, int R, int Sk,
                             int stride, int pad, int Kc, int Ncols, int M, int bm, int bn,
@@ -122,6 +149,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("igemm_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!igemm_read_stamps(v.data(), n)) v.clear();
+    return v;
+  });
+  m.def("hconv_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
+    std::vector<unsigned long long> v((size_t)n * 12, 0ull);
+    if (!hconv_read_stamps(v.data(), n)) v.clear();
     return v;
   });
   m.def("igemm_slab_bytes", [](int M, int Ncols, int bm, int bn, int splits) {
@@ -259,6 +291,14 @@ PYBIND11_MODULE(_C, m) {
                       ndraw, seed, P<int64_t>(out), P<int>(out32)};
     table_sample_launch(a, S(st));
     check_launch("table_sample");
+  });
+  m.def("table_weights", [](uintptr_t pos, int ndraw, uintptr_t imp, uintptr_t sc,
+                            uintptr_t pool_index, int Ns, int npool, uintptr_t idx, uintptr_t isw,
+                            uintptr_t meters, uintptr_t st) {
+    table_weights_launch(P<const int>(pos), ndraw, P<const float>(imp), (const void*)sc,
+                         P<const int>(pool_index), Ns, npool, P<int>(idx), P<float>(isw),
+                         P<float>(meters), S(st));
+    check_launch("table_weights");
   });
 
   m.def("pack_opt_segs", [](const std::vector<std::vector<long long>>& rows) {

@@ -2,28 +2,34 @@
 // staging (reference conv/BN/ReLU stack `pytorch_model.py:19-36,72-97`).
 //
 // Why a halo tile.  The generic implicit GEMM (igemm.hip) gathers every input pixel once per
-// filter tap: a 3x3 conv moves 9x its input through each CU's vector-memory path, and on
-// MI355X the per-CU load path -- not the MFMAs -- sets the pace of the register-staged loop
-// (stamps: ~1.1k cycles of load issue per 64-deep stage against ~0.5k of MFMA).  Here a
+// filter tap: a 3x3 conv moves 9x its input through each CU's vector-memory path.  Here a
 // block's output tile is IMG whole images or TR whole output rows of one image, so the input
-// it needs for one 64-channel slice is a small rectangle (the halo).  It is staged into LDS
-// ONCE and every tap reads its A fragments from it at a uniform pixel offset; per stage only
-// the BN x 64 weight tile streams in.
+// it needs for one 64-channel slice is a small rectangle (the halo), staged into LDS ONCE and
+// read by every tap at a uniform pixel offset; per tap only the BN x 64 weight tile streams in.
 //
 // Why the BN goes here.  A ResNet block's BatchNorm (+ residual, + shortcut BatchNorm) and
 // ReLU are elementwise on the conv INPUT, and a halo stages each input element exactly once:
-// applying scale/shift + activation there costs one FMA/max per element, not 9 (the reason the
-// generic kernel's prologue was restricted to 1x1 convs).  The activation is also written back
-// once (``keep``) where the training backward or the next residual needs it, by the blocks of
-// the first N tile, for the pixels that tile owns.  So no standalone bn_apply pass remains in a
-// ResNet forward except the last block's (read by the pooling head).
+// applying scale/shift + activation there costs one FMA/max per element, not 9.  The activation
+// is also written back once (``keep``) where the training backward or the next residual needs
+// it, by the blocks of the first N tile, for the pixels that tile owns.
+//
+// Pipeline (everything global -> LDS is LDS-DMA, `global_load_lds_dwordx4`, so no VGPR ever
+// holds a tile in flight and every wait is an explicit counted `s_waitcnt vmcnt`):
+//   * weights: a 3-slot ring, the tile of step s + 2 issued while step s computes;
+//   * halo: slice c + 1's raw halo is issued in pieces during taps 0..T-3 of slice c into the
+//     second halo buffer (single-slice tiles use one buffer, two blocks share a CU instead);
+//   * MODE > 0: at a slice start the raw halo is normalised IN PLACE in LDS (+ residual / +
+//     shortcut BN loaded to registers, + activation, + the kept activation written once);
+//   * one barrier per step (a ring slot is rewritten only after every wave left it).
+// Issue counts per step are uniform by construction (halo pieces past the last load the zero
+// page into a dump area), so each wait is one of four immediates.
 //
 // Layout.  Halo pixel (img, hr, col) lives at LDS pixel index (img*HT + hr)*HWP + col, 128 B per
 // pixel (the 64-channel slice), chunk c of pixel p at slot c ^ (p & 7).  Stride-2 3x3 convs
 // store the even input columns first and the odd ones from HALF on, so consecutive output
-// pixels read consecutive LDS pixels at every tap.  With the row pitch HWP chosen on the host
-// by a model of ds_read_b128's lane groups (ops/hconv.py), every A-fragment read of the ResNet
-// shapes is bank-conflict-free.  The weight tile uses the igemm.hip image ([row][64],
+// pixels read consecutive LDS pixels at every tap.  The row pitch HWP is chosen on the host by
+// a model of ds_read_b128's lane groups (mercury_amd/ops/hconv.py) so every A-fragment read of
+// the ResNet shapes is bank-conflict-free.  The weight slot uses the igemm.hip image ([row][64],
 // chunk c ^ (row & 7)).  MFMA v_mfma_f32_16x16x32_bf16 with swapped operands (lane l: output
 // pixel l&15, four consecutive channels), so the shared epilogue of conv_epi.h applies as is:
 // ghost-BN statistics, split-K (over 64-channel slices) reduced in-launch by the last slice.
@@ -31,7 +37,8 @@
 
 namespace {
 
-MA_DEV int bswz(int row, int chunk) { return chunk ^ (row & 7); }
+constexpr int NSLOT = 3;     // weight ring slots (prefetch distance 2)
+constexpr int HRMAX = 16;    // halo DMA pieces per wave (32 pixels per piece over 4 waves)
 
 MA_DEV float act_f(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
@@ -65,18 +72,47 @@ MA_DEV void bn_coef8(const float* stats, const float* rmean, const float* rvar, 
   }
 }
 
-constexpr int HRMAX = 16;    // halo 16-B chunks per thread (HPIX * 8 <= 16 * 256)
+// 16 bytes per lane, global -> LDS (`global_load_lds_dwordx4`), lane l landing at the wave-uniform
+// LDS address + 16 l.  Issued from inline asm on purpose: the compiler models LDS-DMA as an LDS
+// event of unknown order and then answers every fragment read with lgkmcnt(0) (measured on the
+// ROCm 7.2 hipcc), so it must not see these; their completion is tracked by our own vmcnt waits.
+MA_DEV void dma16(const void* src, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
+MA_DEV unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// zero source for padding halo pixels: one 64-channel slice per possible slice offset
+__device__ __attribute__((aligned(16))) bf16 g_hzero[64 * 17];
+
+template <int N>
+MA_DEV void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier WITHOUT the release fence of __syncthreads (whose vmcnt(0) would drain the
+// LDS-DMA ring every step).  DMA visibility comes from each wave's counted vmcnt before it;
+// the memory clobber keeps the compiler from moving LDS accesses across it.
+MA_DEV void bar_raw() { asm volatile("s_barrier" ::: "memory"); }
+// ... after this wave's LDS writes have completed
+MA_DEV void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int BM, int BN, int WM, int MODE>
-__global__ __launch_bounds__(NT, 2) void hconv_kernel(const bf16* __restrict__ src,
+__global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ src,
                                                       const bf16* __restrict__ wt, HconvGeom g,
                                                       EpiParams e, HconvPro pro) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  constexpr int BRW = BN / 32;                      // weight rows per thread per stage
+  constexpr int BI = BN / 32;                       // weight DMA pieces per wave per step
+  constexpr int HI = 3;                             // halo pieces per wave per prefetch step
+  constexpr int SLOT = BN * 128;                    // bytes per weight slot
+  constexpr int R = 3, T = R * R;                   // 3x3 filters (1x1 convs stay on igemm)
+  constexpr int HP = T - 2;                         // taps that carry next-slice halo pieces
+  static_assert(T % NSLOT == 0, "ring slot = tap % NSLOT");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* halo = smem;
-  bf16* sB = (bf16*)(smem + g.HPIX * 128);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
@@ -90,24 +126,28 @@ __global__ __launch_bounds__(NT, 2) void hconv_kernel(const bf16* __restrict__ s
   const int M = g.N * PQ;
   const int n0i = m0 / PQ;
   const int p0 = (m0 - n0i * PQ) / g.Q;
-  const int cc = tid & 7;
   const int nchunks = g.C >> 6;
   const int cb0 = by * g.chunks_per_split;
   const int cb1 = min(nchunks, cb0 + g.chunks_per_split);
-  const int T = g.R * g.R;
+  const int nsl = cb1 - cb0;
+  const int nst = nsl * T;
   const int Kt = T * g.C;
   const bf16* zp = g.zero;
+  (void)zp;
+  const int HR = (g.HPIX + 31) >> 5;                // DMA pieces per wave for a whole halo
+  const int HBYTES = HR * 32 * 128;
+  const int NH = g.chunks_per_split > 1 ? 2 : 1;
+  char* ring = smem + NH * HBYTES;
+  const int lc = (lane & 7) ^ (lane >> 3);          // logical chunk this lane fetches
 
-  // ---- halo slots of this thread (the same for every 64-channel slice): source element
-  // offset of channel chunk cc of slice 0 (or -1: padding / beyond the batch), and whether the
-  // pixel belongs to this tile (activation write-back).  Slot i is halo pixel (tid >> 3) + 32 i,
-  // so its LDS byte offset is hbase + 4096 i (pixel & 7 is the same for every i).
-  const int HR = (g.HPIX * 8 + NT - 1) / NT;
+  // ---- halo slots of this thread: slot j is pixel (tid >> 3) + 32 j; source element offset
+  // of its logical chunk lc in slice 0 (or -1: padding / beyond the batch), and whether the
+  // pixel belongs to this tile (activation write-back)
   int hsrc[HRMAX];
+  const bf16* hptr[HRMAX];                          // DMA source of slice 0 (zero rows for pads)
   unsigned own = 0;
   const int per_img = g.HT * g.HWP;
   const int h0 = p0 * g.stride - g.pad;
-  const int hbase = ((tid >> 3) * 8 + (cc ^ ((tid >> 3) & 7))) * 16;
 #pragma unroll
   for (int i = 0; i < HRMAX; ++i) {
     hsrc[i] = -1;
@@ -127,12 +167,14 @@ __global__ __launch_bounds__(NT, 2) void hconv_kernel(const bf16* __restrict__ s
       const int h = h0 + hr * g.HS, ww = hc * g.HS - g.pad, n = n0i + img;
       ok = ok && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       if (ok) {
-        hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + cc * 8;
+        hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + lc * 8;
         // the tile owns input rows [p0*stride, (p0+TR)*stride) of its images (all columns)
         if (h >= p0 * g.stride && h < (p0 + g.TR) * g.stride) own |= 1u << i;
       }
     }
   }
+#pragma unroll
+  for (int i = 0; i < HRMAX; ++i) hptr[i] = hsrc[i] >= 0 ? src + hsrc[i] : g_hzero + lc * 8;
   const bool keep = MODE > 0 && pro.keep != nullptr && nt == 0;   // host: only when owned = all
   const int grp = MODE > 0 ? n0i / pro.group_imgs : 0;
 
@@ -147,73 +189,82 @@ __global__ __launch_bounds__(NT, 2) void hconv_kernel(const bf16* __restrict__ s
     const int col = g.HALF ? ((hc & 1) * g.HALF + (hc >> 1)) : hc;
     apix[tm] = img * per_img + tr * g.SR * g.HWP + col;
   }
-  int boff[BRW];
+  // weight rows this lane fetches (DMA piece j covers rows 8 * (w + 4 j) .. + 8)
+  // (the host guarantees K % BN == 0: every weight row exists)
+  const bf16* bptr[BI];
 #pragma unroll
-  for (int i = 0; i < BRW; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
-    boff[i] = n < g.K ? n * Kt : -1;
+  for (int j = 0; j < BI; ++j) {
+    const int n = n0 + 8 * (w + 4 * j) + (lane >> 3);
+    bptr[j] = wt + (size_t)n * Kt + lc * 8;
   }
+  // wave-uniform LDS byte addresses (scalar: no per-DMA readfirstlane / pointer casts)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned s_halo = lds_addr(smem);
+  const unsigned s_ring = s_halo + NH * HBYTES;
+  const unsigned s_dump = s_ring + NSLOT * SLOT + wu * 1024;
 
-  // ---- staging helpers
-  auto stage_halo = [&](int cb) {
-    // load, (MODE) normalise + residual + activation, write back the owned pixels, LDS store;
-    // in batches so at most 8 (4 with a second input) 16-byte loads per thread are in flight
-    constexpr int BATCH = MODE >= 2 ? 4 : 8;
-    float sc[8], sh[8], sc2[8], sh2[8];
+  // ---- issue helpers (wave-uniform LDS bases)
+  // weight tile of (slice cb, tap t) into ring slot `slot`
+  auto issue_b = [&](int cb, int t, int slot) {
+    const int k = t * g.C + cb * 64;
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      dma16(bptr[j] + k, s_ring + slot * SLOT + 8 * (wu + 4 * j) * 128);
+  };
+  // halo DMA piece j (compile-time: the tap loop is unrolled) of slice cb into buffer buf.  A
+  // piece past the halo's last loads zeros into a 4 KB dump area, so every prefetch tap issues
+  // exactly HI pieces and the counted waits hold.
+  auto issue_h = [&](int cb, int buf, int j) {
+    const bool v = j < HR;
+    dma16(hptr[j] + cb * 64, v ? s_halo + buf * HBYTES + (32 * j + 8 * wu) * 128 : s_dump);
+  };
+
+  // ---- in-place BN (+ residual / shortcut BN) + activation of a landed raw halo
+  auto transform = [&](int cb, int buf) {
     if constexpr (MODE > 0) {
-      const int ch = cb * 64 + cc * 8;
+      float sc[8], sh[8], sc2[8], sh2[8];
+      const int ch = cb * 64 + lc * 8;            // this thread's logical chunk: lc of its lane
       bn_coef8(pro.stats, pro.rmean, pro.rvar, pro.gamma, pro.beta, g.C, grp, ch, pro.inv_count,
                pro.eps, sc, sh);
       if constexpr (MODE == 3)
         bn_coef8(pro.stats2, pro.rmean2, pro.rvar2, pro.gamma2, pro.beta2, g.C, grp, ch,
                  pro.inv_count, pro.eps, sc2, sh2);
-    }
+      char* hb = smem + buf * HBYTES + (tid >> 3) * 128 + (tid & 7) * 16;
+      constexpr int BATCH = 8;
 #pragma unroll
-    for (int i0 = 0; i0 < HRMAX; i0 += BATCH) {
-      if (i0 >= HR) break;
-      u32x4 v[BATCH], r[BATCH];
+      for (int i0 = 0; i0 < HRMAX; i0 += BATCH) {
+        if (i0 >= HR) break;
+        u32x4 r[BATCH];
+        if constexpr (MODE >= 2) {
 #pragma unroll
-      for (int j = 0; j < BATCH; ++j) {
-        const int o = hsrc[i0 + j];
-        v[j] = *(const u32x4*)(o >= 0 ? src + o + cb * 64 : zp);
-        if constexpr (MODE == 2) r[j] = *(const u32x4*)(o >= 0 ? pro.res + o + cb * 64 : zp);
-        if constexpr (MODE == 3) r[j] = *(const u32x4*)(o >= 0 ? pro.y2 + o + cb * 64 : zp);
-      }
-#pragma unroll
-      for (int j = 0; j < BATCH; ++j) {
-        const int i = i0 + j;
-        if constexpr (MODE > 0) {
-          const bf16x8 y = __builtin_bit_cast(bf16x8, v[j]);
-          const bf16x8 rr = __builtin_bit_cast(bf16x8, r[j]);
-          bf16x8 o;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            float a = bf2f(y[k]) * sc[k] + sh[k];
-            if constexpr (MODE == 2) a += bf2f(rr[k]);
-            if constexpr (MODE == 3) a += bf2f(rr[k]) * sc2[k] + sh2[k];
-            o[k] = f2bf(act_f(a, pro.act));
+          for (int j = 0; j < BATCH; ++j) {
+            const int o = hsrc[i0 + j];
+            const bf16* base = MODE == 2 ? pro.res : pro.y2;
+            r[j] = *(const u32x4*)(o >= 0 ? base + o + cb * 64 : zp);
           }
-          // padding stays zero in ACTIVATION space (the conv pads the normalised input)
-          v[j] = hsrc[i] >= 0 ? __builtin_bit_cast(u32x4, o) : u32x4{0u, 0u, 0u, 0u};
-          if (keep && ((own >> i) & 1)) *(u32x4*)(pro.keep + hsrc[i] + cb * 64) = v[j];
         }
-        if (i < HR && (tid >> 3) + 32 * i < g.HPIX) *(u32x4*)(halo + hbase + 4096 * i) = v[j];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+          const int i = i0 + j;
+          if (i < HR && (tid >> 3) + 32 * i < g.HPIX) {
+            u32x4* lp = (u32x4*)(hb + i * 4096);
+            const bf16x8 y = __builtin_bit_cast(bf16x8, *lp);
+            const bf16x8 rr = __builtin_bit_cast(bf16x8, r[j]);
+            bf16x8 o;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              float a = bf2f(y[k]) * sc[k] + sh[k];
+              if constexpr (MODE == 2) a += bf2f(rr[k]);
+              if constexpr (MODE == 3) a += bf2f(rr[k]) * sc2[k] + sh2[k];
+              o[k] = f2bf(act_f(a, pro.act));
+            }
+            // padding stays zero in ACTIVATION space (the conv pads the normalised input)
+            const u32x4 v = hsrc[i] >= 0 ? __builtin_bit_cast(u32x4, o) : u32x4{0u, 0u, 0u, 0u};
+            *lp = v;
+            if (keep && ((own >> i) & 1)) *(u32x4*)(pro.keep + hsrc[i] + cb * 64) = v;
+          }
+        }
       }
-    }
-  };
-
-  u32x4 rb[BRW];
-  auto load_b = [&](int cb, int t) {
-    const int k = t * g.C + cb * 64 + cc * 8;
-#pragma unroll
-    for (int i = 0; i < BRW; ++i) rb[i] = *(const u32x4*)(boff[i] >= 0 ? wt + boff[i] + k : zp);
-  };
-  auto store_b = [&](int buf) {
-    bf16* b = sB + buf * (BN * BK);
-#pragma unroll
-    for (int i = 0; i < BRW; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *(u32x4*)(b + row * BK + bswz(row, cc) * 8) = rb[i];
     }
   };
 
@@ -223,56 +274,118 @@ __global__ __launch_bounds__(NT, 2) void hconv_kernel(const bf16* __restrict__ s
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (cb0 < cb1) {
-    const int nst = (cb1 - cb0) * T;
-    load_b(cb0, 0);
-    stage_halo(cb0);
-    store_b(0);
-    __syncthreads();
-    for (int s = 0; s < nst; ++s) {
-      const int cl = s / T, t = s - cl * T;
-      const int cb = cb0 + cl;
-      const bool more = s + 1 < nst;
-      if (more) load_b(t + 1 < T ? cb : cb + 1, t + 1 < T ? t + 1 : 0);
-      // A from the halo at the tap's uniform pixel offset, B from the weight stage
-      const int r = t / g.R, ss = t - r * g.R;
-      const int toff = g.HALF ? r * g.HWP + (ss >> 1) + (ss & 1) * g.HALF : r * g.HWP + ss;
-      const bf16* b = sB + (s & 1) * (BN * BK);
+  MA_STAMP(0);
+#ifdef MERCURY_STAMPS
+  unsigned long long lap[4] = {0, 0, 0, 0};
+  unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
+  if (nst > 0) {
+    // prologue: the first slice's whole halo, then the weight tiles of steps 0 and 1
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + (lane >> 4);
-        bf16x8 fa[TM], fb[TN];
+    for (int j = 0; j < HRMAX; ++j)
+      if (j < HR) issue_h(cb0, 0, j);
+    issue_b(cb0, 0, 0);
+    issue_b(cb0, 1, 1);                           // nst >= T = 9
+    for (int cl = 0; cl < nsl; ++cl) {
+      const int buf = NH == 2 ? (cl & 1) : 0;
+      const bool more = NH == 2 && cl + 1 < nsl;  // prefetch the next slice's halo
+      // this slice's halo: everything but the two newest weight tiles has landed
+      vm_wait<2 * BI>();
+      bar_raw();
+      if (cl == 0) MA_STAMP(1);
+      MA_LAP(3, tl);
+      if constexpr (MODE > 0) {
+        transform(cb0 + cl, buf);
+        bar_lds();
+      }
+      const char* hb = smem + buf * HBYTES;
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          const int p = apix[tm] + toff;
-          fa[tm] = *(const bf16x8*)(halo + (p * 8 + (chunk ^ (p & 7))) * 16);
+      for (int t = 0; t < T; ++t) {
+        const int s = cl * T + t;
+        // weight tile of step s: newer are the halo pieces of step s-1 and the tile of s+1
+        const bool hprev = more && t >= 1 && t - 1 < HP;
+        const bool nxt = s + 1 < nst;
+        if (hprev) {
+          if (nxt) vm_wait<HI + BI>();
+          else vm_wait<HI>();
+        } else {
+          if (nxt) vm_wait<BI>();
+          else vm_wait<0>();
+        }
+        bar_raw();
+        MA_LAP(0, tl);
+        if (more && t < HP) {
+#pragma unroll
+          for (int q = 0; q < HI; ++q) {
+            const int j = t * HI + q;
+            issue_h(cb0 + cl + 1, buf ^ 1, j < HRMAX ? j : 0);
+          }
+        }
+        // (T % NSLOT == 0, so the ring slot of step s is t % NSLOT for every slice)
+        if (t + 2 < T) issue_b(cb0 + cl, t + 2, (t + 2) % NSLOT);
+        else if (cl + 1 < nsl) issue_b(cb0 + cl + 1, t + 2 - T, (t + 2) % NSLOT);
+        MA_LAP(1, tl);
+        // MFMA phase: A from the halo at the tap's pixel offset, B from ring slot s % 3
+        const int r = t / R, ss = t % R;
+        const int toff = g.HALF ? r * g.HWP + (ss >> 1) + (ss & 1) * g.HALF : r * g.HWP + ss;
+        const char* bs = ring + (t % NSLOT) * SLOT;
+        // all 16 fragment reads of the tap first (both 32-deep halves in flight at once: one
+        // wave per SIMD has no partner to hide LDS latency), then the MFMAs
+        bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) {
+            const int row = wn * (BN / WN) + tn * 16 + (lane & 15);
+            fb[kk][tn] = *(const bf16x8*)(bs + (row * 8 + (chunk ^ (row & 7))) * 16);
+          }
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm) {
+            const int p = apix[tm] + toff;
+            fa[kk][tm] = *(const bf16x8*)(hb + (p * 8 + (chunk ^ (p & 7))) * 16);
+          }
         }
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          const int row = wn * (BN / WN) + tn * 16 + (lane & 15);
-          fb[tn] = *(const bf16x8*)(b + row * BK + bswz(row, chunk) * 8);
-        }
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
+          for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
+            for (int tn = 0; tn < TN; ++tn)
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][tn], fa[kk][tm],
+                                                                   acc[tm][tn], 0, 0, 0);
+        // keep that order: the scheduler otherwise re-serialises the reads (one fragment
+        // register, an lgkmcnt(0) before every four MFMAs) to save registers it has plenty of
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (TM + TN), 0);   // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * TM * TN, 0);     // MFMAs
+#ifdef MERCURY_STAMPS
+        // (diagnostic build: make the MFMA phase's end observable)
+        asm volatile("s_nop 0" ::"v"(acc[0][0]));
+#endif
+        MA_LAP(2, tl);
       }
-      if (t == T - 1 && more) {
-        __syncthreads();                 // every wave is done with this slice's halo
-        stage_halo(cb + 1);
-      }
-      if (more) store_b((s + 1) & 1);
-      __syncthreads();
     }
+    vm_wait<0>();
   }
+  MA_STAMP(2);
+#ifdef MERCURY_STAMPS
+  if (threadIdx.x == 0) {
+    const int b_ = blockIdx.x + blockIdx.y * gridDim.x;
+    if (b_ < 8192)
+      for (int q = 0; q < 4; ++q) g_stamps[b_][4 + q] = lap[q];
+  }
+#endif
+  __syncthreads();                                // LDS is reused by the epilogue
   finish<BM, BN, WM>(acc, smem, e, M, g.K, m0, n0, bx, by, gx, gy);
+  MA_STAMP(3);
 }
 
 template <int BM, int BN, int WM, int MODE>
 void launch_one(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                 const HconvPro& pro, dim3 grid, hipStream_t st) {
-  const int main_bytes = g.HPIX * 128 + 2 * BN * BK * 2;
+  const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
+  const int nh = g.chunks_per_split > 1 ? 2 : 1;
+  const int main_bytes = nh * hbytes + NSLOT * BN * 128 + 4096;
   const int red = Smem<BM, BN>::RED_BYTES;
   const int bytes = main_bytes > red ? main_bytes : red;
   static bool attr = false;
@@ -298,6 +411,24 @@ void launch_mode(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiP
 
 }  // namespace
 
+int hconv_read_stamps(unsigned long long* host, int n) {
+#ifdef MERCURY_STAMPS
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 12 * n) ==
+         hipSuccess;
+#else
+  (void)host;
+  (void)n;
+  return 0;
+#endif
+}
+
+int hconv_lds_bytes(const HconvGeom& g, int bm, int bn, int splits_gt1) {
+  const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
+  const int main_bytes = (splits_gt1 ? 2 : 1) * hbytes + NSLOT * bn * 128 + 4096;
+  const int red = 16 * bn * 4 + bm * (bn + 8) * 2;
+  return main_bytes > red ? main_bytes : red;
+}
+
 int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const EpiParams& e_in,
                  const HconvPro& pro, int bm, int bn, int splits, hipStream_t st) {
   HconvGeom g = g_in;
@@ -311,6 +442,7 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   int gy = (nchunks + g.chunks_per_split - 1) / g.chunks_per_split;
   if (gx > 1024) gy = 1, g.chunks_per_split = nchunks;    // tile counters: SEM_INTS
   if (gy == 1) e.slab = nullptr;
+  if (((g.HPIX + 31) >> 5) > HRMAX || g.R != 3) return 0;
   const dim3 grid(gx, gy);
 #define HC_CASE(BM_, BN_, WM_)                                  \
   if (bm == BM_ && bn == BN_) {                                 \
@@ -320,6 +452,7 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   HC_CASE(256, 64, 4)
   HC_CASE(128, 64, 2)
   HC_CASE(64, 64, 1)
+  HC_CASE(256, 128, 4)
   HC_CASE(128, 128, 2)
   HC_CASE(64, 128, 1)
 #undef HC_CASE

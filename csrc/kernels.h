@@ -171,6 +171,9 @@ struct TableSampleArgs {
 };
 int table_num_segments(int N);
 void table_sample_launch(const TableSampleArgs& a, hipStream_t st);
+void table_weights_launch(const int* pos, int ndraw, const float* imp, const void* sc,
+                          const int* pool_index, int Ns, int P, int* idx, float* isw,
+                          float* meters, hipStream_t st);
 
 // ------------------------------------------------------------------ optimizer
 struct OptSeg {

@@ -174,7 +174,41 @@ __global__ __launch_bounds__(256) void table_draw_kernel(const float* imp, const
   if (out32) out32[d] = pick;
 }
 
+// Native groupwise step (engine sampler='groupwise'): the drawn table positions -> pool slots
+// of the current contiguous slice (slot = (pos - slice start) mod Ns; the slice is exactly the
+// current group) and unbiased importance weights  w = n_group * p = n_group (imp + mean) / total
+// (the pool sampler's N*p convention: the train loss divides by w).  meters[3] gets the group's
+// mean importance (the pool-mean slot).
+__global__ __launch_bounds__(256) void table_weights_kernel(const int* pos, int ndraw,
+                                                            const float* imp,
+                                                            const TableScalars* sc,
+                                                            const int* pool_index, int Ns, int P,
+                                                            int* idx, float* isw, float* meters) {
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  const float mean = sc->mean, cnt = sc->count;
+  const double total = sc->total;
+  if (d == 0 && meters) meters[3] = mean;
+  if (d >= ndraw) return;
+  const int q = pos[d];
+  if (q < 0 || !(total > 0.0)) {          // empty group (cannot happen after a scatter): slot 0
+    idx[d] = 0;
+    isw[d] = 1.f;
+    return;
+  }
+  int slot = q - pool_index[0];
+  slot = slot < 0 ? slot + Ns : slot;
+  idx[d] = slot < P ? slot : P - 1;
+  isw[d] = (float)((double)cnt * ((double)imp[q] + (double)mean) / total);
+}
+
 }  // namespace
+
+void table_weights_launch(const int* pos, int ndraw, const float* imp, const void* sc,
+                          const int* pool_index, int Ns, int P, int* idx, float* isw,
+                          float* meters, hipStream_t st) {
+  hipLaunchKernelGGL(table_weights_kernel, dim3((ndraw + 255) / 256), dim3(256), 0, st, pos, ndraw,
+                     imp, (const TableScalars*)sc, pool_index, Ns, P, idx, isw, meters);
+}
 
 int table_num_segments(int N) { return (N + TSEG - 1) / TSEG; }
 

@@ -25,7 +25,8 @@ class Config:
     exchange_scores: bool = False   # all-gather pool scores every step (global importance view)
     score: str = 'loss'             # importance score: 'loss' (reference) | 'gradnorm' (per-sample
                                     # classifier-layer gradient norm)
-    sampler: str = 'alias'          # draw kernel: 'alias' (Walker table) | 'cdf' (inverse CDF)
+    sampler: str = 'alias'          # 'alias' (Walker table) | 'cdf' (inverse CDF) | 'groupwise'
+    #                                 (draws from the HBM importance table, Groupwise_Sampler)
     # data
     dataset: str = 'cifar10'
     data_dir: str = './data/cifar10'

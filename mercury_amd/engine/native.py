@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
-from ..ops import tune
+from ..ops import hconv, tune
 from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
@@ -129,7 +129,15 @@ class NativeEngine(object):
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
         # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
         self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
+        # stride-1 3x3 forward convs on the halo-tile kernel (csrc/hconv.hip) where measured faster
+        self.use_hconv = os.environ.get('MERCURY_HCONV', '1') == '1'
+        if sampler not in ('alias', 'cdf', 'groupwise'):
+            raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
         self.sampler = sampler
+        if sampler == 'groupwise' and not global_table:
+            raise ValueError("sampler='groupwise' draws from the global table (global_table=True)")
+        if sampler == 'groupwise' and (exchange_scores or global_ema):
+            raise ValueError("sampler='groupwise' has no pool EMA to share across ranks")
         if score not in ('loss', 'gradnorm'):
             raise ValueError('score must be loss or gradnorm')
         self.score = score
@@ -249,6 +257,11 @@ class NativeEngine(object):
                     m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(
                         sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
+                    # stride-1 3x3 convs on the halo-tile kernel where it measured faster
+                    hp = hconv.engine_plan(sp) if self.use_hconv else None
+                    if hp is not None:
+                        m.plan[u.name, 'hconv'] = hp
+                        slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
                     if train:
                         if u.need_dgrad and sp.K % 8 == 0:
                             dp, wp = tune.bwd_plans_for(sp, dgrad_plan(sp), wgrad_plan(sp))
@@ -326,6 +339,10 @@ class NativeEngine(object):
         if u.depthwise:
             ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
                            sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M)
+        elif pro is None and (u.name, 'hconv') in m.plan:
+            hconv.hconv_fwd(x, self.w_krsc[u.name], y, sp, m.plan[u.name, 'hconv'], stats=stats,
+                            slab=m.slab,
+                            bias=self._pview(u.b_seg) if u.b_seg is not None else None)
         else:
             ops.conv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, slab=m.slab,
                          plan=m.plan[u.name, 'fwd'],
@@ -626,6 +643,12 @@ class NativeEngine(object):
             # shard-wide importance table resident in HBM: every scored pool sample's latest
             # loss, stamped with the optimizer step that scored it
             self.table = ops.ImportanceTable(self.shard.shape[0], self.device)
+        if self.sampler == 'groupwise':
+            if self.shard.shape[0] < self.P:
+                raise ValueError("sampler='groupwise' needs a shard of at least one pool "
+                                 '(%d samples)' % self.P)
+            self._draw_pos = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+            self._gstamp = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._build_bn_table()
 
     def _build_bn_table(self):
@@ -661,20 +684,37 @@ class NativeEngine(object):
             self.idx.copy_(self._arange_b)
             self.isw.fill_(1.0)
             return
+        # groupwise (Groupwise_Sampler, `util.py:114-138`): the pool is the next CONTIGUOUS slice
+        # of the shard (cursor order, wrapping), which becomes this iteration's group
         ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label, sm.index,
-                       self.P, self.B, self.seed, zero=sm.stats_arena)
+                       self.P, self.B, self.seed, zero=sm.stats_arena,
+                       shuffle=self.sampler != 'groupwise')
         # (the scoring convs keep their full occupancy: reserving extra LDS per scoring block
         # so train blocks fit beside them measured 1.70-2.21 ms/step vs 1.65 -- in the
         # concurrent step the GPU is throughput-bound, bench/ab_env.sh)
         x = self.forward(sm)
         self.head(sm, x, 'score')
         if self.table is not None:
-            self.table.scatter(sm.index, sm.losses, stamp=self.ctrl[2:3])
+            if self.sampler == 'groupwise':
+                # a new group per scored slice (never 0: group 0 is the initial uniform table)
+                torch.add(self.ctrl[0:1], 1, out=self._gstamp)
+                self.table.scatter(sm.index, sm.losses, stamp=self._gstamp)
+            else:
+                self.table.scatter(sm.index, sm.losses, stamp=self.ctrl[2:3])
 
     def score_sample(self):
         if not self.scoring:
             return
         sm = self.score_mode
+        if self.sampler == 'groupwise':
+            # draw from the global HBM table over the current group (the slice just scattered,
+            # stamped with this step's counter): p ~ imp + mean(imp) (`util.py:144-152`), then
+            # pool slots + unbiased weights n_group * p
+            self.table.draw_batch(self.B, self._gstamp, self._draw_pos, sm.index,
+                                  self.shard.shape[0], self.P, self.idx, self.isw, seed=self.seed,
+                                  meters=self.meters)
+            self.ctrl[0:2].add_(1)       # pool and draw counters (is_sample bumps them otherwise)
+            return
         gathered = self.score_exchange.gathered if self._split_score else None
         ops.is_sample(sm.losses, self.ema, self.ctrl, self.idx, self.isw, self.P, self.B, self.B,
                       self.alpha, self.ema_alpha, self.seed, self.importance, self.meters,

@@ -1,0 +1,272 @@
+"""Halo-tile forward convolution (csrc/hconv.hip): geometry, LDS pitch and launch.
+
+A block's output tile is IMG whole images (IMG * P * Q rows) or TR whole output rows of one
+image (TR * Q rows), so the input one 64-channel slice of the tile reads is a rectangle -- the
+halo -- staged into LDS once and read by all R*R taps.  The producer's BatchNorm (+ identity
+residual or shortcut BatchNorm) + activation is applied while staging (``pro``), so a ResNet
+forward needs no standalone bn_apply pass between convs.
+
+Reference: the conv/BN/ReLU stack of `pytorch_model.py:19-36,72-97`.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _chk, lib, ptr, stream_ptr
+from .conv import ConvSpec, slab_bytes
+
+HRMAX_PIX = 512                 # halo pixels per tile (csrc/hconv.hip HRMAX pieces x 32 pixels)
+LDS_MAX = 160 * 1024            # one workgroup may take the whole 160 KiB of a CU
+NSLOT = 3                       # weight ring slots (csrc/hconv.hip)
+TILES = ((256, 64, 4), (128, 64, 2), (64, 64, 1), (256, 128, 4), (128, 128, 2), (64, 128, 1))
+_WM = {(bm, bn): wm for bm, bn, wm in TILES}
+_ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
+
+# ds_read_b128 lane groups (MI355X_MICROARCH.md §LDS): one LDS cycle per group when its 16
+# lanes hit 16 distinct 16-byte bank quads
+_GROUPS = ([0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+           [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31])
+_GROUPS = _GROUPS + tuple([l + 32 for l in g] for g in _GROUPS)
+
+
+def supported(spec: ConvSpec):
+    """3x3 convs (stride 1 or 2, pad 1) on 64-channel slices with whole 64/128-column weight
+    tiles; 1x1 convs stay on igemm."""
+    return (spec.R == spec.S == 3 and spec.stride in (1, 2) and spec.C % 64 == 0
+            and spec.pad == 1 and spec.Cp == spec.C and spec.K % 64 == 0
+            and (spec.K <= 64 or spec.K % 128 == 0))
+
+
+def lds_bytes(g, bm, bn, splits):
+    """Dynamic LDS of one block (csrc/hconv.hip launch_one): one halo buffer per tile, two when
+    a block walks several 64-channel slices (the next slice's halo is prefetched), the weight
+    ring, a 4 KB DMA sink; at least the epilogue's staging area."""
+    nch = g['C'] // 64
+    per = -(-nch // max(1, min(splits, nch)))
+    hbytes = -(-g['HPIX'] // 32) * 32 * 128
+    main = (2 if per > 1 else 1) * hbytes + NSLOT * bn * 128 + 4096
+    red = 16 * bn * 4 + bm * (bn + 8) * 2
+    return max(main, red)
+
+
+def _tile_shape(spec: ConvSpec, bm):
+    """(IMG, TR) for a BM-row tile, or None."""
+    P, Q = spec.P, spec.Q
+    PQ = P * Q
+    if bm >= PQ:
+        if bm % PQ:
+            return None
+        img = bm // PQ
+        if spec.N % img:
+            return None
+        if spec.group_rows and (spec.group_rows // PQ) % img:
+            return None                       # a tile's images share one ghost-BN group
+        return img, P
+    if bm % Q:
+        return None
+    tr = bm // Q
+    if P % tr:
+        return None
+    return 1, tr
+
+
+def _conflict_cycles(g, bm, bn):
+    """LDS cycles of every A-fragment ds_read_b128 of one 64-channel slice (all taps), by the
+    lane-group model: each group costs its maximum multiplicity over 16-byte bank quads."""
+    wm = _WM[bm, bn]
+    TM = bm // (16 * wm)
+    IMG, TR, Q, SR, HWP, HALF, R = g['IMG'], g['TR'], g['Q'], g['SR'], g['HWP'], g['HALF'], g['R']
+    per_img = g['HT'] * HWP
+    cyc = 0
+    for w in range(wm):
+        for tm in range(TM):
+            pix = []
+            for l in range(16):
+                row = w * (bm // wm) + tm * 16 + l
+                img, rem = divmod(row, TR * Q)
+                tr, q = divmod(rem, Q)
+                hc = q * SR
+                col = ((hc & 1) * HALF + (hc >> 1)) if HALF else hc
+                pix.append(img * per_img + tr * SR * HWP + col)
+            for t in range(R * R):
+                r, s = divmod(t, R)
+                toff = r * HWP + ((s >> 1) + (s & 1) * HALF if HALF else s)
+                for kk in range(2):
+                    for grp in _GROUPS:
+                        seen = {}
+                        for lane in grp:
+                            p = pix[lane & 15] + toff
+                            c = kk * 4 + (lane >> 4)
+                            u = (p * 8 + (c ^ (p & 7))) % 16
+                            seen[u] = seen.get(u, 0) + 1
+                        cyc += max(seen.values())
+    return cyc
+
+
+def geometry(spec: ConvSpec, bm, bn):
+    """HconvGeom as a dict (csrc/igemm.h), or None when this tile does not fit the conv."""
+    if not supported(spec) or (bm, bn) not in _WM:
+        return None
+    ts = _tile_shape(spec, bm)
+    if ts is None:
+        return None
+    IMG, TR = ts
+    R, st = spec.R, spec.stride
+    if R == 1 and st == 2:
+        HS, SR = 2, 1                          # only the even input pixels are ever read
+        HT, HWd = TR, spec.Q
+    else:
+        HS, SR = 1, st
+        HT, HWd = (TR - 1) * st + R, (spec.Q - 1) * st + R
+    g = dict(N=spec.N, H=spec.H, W=spec.W, C=spec.C, P=spec.P, Q=spec.Q, K=spec.K, R=R,
+             stride=st, pad=spec.pad, IMG=IMG, TR=TR, HT=HT, HWd=HWd, HS=HS, SR=SR)
+    best = None
+    halves = [0] if SR == 1 else [(HWd + 1) // 2 + d for d in range(0, 9)]
+    for half in halves:
+        base = max(HWd, half + HWd // 2) if half else HWd
+        for hwp in range(base, base + 17):
+            hp = IMG * HT * hwp
+            if hp > HRMAX_PIX:
+                break
+            g.update(HWP=hwp, HALF=half, HPIX=hp)
+            c = _conflict_cycles(g, bm, bn)
+            key = (c, hp)
+            if best is None or key < best[0]:
+                best = (key, dict(g))
+    return None if best is None else best[1]
+
+
+_GEO_CACHE = {}
+
+
+def geometry_cached(spec: ConvSpec, bm, bn):
+    key = (spec.N, spec.H, spec.W, spec.C, spec.K, spec.R, spec.stride, spec.pad,
+           spec.group_rows, bm, bn)
+    if key not in _GEO_CACHE:
+        _GEO_CACHE[key] = geometry(spec, bm, bn)
+    return _GEO_CACHE[key]
+
+
+_ORDER = ('N', 'H', 'W', 'C', 'P', 'Q', 'K', 'R', 'stride', 'pad', 'IMG', 'TR', 'HT', 'HWd',
+          'HWP', 'HALF', 'HS', 'SR', 'HPIX')
+
+
+def plan(spec: ConvSpec, min_blocks=256):
+    """(bm, bn, splits) for hconv, or None.  Larger tiles first (fewer halo re-reads per FLOP);
+    split the 64-channel slices when the grid would leave CUs idle."""
+    bn = 64 if spec.K <= 64 else 128
+    for bm in (256, 128, 64):
+        if (bm, bn) not in _WM:
+            continue
+        g = geometry_cached(spec, bm, bn)
+        if g is None or lds_bytes(g, bm, bn, 1) > LDS_MAX:
+            continue
+        blocks = math.ceil(spec.M / bm) * math.ceil(spec.K / bn)
+        if blocks >= min_blocks or bm == 64:
+            break
+    else:
+        return None
+    g = geometry_cached(spec, bm, bn)
+    if g is None:
+        return None
+    blocks = math.ceil(spec.M / bm) * math.ceil(spec.K / bn)
+    nch = spec.C // 64
+    splits = 1
+    if blocks < min_blocks * 3 // 4 and nch >= 2 and blocks <= 1024:
+        splits = min(nch, math.ceil(min_blocks / blocks), 8)
+    if lds_bytes(g, bm, bn, splits) > LDS_MAX:
+        return None
+    return bm, bn, splits
+
+
+# Measured winners (bench/hconv_sweep.py, graph-timed, MI355X; profiles/r2/hconv_sweep_b*.jsonl):
+# stride-1 3x3 convs of the CIFAR ResNets, keyed (N, H, C, K) -> (bm, bn, splits).  On these the
+# halo conv beats the generic implicit GEMM by 2-30 % (B=320 layer4 46 vs 66 us); on stride-2
+# convs it does not, so those stay on igemm.
+MEASURED = {
+    (320, 32, 64, 64): (128, 64, 1), (320, 16, 128, 128): (128, 64, 2),
+    (320, 8, 256, 256): (256, 128, 1), (320, 4, 512, 512): (128, 128, 1),
+    (32, 32, 64, 64): (256, 64, 1), (32, 16, 128, 128): (64, 64, 1),
+    (32, 8, 256, 256): (64, 64, 2), (32, 4, 512, 512): (64, 64, 4),
+}
+
+
+def engine_plan(spec: ConvSpec):
+    """The plan the engine runs hconv with for this conv, or None (use igemm): measured winners,
+    else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every measured
+    shape)."""
+    if not supported(spec) or spec.stride != 1:
+        return None
+    p = MEASURED.get((spec.N, spec.H, spec.C, spec.K))
+    if p is not None:
+        g = geometry_cached(spec, p[0], p[1])
+        if g is not None and lds_bytes(g, *p) <= LDS_MAX:
+            return p
+    if spec.C >= 128:
+        return plan(spec)
+    return None
+
+
+def _pro_args(pro, spec):
+    """HconvPro from a dict: mode (0 plain, 1 bn, 2 bn + res, 3 bn + bn2(y2)), the producer's
+    stats [G][2][C] (or rmean/rvar), gamma, beta, act, eps, count (pixels per stat group),
+    group_imgs, res / y2 (+ stats2 / rmean2 / rvar2 / gamma2 / beta2), keep."""
+    if pro is None:
+        return (0,) + (0,) * 13 + (1, 1.0, 1e-5, 0)
+    mode = 1
+    if pro.get('res') is not None:
+        mode = 2
+    if pro.get('y2') is not None:
+        mode = 3
+    n_in = spec.N * spec.H * spec.W * spec.C
+    for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta', 'stats2', 'rmean2', 'rvar2', 'gamma2',
+              'beta2'):
+        _chk(pro.get(k), torch.float32, 'pro.' + k)
+    for k in ('res', 'y2', 'keep'):
+        _chk(pro.get(k), torch.bfloat16, 'pro.' + k, n_in)
+    if pro.get('stats') is None and pro.get('rmean') is None:
+        raise ValueError('pro needs stats or running statistics')
+    if mode == 3 and pro.get('stats2') is None and pro.get('rmean2') is None:
+        raise ValueError('pro with y2 needs stats2 or running statistics 2')
+    gi = pro.get('group_imgs') or spec.N
+    return (mode, ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')),
+            ptr(pro['gamma']), ptr(pro['beta']), ptr(pro.get('res')), ptr(pro.get('y2')),
+            ptr(pro.get('stats2')), ptr(pro.get('rmean2')), ptr(pro.get('rvar2')),
+            ptr(pro.get('gamma2')), ptr(pro.get('beta2')), ptr(pro.get('keep')), gi,
+            1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)), _ACT[pro.get('act')])
+
+
+def keep_ok(spec: ConvSpec):
+    """The kept activation covers every input pixel exactly once (stride-1 same conv, or a
+    padded 3x3 stride-2 conv whose halos tile the input)."""
+    return spec.R == 3 and spec.pad == 1 and spec.H == spec.P * spec.stride \
+        and spec.W == spec.Q * spec.stride
+
+
+def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab=None, pro=None):
+    """out[M][K] = conv(pro(x) NHWC, w [K][R][S][C]) with the fused BN-statistics epilogue."""
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * spec.C)
+    _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * spec.C)
+    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    _chk(bias, torch.float32, 'bias', spec.K)
+    p = plan_ or plan(spec)
+    if p is None:
+        raise ValueError('hconv does not support this conv')
+    bm, bn, splits = p[:3]
+    g = geometry_cached(spec, bm, bn)
+    if g is None or lds_bytes(g, bm, bn, splits) > LDS_MAX:
+        raise ValueError('hconv: tile %dx%d does not fit this conv' % (bm, bn))
+    if pro is not None and pro.get('keep') is not None and not keep_ok(spec):
+        raise ValueError('hconv: keep needs a padded 3x3 conv whose halos tile the input')
+    if splits > 1:
+        need = slab_bytes(spec.M, spec.K, bm, bn, splits)
+        if slab is None or slab.numel() * slab.element_size() < need:
+            raise ValueError('hconv: split-K slab too small')
+    grp = spec.group_rows if spec.group_rows else spec.M
+    lib().hconv(ptr(x), ptr(w), ptr(out), ptr(bias), ptr(stats), grp,
+                ptr(slab) if splits > 1 else 0, [int(g[k]) for k in _ORDER], bm, bn, splits,
+                stream_ptr(), *_pro_args(pro, spec))
+    return out

@@ -55,6 +55,21 @@ class ImportanceTable(object):
                            ptr(out32) if out32 is not None else 0, stream_ptr())
         return out if out is not None else out32
 
+    def draw_batch(self, ndraw, group_dev, pos32, pool_index, Ns, P, idx, isw, seed=0,
+                   meters=None):
+        """Native groupwise step: ``ndraw`` draws from the group stamped ``group_dev`` (device
+        int64) into ``pos32``, then pool slots ``idx`` (the group is the contiguous slice that
+        ``pool_index`` holds) and unbiased weights ``isw = n_group * p`` -- all on the current
+        stream, graph-capturable."""
+        _chk(pos32, torch.int32, 'pos32', ndraw)
+        _chk(idx, torch.int32, 'idx', ndraw)
+        _chk(isw, torch.float32, 'isw', ndraw)
+        _chk(pool_index, torch.int32, 'pool_index', P)
+        self.sample(ndraw, seed=seed, out32=pos32, group_dev=group_dev)
+        lib().table_weights(ptr(pos32), int(ndraw), ptr(self.importance), ptr(self._sc),
+                            ptr(pool_index), int(Ns), int(P), ptr(idx), ptr(isw), ptr(meters),
+                            stream_ptr())
+
     def group_stats(self):
         """(mean importance, member count, total weight) of the last sampled group (syncs)."""
         f = self._sc[:2].view(torch.float32).tolist()

@@ -1,0 +1,162 @@
+"""Halo-tile conv (csrc/hconv.hip) vs a plain PyTorch fp32 reference.
+
+The kernel applies the PRODUCER's BatchNorm (+ identity residual or shortcut BatchNorm) and
+activation while staging its input, so the reference is
+
+    a   = act(bn(y) [+ res | + bn2(y2)])        (fp32 from the bf16 tensors, then bf16)
+    out = conv2d(a, w)                           (fp32 on the bf16-rounded a and w)
+
+with ghost-BN statistics per image group, running statistics (eval), the kept activation
+(equal to ``a`` on every input pixel), the output BN sums of the epilogue, and split-K over
+64-channel slices.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, 'max err %g (scale %g)' % (err, scale)
+
+
+CASES = [
+    # N, H, C, K, R, stride, plan
+    (8, 16, 64, 64, 3, 1, (128, 64, 1)),     # TR rows of one image
+    (8, 16, 128, 64, 3, 1, (64, 64, 2)),     # split over the two 64-channel slices
+    (8, 32, 64, 64, 3, 1, (256, 64, 1)),     # layer1 scoring tile
+    (8, 16, 64, 128, 3, 2, (64, 128, 1)),    # stride 2: even/odd column halves
+    (8, 8, 128, 128, 3, 1, (128, 128, 1)),   # IMG = 2 whole images per tile
+    (16, 4, 128, 128, 3, 1, (64, 128, 2)),   # IMG = 4, split
+    (8, 16, 256, 128, 3, 1, (256, 128, 2)),  # 256 x 128 tile, two slices per split block
+    (4, 8, 192, 64, 3, 1, (64, 64, 1)),      # three slices in one block (halo prefetch)
+]
+
+
+def _bn_ref(y, stats, gamma, beta, cnt, G, running=None, eps=1e-5):
+    N, C = y.shape[0], y.shape[1]
+    yg = y.view(G, N // G, C, *y.shape[2:])
+    if running is not None:
+        mean = running[0].view(1, 1, C, 1, 1)
+        var = running[1].view(1, 1, C, 1, 1)
+    else:
+        mean = (stats[:, 0] / cnt).view(G, 1, C, 1, 1)
+        var = (stats[:, 1] / cnt).view(G, 1, C, 1, 1) - mean ** 2
+    z = (yg - mean) / torch.sqrt(var + eps) * gamma.view(1, 1, C, 1, 1) + beta.view(1, 1, C, 1, 1)
+    return z.view_as(y)
+
+
+@pytest.mark.parametrize('mode', ['plain', 'bn', 'res', 'bn2', 'eval', 'ghost'])
+@pytest.mark.parametrize('case', CASES)
+def test_hconv_modes(case, mode):
+    from mercury_amd import ops
+    from mercury_amd.ops import hconv as H
+    from mercury_amd.ops.conv import ConvSpec, slab_bytes
+    ops.lib()
+    N, Hh, C, K, R, st, plan = case
+    spec = ConvSpec(N, Hh, Hh, C, K, R, R, st, R // 2)
+    gimgs = N // 2 if mode == 'ghost' else 0
+    G = 2 if gimgs else 1
+    if gimgs:
+        spec.group_rows = gimgs * spec.P * spec.Q
+    if H.geometry(spec, plan[0], plan[1]) is None:
+        pytest.skip('tile does not fit')
+    g = torch.Generator(device='cpu').manual_seed(11)
+    y = bf(torch.randn(N, C, Hh, Hh, generator=g) * 1.5 + 0.3).to(DEV)
+    w = bf(torch.randn(K, C, R, R, generator=g) / math.sqrt(C * R * R)).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    cnt = (N // G) * Hh * Hh
+    yg = y.view(G, -1, C, Hh, Hh)
+    stats = torch.stack([yg.sum((1, 3, 4)), yg.pow(2).sum((1, 3, 4))], 1).contiguous()
+    run = ((torch.randn(C, generator=g) * 0.2).to(DEV), (torch.rand(C, generator=g) + 0.5).to(DEV))
+    keep_ok = H.keep_ok(spec)
+    pro = None
+    if mode == 'plain':
+        a = y
+    else:
+        eval_ = mode == 'eval'
+        z = _bn_ref(y, stats, gamma, beta, cnt, G, running=run if eval_ else None)
+        pro = dict(gamma=gamma, beta=beta, act='relu', eps=1e-5, count=cnt,
+                   group_imgs=gimgs or N)
+        if eval_:
+            pro.update(rmean=run[0], rvar=run[1])
+        else:
+            pro.update(stats=stats.reshape(-1))
+        if mode == 'res':
+            res = bf(torch.randn(N, C, Hh, Hh, generator=g)).to(DEV)
+            z = z + res
+            pro['res'] = ops.to_nhwc(res)
+        if mode == 'bn2':
+            y2 = bf(torch.randn(N, C, Hh, Hh, generator=g) * 0.7 - 0.2).to(DEV)
+            y2g = y2.view(G, -1, C, Hh, Hh)
+            st2 = torch.stack([y2g.sum((1, 3, 4)), y2g.pow(2).sum((1, 3, 4))], 1).contiguous()
+            g2 = (torch.rand(C, generator=g) + 0.5).to(DEV)
+            b2 = (torch.randn(C, generator=g) * 0.3).to(DEV)
+            z = z + _bn_ref(y2, st2, g2, b2, cnt, G)
+            pro.update(y2=ops.to_nhwc(y2), stats2=st2.reshape(-1), gamma2=g2, beta2=b2)
+        a = bf(torch.relu(z))
+        if keep_ok:
+            pro['keep'] = torch.full((N, Hh, Hh, C), float('nan'), dtype=torch.bfloat16,
+                                     device=DEV)
+    ref = F.conv2d(a, w, stride=st, padding=R // 2)
+    wk, _ = ops.pack_conv_weight(w)
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    ostats = torch.zeros(G, 2, K, device=DEV)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, K, *plan) // 4 + 1), device=DEV)
+    H.hconv_fwd(ops.to_nhwc(y), wk, out, spec, plan, stats=ostats, slab=slab, pro=pro)
+    torch.cuda.synchronize()
+    got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2)
+    close(got, ref)
+    rb = bf(ref)
+    rg = rb.view(G, -1, K, spec.P, spec.Q)
+    close(ostats[:, 0], rg.sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+    close(ostats[:, 1], rg.pow(2).sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+    if pro is not None and pro.get('keep') is not None:
+        kept = pro['keep'].permute(0, 3, 1, 2).float()
+        assert not torch.isnan(kept).any()
+        close(kept, a, rtol=1e-2, atol=1e-2)
+
+
+def test_hconv_matches_igemm_on_scoring_shapes():
+    """Plain mode at the B=320 layer shapes (10 ghost groups): same output and BN sums as the
+    generic implicit GEMM."""
+    from mercury_amd import ops
+    from mercury_amd.ops import hconv as H
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes
+    ops.lib()
+    for (C, K, Hh, R, st) in [(64, 64, 32, 3, 1), (128, 256, 16, 3, 2), (256, 256, 8, 3, 1),
+                              (512, 512, 4, 3, 1), (128, 128, 16, 3, 1)]:
+        spec = ConvSpec(320, Hh, Hh, C, K, R, R, st, R // 2)
+        spec.group_rows = 32 * spec.P * spec.Q
+        plan = H.plan(spec)
+        assert plan is not None, (C, K, Hh)
+        g = torch.Generator(device='cpu').manual_seed(3)
+        x = ops.to_nhwc(bf(torch.randn(320, C, Hh, Hh, generator=g)).to(DEV))
+        wk, _ = ops.pack_conv_weight(bf(torch.randn(K, C, R, R, generator=g) * 0.05).to(DEV))
+        outs, sts = [], []
+        for use_h in (False, True):
+            out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+            stt = torch.zeros(10, 2, K, device=DEV)
+            p = plan if use_h else fwd_plan(spec)
+            slab = torch.zeros(max(1, slab_bytes(spec.M, K, *p[:3]) // 4 + 1), device=DEV)
+            if use_h:
+                H.hconv_fwd(x, wk, out, spec, p, stats=stt, slab=slab)
+            else:
+                ops.conv_fwd(x, wk, out, spec, stats=stt, slab=slab, plan=p)
+            outs.append(out)
+            sts.append(stt)
+        torch.cuda.synchronize()
+        close(outs[1], outs[0], rtol=1e-2, atol=1e-2)
+        close(sts[1], sts[0], rtol=1e-3, atol=0.5)
