@@ -130,7 +130,12 @@ class NativeEngine(object):
         # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
         self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
         # stride-1 3x3 forward convs on the halo-tile kernel (csrc/hconv.hip) where measured faster
-        self.use_hconv = os.environ.get('MERCURY_HCONV', '1') == '1'
+        # ('1' both batch modes, 'score' / 'train' one of them, '0' off).  Default: the scoring
+        # pass only -- same-box A/B of the two-stream step (profiles/r2/ab_hconv_modes.json):
+        # off 1.614, score 1.605, train 1.615, both 1.640 ms/step.  The halo conv's one-wave-
+        # per-SIMD blocks are faster alone but crowd the concurrently running train kernels out
+        # of the CUs they share
+        self.use_hconv = os.environ.get('MERCURY_HCONV', 'score')
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
         self.sampler = sampler
@@ -258,7 +263,8 @@ class NativeEngine(object):
                         sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
                     # stride-1 3x3 convs on the halo-tile kernel where it measured faster
-                    hp = hconv.engine_plan(sp) if self.use_hconv else None
+                    uh = self.use_hconv == '1' or self.use_hconv == ('train' if train else 'score')
+                    hp = hconv.engine_plan(sp) if uh else None
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
