@@ -78,7 +78,7 @@ def diagnostics(eng, steps, ws):
     out = {'device_phase_ms': {k: med[k] for k in ('step', 'critical', 'score', 'train', 'wait',
                                                    'tail') if k in med}}
     dp = {'backend': dist.get_backend() if dist.is_initialized() else None,
-          'comm': 'rccl' if eng.comm is not None else ('pg' if eng.dp else None),
+          'comm': eng.comm_kind,
           'comm_ranks': eng.comm.size if eng.comm is not None else
           (dist.get_world_size() if dist.is_initialized() else 1),
           'buckets_bytes': [4 * (e - s) for s, e in sorted(plan.values(), reverse=True)],
@@ -109,9 +109,9 @@ def main():
     ap.add_argument('--no-graphs', action='store_true')
     ap.add_argument('--force-buckets', action='store_true',
                     help='issue the RCCL bucket all-reduces even at one GPU (path check)')
-    ap.add_argument('--comm', default='auto', choices=('auto', 'rccl', 'pg'),
-                    help='DP all-reduce: own RCCL communicator on a comm stream, or the torch '
-                         'ProcessGroup')
+    ap.add_argument('--comm', default='auto', choices=('auto', 'rccl', 'xgmi', 'pg'),
+                    help='DP all-reduce: own RCCL communicator on a comm stream, the direct-xGMI '
+                         'two-shot over IPC-mapped peer buffers, or the torch ProcessGroup')
     ap.add_argument('--wire-bf16', action='store_true', help='bf16 gradients on the wire')
     ap.add_argument('--sampler', default='alias', choices=('alias', 'cdf', 'groupwise'),
                     help="pool draw kernel, or 'groupwise': draws from the HBM importance table "

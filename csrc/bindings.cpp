@@ -27,6 +27,18 @@ void comm_broadcast(uintptr_t c, uintptr_t buf, long long count, int dtype, int 
 void comm_ring_allreduce(uintptr_t c, uintptr_t buf, long long count, uintptr_t work, int avg,
                          uintptr_t st);
 void add_f32(float* dst, const float* src, long long n, hipStream_t s);
+// direct-xGMI two-shot all-reduce (xgmi.hip)
+void xgmi_pack(const float* src, void* xbuf, long long n, int bf, hipStream_t st);
+void xgmi_reduce_scatter(const void* const* peers, int W, int rank, long long n, int bf,
+                         float scale, hipStream_t st);
+void xgmi_all_gather(const void* const* peers, int W, long long n, int bf, float* dst,
+                     hipStream_t st);
+int xgmi_max_ranks();
+std::string xgmi_ipc_handle(uintptr_t ptr);
+uintptr_t xgmi_ipc_open(const std::string& handle);
+uintptr_t xgmi_malloc(long long bytes);
+void xgmi_free(uintptr_t p);
+void xgmi_ipc_close(uintptr_t p);
 void order_check_launch(int* o, int slot, int ref, int mult, int add, int ge, int tick, int at,
                         hipStream_t st);
 
@@ -136,6 +148,33 @@ PYBIND11_MODULE(_C, m) {
     comm_ring_allreduce(c, buf, count, work, avg, st);
     check_launch("comm_ring_allreduce");
   });
+  m.def("xgmi_pack", [](uintptr_t src, uintptr_t xbuf, long long n, int bf, uintptr_t st) {
+    xgmi_pack(P<const float>(src), P<void>(xbuf), n, bf, S(st));
+    check_launch("xgmi_pack");
+  });
+  m.def("xgmi_reduce_scatter", [](const std::vector<uintptr_t>& peers, int rank, long long n,
+                                  int bf, float scale, uintptr_t st) {
+    if (peers.empty() || (int)peers.size() > xgmi_max_ranks() || n % 4)
+      throw std::invalid_argument("xgmi_reduce_scatter: 1..8 peers, n % 4 == 0");
+    std::vector<const void*> p(peers.size());
+    for (size_t i = 0; i < peers.size(); ++i) p[i] = P<const void>(peers[i]);
+    xgmi_reduce_scatter(p.data(), (int)p.size(), rank, n, bf, scale, S(st));
+    check_launch("xgmi_reduce_scatter");
+  });
+  m.def("xgmi_all_gather", [](const std::vector<uintptr_t>& peers, long long n, int bf,
+                              uintptr_t dst, uintptr_t st) {
+    if (peers.empty() || (int)peers.size() > xgmi_max_ranks() || n % 4)
+      throw std::invalid_argument("xgmi_all_gather: 1..8 peers, n % 4 == 0");
+    std::vector<const void*> p(peers.size());
+    for (size_t i = 0; i < peers.size(); ++i) p[i] = P<const void>(peers[i]);
+    xgmi_all_gather(p.data(), (int)p.size(), n, bf, P<float>(dst), S(st));
+    check_launch("xgmi_all_gather");
+  });
+  m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(xgmi_ipc_handle(p)); });
+  m.def("xgmi_ipc_open", [](py::bytes h) { return xgmi_ipc_open(std::string(h)); });
+  m.def("xgmi_ipc_close", &xgmi_ipc_close);
+  m.def("xgmi_malloc", &xgmi_malloc);
+  m.def("xgmi_free", &xgmi_free);
   m.def("add_f32", [](uintptr_t dst, uintptr_t src, long long n, uintptr_t st) {
     add_f32(P<float>(dst), P<const float>(src), n, S(st));
     check_launch("add_f32");
@@ -326,6 +365,16 @@ PYBIND11_MODULE(_C, m) {
               total, P<const float>(hyper), P<const int64_t>(step), algo, zero_grad, start};
     optimizer_launch(a, S(st));
     check_launch("optimizer");
+  });
+  m.def("optimizer_fused", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t segs,
+                              int nsegs, long long total, uintptr_t hyper, uintptr_t step,
+                              int algo, int zero_grad, uintptr_t jobs, int njobs, uintptr_t ew,
+                              uintptr_t ewp, int new_, long long ew4, uintptr_t st) {
+    OptArgs a{P<float>(p), P<float>(g), P<float>(mm), P<float>(v), P<const OptSeg>(segs), nsegs,
+              total, P<const float>(hyper), P<const int64_t>(step), algo, zero_grad, 0};
+    optimizer_fused_launch(a, P<const int>(jobs), njobs, P<const long long>(ew),
+                           P<const long long>(ewp), new_, ew4, S(st));
+    check_launch("optimizer_fused");
   });
   m.def("pack_weights", [](uintptr_t p, uintptr_t segs, int nsegs, long long total, uintptr_t st) {
     pack_weights_launch(P<const float>(p), P<const OptSeg>(segs), nsegs, total, S(st));

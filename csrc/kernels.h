@@ -199,6 +199,10 @@ struct OptArgs {
   long long start;               // first element of the swept range (4-aligned segment start)
 };
 void optimizer_launch(const OptArgs& a, hipStream_t st);
+// full step in one launch: tile jobs (conv segments with a dgrad copy, C % 4 == 0) write both
+// bf16 copies; ew ([n][2] start, numel) / ewp ([n+1] float4 prefix) cover everything else
+void optimizer_fused_launch(const OptArgs& a, const int* jobs, int njobs, const long long* ew,
+                            const long long* ewp, int new_, long long ew4, hipStream_t st);
 void step_begin_launch(int64_t* ctrl, float* z0, int n0, float* z1, int n1, hipStream_t st);
 // jobs: [njobs][4] = (segment index, r*S+s, k0, c0) -> one 64x64 tile each
 void transpose_weights_launch(const OptSeg* segs, const int* jobs, int njobs, hipStream_t st);

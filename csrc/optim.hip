@@ -72,13 +72,28 @@ __global__ __launch_bounds__(256) void transpose_weights_kernel(const OptSeg* se
   }
 }
 
-__global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
-  const long long i4 = (long long)blockIdx.x * NT + threadIdx.x;
-  const long long e = a.start + i4 * 4;
-  if (e >= a.total) return;
-  const int si = find_seg(a.segs, a.nsegs, e);
-  const OptSeg sg = a.segs[si];
-  const float lr = a.hyper[0], b1 = a.hyper[1], b2 = a.hyper[2], eps = a.hyper[3], wd = a.hyper[4];
+// Adam / AdamW / SGD-momentum on 4 consecutive elements (the flat layout keeps segments
+// 4-aligned, so a float4 never straddles two parameters)
+struct OptHyper {
+  float lr, b1, b2, eps, wd, step_size, rbc2;
+  bool first;
+};
+
+MA_DEV OptHyper opt_hyper(const OptArgs& a) {
+  OptHyper h;
+  h.lr = a.hyper[0];
+  h.b1 = a.hyper[1];
+  h.b2 = a.hyper[2];
+  h.eps = a.hyper[3];
+  h.wd = a.hyper[4];
+  const float t = (float)(*a.step);
+  h.step_size = h.lr / (1.f - __powf(h.b1, t));
+  h.rbc2 = rsqrtf(1.f - __powf(h.b2, t));
+  h.first = *a.step <= 1;
+  return h;
+}
+
+MA_DEV float4 opt_update4(const OptArgs& a, const OptHyper& h, long long e) {
   float4 p = *(const float4*)(a.p + e);
   float4 g = *(const float4*)(a.g + e);
   float4 m = *(const float4*)(a.m + e);
@@ -86,51 +101,135 @@ __global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
   if (a.algo == 0 || a.algo == 2) {
     float4 v = *(const float4*)(a.v + e);
     float vv[4] = {v.x, v.y, v.z, v.w};
-    const float t = (float)(*a.step);
-    const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
-    const float step_size = lr / bc1, rbc2 = rsqrtf(bc2);
     const bool decoupled = a.algo == 2;   // AdamW: p *= 1 - lr*wd before the Adam update
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gv[k];
-      if (decoupled) pv[k] *= 1.f - lr * wd;
-      else if (wd != 0.f) gk += wd * pv[k];
-      mv[k] = b1 * mv[k] + (1.f - b1) * gk;
-      vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
-      const float denom = sqrtf(vv[k]) * rbc2 + eps;
-      pv[k] -= step_size * mv[k] / denom;
+      if (decoupled) pv[k] *= 1.f - h.lr * h.wd;
+      else if (h.wd != 0.f) gk += h.wd * pv[k];
+      mv[k] = h.b1 * mv[k] + (1.f - h.b1) * gk;
+      vv[k] = h.b2 * vv[k] + (1.f - h.b2) * gk * gk;
+      const float denom = sqrtf(vv[k]) * h.rbc2 + h.eps;
+      pv[k] -= h.step_size * mv[k] / denom;
     }
     *(float4*)(a.v + e) = make_float4(vv[0], vv[1], vv[2], vv[3]);
   } else {
-    const float mom = b1;
-    const bool first = *a.step <= 1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gv[k];
-      if (wd != 0.f) gk += wd * pv[k];
-      mv[k] = first ? gk : mom * mv[k] + gk;
-      pv[k] -= lr * mv[k];
+      if (h.wd != 0.f) gk += h.wd * pv[k];
+      mv[k] = h.first ? gk : h.b1 * mv[k] + gk;
+      pv[k] -= h.lr * mv[k];
     }
   }
-  *(float4*)(a.p + e) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  const float4 pn = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  *(float4*)(a.p + e) = pn;
   *(float4*)(a.m + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
   if (a.zero_grad) *(float4*)(a.g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (sg.kind == 1) {
-    const long long local = e - sg.off;
-    if ((sg.C & 3) == 0 && local + 3 < sg.numel) {  // 4 consecutive channels: one 8-B store
-      const int rsc = sg.R * sg.S * sg.C;
-      const int k = (int)(local / rsc);
-      const int rem = (int)(local - (long long)k * rsc);
-      const int rs = rem / sg.C, c = rem - rs * sg.C;
-      bf16x4 b;
+  return pn;
+}
+
+MA_DEV void write_krsc4(const OptSeg& sg, long long local, const float4& pn) {
+  const float pv[4] = {pn.x, pn.y, pn.z, pn.w};
+  if ((sg.C & 3) == 0 && local + 3 < sg.numel) {  // 4 consecutive channels: one 8-B store
+    const int rsc = sg.R * sg.S * sg.C;
+    const int k = (int)(local / rsc);
+    const int rem = (int)(local - (long long)k * rsc);
+    const int rs = rem / sg.C, c = rem - rs * sg.C;
+    bf16x4 b;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = f2bf(pv[q]);
-      *(bf16x4*)(sg.w_krsc + ((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c) = b;
-    } else {
+    for (int q = 0; q < 4; ++q) b[q] = f2bf(pv[q]);
+    *(bf16x4*)(sg.w_krsc + ((size_t)k * sg.R * sg.S + rs) * sg.Cpad + c) = b;
+  } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) write_copies(sg, local + q, pv[q]);
-    }
+    for (int q = 0; q < 4; ++q) write_copies(sg, local + q, pv[q]);
   }
+}
+
+__global__ __launch_bounds__(NT) void optimizer_kernel(OptArgs a) {
+  const long long i4 = (long long)blockIdx.x * NT + threadIdx.x;
+  const long long e = a.start + i4 * 4;
+  if (e >= a.total) return;
+  const int si = find_seg(a.segs, a.nsegs, e);
+  const OptSeg sg = a.segs[si];
+  const float4 pn = opt_update4(a, opt_hyper(a), e);
+  if (sg.kind == 1) write_krsc4(sg, e - sg.off, pn);
+}
+
+// The whole step in ONE launch, with the dgrad weight copy produced from the update itself
+// (no separate transpose kernel re-reading the bf16 forward copy with 2-byte accesses):
+//   blocks [0, njobs)  : one 64(k) x 64(c) tile of one (conv segment, r*S+s) each -- 16 rows of
+//                        4 float4 per thread, coalesced 256-B rows of p/g/m/v, the bf16 [K][R][S]
+//                        [Cpad] copy from registers, and the [C][R][S][K] copy through an LDS
+//                        transpose written as 16-byte chunks of 8 k;
+//   blocks [njobs, ..) : every other element (BN / fc / conv segments the tiles do not cover),
+//                        float4 per thread over the concatenated ranges `ew` ([n][2] = start,
+//                        numel; prefix sums in float4 units in `ewp`).
+__global__ __launch_bounds__(NT) void optimizer_fused_kernel(OptArgs a, const int* jobs, int njobs,
+                                                             const long long* ew,
+                                                             const long long* ewp, int new_) {
+  const OptHyper h = opt_hyper(a);
+  if ((int)blockIdx.x < njobs) {
+    __shared__ float tile[64][65];
+    const int* j = jobs + blockIdx.x * 4;
+    const OptSeg sg = a.segs[j[0]];
+    const int rs = j[1], k0 = j[2], c0 = j[3];
+    const int RS = sg.R * sg.S;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 float4 columns x 16 rows
+    const int c = c0 + tx * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = ty + 16 * i, k = k0 + r;
+      float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < sg.K && c < sg.C) {                 // host: C % 4 == 0, so c < C => c + 3 < C
+        const long long local = ((long long)k * RS + rs) * sg.C + c;
+        pn = opt_update4(a, h, sg.off + local);
+        bf16x4 b;
+        b[0] = f2bf(pn.x);
+        b[1] = f2bf(pn.y);
+        b[2] = f2bf(pn.z);
+        b[3] = f2bf(pn.w);
+        *(bf16x4*)(sg.w_krsc + ((size_t)k * RS + rs) * sg.Cpad + c) = b;
+      }
+      tile[r][tx * 4 + 0] = pn.x;
+      tile[r][tx * 4 + 1] = pn.y;
+      tile[r][tx * 4 + 2] = pn.z;
+      tile[r][tx * 4 + 3] = pn.w;
+    }
+    __syncthreads();
+    // [C][R][S][K]: row (c, rs) holds k contiguous -> 8 chunks of 8 k per 64-k tile row
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = threadIdx.x + NT * i;         // 512 chunks = 64 c x 8
+      const int cr = q >> 3, kc = (q & 7) * 8;
+      const int cc = c0 + cr, kk = k0 + kc;
+      if (cc < sg.C && kk < sg.K) {
+        bf16x8 o;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) o[t] = f2bf(tile[kc + t][cr]);
+        bf16* dst = sg.w_crsk + ((size_t)cc * RS + rs) * sg.K + kk;
+        if (kk + 8 <= sg.K && (sg.K & 7) == 0) {
+          *(bf16x8*)dst = o;
+        } else {
+          for (int t = 0; t < 8 && kk + t < sg.K; ++t) dst[t] = o[t];
+        }
+      }
+    }
+    return;
+  }
+  // elementwise remainder
+  const long long v4 = (long long)(blockIdx.x - njobs) * NT + threadIdx.x;
+  if (v4 >= ewp[new_]) return;
+  int lo = 0, hi = new_ - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ewp[mid] <= v4) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long e = ew[2 * lo] + (v4 - ewp[lo]) * 4;
+  const float4 pn = opt_update4(a, h, e);
+  const OptSeg sg = a.segs[find_seg(a.segs, a.nsegs, e)];
+  if (sg.kind == 1) write_krsc4(sg, e - sg.off, pn);
 }
 
 __global__ __launch_bounds__(NT) void pack_kernel(const float* p, const OptSeg* segs, int nsegs,
@@ -157,6 +256,14 @@ void optimizer_launch(const OptArgs& a, hipStream_t st) {
   if (a.total <= a.start) return;
   const long long n4 = (a.total - a.start + 3) / 4;
   hipLaunchKernelGGL(optimizer_kernel, dim3((unsigned)((n4 + NT - 1) / NT)), dim3(NT), 0, st, a);
+}
+
+void optimizer_fused_launch(const OptArgs& a, const int* jobs, int njobs, const long long* ew,
+                            const long long* ewp, int new_, long long ew4, hipStream_t st) {
+  const long long blocks = njobs + (ew4 + NT - 1) / NT;
+  if (blocks > 0)
+    hipLaunchKernelGGL(optimizer_fused_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, a, jobs,
+                       njobs, ew, ewp, new_);
 }
 
 void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long long total,

@@ -53,6 +53,7 @@ class Config:
     overlap: bool = True            # scoring of step t+1 overlaps backward/all-reduce of step t
     use_graphs: bool = True
     comm: str = 'auto'              # native DP all-reduce: 'rccl' (own communicator + comm stream),
+                                    # 'xgmi' (direct two-shot over IPC-mapped peer buffers),
                                     # 'pg' (torch ProcessGroup), 'auto' (rccl on nccl backends)
     force_buckets: bool = False     # issue the bucket all-reduces even at world size 1
     # debug / race detection

@@ -98,12 +98,14 @@ class NativeEngine(object):
             self._avg_op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM
             if comm == 'auto':
                 comm = 'rccl' if nccl else 'pg'
-            if comm == 'rccl':
+            if comm in ('rccl', 'xgmi'):
                 from ..parallel.rccl import RcclComm
                 self.comm = RcclComm.shared()
                 self.s_comm = torch.cuda.Stream(self.device)
             elif comm != 'pg':
-                raise ValueError("comm must be 'auto', 'rccl' or 'pg'")
+                raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
+        self.comm_kind = comm if self.dp else None
+        self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
         self.units = []
         for blk in self.lw.blocks:
@@ -161,6 +163,10 @@ class NativeEngine(object):
         self.check_order = check_order or debug
         self.order = torch.zeros(16, dtype=torch.int32, device=self.device)
         self.debug_log = os.environ.get('MERCURY_DEBUG_LOG', '0') == '1'
+        if self.comm_kind == 'xgmi':
+            from ..parallel.xgmi import XgmiAllReduce
+            cap = max(e - s_ for s_, e in self.bucket_plan().values())
+            self.xgmi = XgmiAllReduce(cap, self.device, wire_bf16=wire_bf16)
 
     # ------------------------------------------------------------------ parameters
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
@@ -963,7 +969,11 @@ class NativeEngine(object):
                 # the bucket's gradients are final: train segment si has ticked this step
                 self._order(slot=2, ref=3, mult=self._nseg, add=si + 1, ge=True, at=6)
             self.timer.bucket(i, 0, self.s_comm)
-            if self.wire_bf16:
+            if self.xgmi is not None:
+                # direct two-shot over xGMI (all peers' exchange buffers mapped by IPC); the
+                # bf16 wire option lives in its exchange buffers
+                self.xgmi.allreduce(g, avg=True)
+            elif self.wire_bf16:
                 # bf16 on the wire: half the bytes over xGMI; the sum is rounded once per hop
                 if self.wire is None:
                     self.wire = torch.empty(self.lw.total, dtype=torch.bfloat16,

@@ -9,6 +9,8 @@ is one launch; ``set_lr`` is a 4-byte host->device copy done outside graphs
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import lib, ptr, stream_ptr
@@ -97,6 +99,34 @@ class FlatOptimizer(object):
         self._job_off = [segments[j[0]]['off'] for j in jobs]
         self.jobs = torch.tensor(jobs if jobs else [(0, 0, 0, 0)], dtype=torch.int32,
                                  device=device).contiguous()
+        # fused full step (csrc/optim.hip optimizer_fused_kernel): 64x64 update tiles for conv
+        # segments that carry a dgrad copy (their [C][R][S][K] copy is written from the update),
+        # float4 elementwise ranges for everything else
+        fjobs, ew = [], []
+        for i, s in enumerate(segments):
+            if s['kind'] == 1 and s.get('w_crsk') is not None and s['C'] % 4 == 0:
+                for rs in range(s['R'] * s['S']):
+                    for k0 in range(0, s['K'], 64):
+                        for c0 in range(0, s['C'], 64):
+                            fjobs.append((i, rs, k0, c0))
+            else:
+                ew.append((int(s['off']), (int(s['numel']) + 3) // 4 * 4))
+        pre = [0]
+        for _, n in ew:
+            pre.append(pre[-1] + n // 4)
+        self.fused = os.environ.get('MERCURY_FUSED_OPT', '1') == '1'
+        self.n_fjobs = len(fjobs)
+        self.fjobs = torch.tensor(fjobs if fjobs else [(0, 0, 0, 0)], dtype=torch.int32,
+                                  device=device).contiguous()
+        self.ew = torch.tensor(ew if ew else [(0, 0)], dtype=torch.int64, device=device)
+        self.ewp = torch.tensor(pre, dtype=torch.int64, device=device)
+        self.n_ew, self.ew4 = len(ew), pre[-1]
+        # dgrad copies of conv segments the tiles do not cover still go through the transpose
+        fused_segs = set(j[0] for j in fjobs)
+        rest = [j for j in jobs if j[0] not in fused_segs]
+        self.n_rest = len(rest)
+        self.rest_jobs = torch.tensor(rest if rest else [(0, 0, 0, 0)], dtype=torch.int32,
+                                      device=device).contiguous()
 
     def _transpose(self, start=0, end=None):
         end = self.total if end is None else end
@@ -121,6 +151,16 @@ class FlatOptimizer(object):
         for b in (start, end):
             if b != self.total and b not in self._seg_starts:
                 raise ValueError('optimizer range bound %d is not a segment start' % b)
+        if self.fused and start == 0 and end == self.total:
+            lib().optimizer_fused(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v),
+                                  ptr(self.segbuf), self.nsegs, self.total, ptr(self.hyper),
+                                  ptr(step_counter), self.algo, int(zero_grad), ptr(self.fjobs),
+                                  self.n_fjobs, ptr(self.ew), ptr(self.ewp), self.n_ew, self.ew4,
+                                  stream_ptr())
+            if self.n_rest:
+                lib().transpose_weights(ptr(self.segbuf), ptr(self.rest_jobs), self.n_rest,
+                                        stream_ptr())
+            return
         lib().optimizer(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), ptr(self.segbuf),
                         self.nsegs, end, ptr(self.hyper), ptr(step_counter), self.algo,
                         int(zero_grad), stream_ptr(), start)

@@ -1,0 +1,133 @@
+"""Direct-xGMI two-shot all-reduce (``csrc/xgmi.hip``).
+
+The reference reduces gradients with a hand-written CPU ring (`util.py:280-324`); RCCL's ring
+algorithms are the GPU analogue and are per-link bound on MI355X's point-to-point xGMI (a ring
+step moves every byte over one of the 7 links).  ``XgmiAllReduce`` instead maps every peer's
+exchange buffer into this process (``hipIpcGetMemHandle`` / ``hipIpcOpenMemHandle``) and
+reduces in two direct passes that pull from all peers at once:
+
+    pack            own gradients -> own exchange buffer (fp32, or bf16 with ``wire_bf16``)
+    barrier         every rank's buffer is filled
+    reduce-scatter  rank r sums chunk r over all W buffers (W-1 remote reads in parallel)
+                    and writes it back into its own buffer
+    barrier         every chunk is reduced
+    all-gather      chunk p of peer p -> local gradients, for every p
+    barrier         no rank refills its buffer while a peer still reads it
+
+The barriers are stream-ordered (a one-element all-reduce on the framework's own RCCL
+communicator, on the same stream) so nothing waits on the host; tests on one GPU use host
+barriers and emulated peers (``emulated_allreduce``: W local buffers stand for W ranks).
+RCCL stays the engine default (``comm='rccl'``); ``comm='xgmi'`` selects this path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops import lib, ptr, stream_ptr
+
+MAX_RANKS = 8
+
+
+class XgmiAllReduce(object):
+
+    def __init__(self, capacity, device, group=None, wire_bf16=False, barrier='rccl'):
+        if capacity % 4:
+            capacity += 4 - capacity % 4
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.group = group
+        init = dist.is_initialized()
+        self.rank = dist.get_rank(group) if init else 0
+        self.size = dist.get_world_size(group) if init else 1
+        if self.size > MAX_RANKS:
+            raise ValueError('xgmi all-reduce: at most %d ranks (one node)' % MAX_RANKS)
+        self.bf16 = bool(wire_bf16)
+        L = lib()
+        self.buf = L.xgmi_malloc(self.capacity * (2 if self.bf16 else 4))
+        if not self.buf:
+            raise RuntimeError('xgmi all-reduce: exchange buffer allocation failed')
+        self._opened = []
+        if self.size > 1:
+            h = L.xgmi_ipc_handle(self.buf)
+            if not h:
+                raise RuntimeError('hipIpcGetMemHandle failed (HSA_ENABLE_IPC_MODE_LEGACY=0 '
+                                   'must be set for dmabuf IPC)')
+            hs = [None] * self.size
+            dist.all_gather_object(hs, h, group=group)
+            peers = []
+            for r, hr in enumerate(hs):
+                if r == self.rank:
+                    peers.append(self.buf)
+                    continue
+                p = L.xgmi_ipc_open(hr)
+                if not p:
+                    raise RuntimeError('hipIpcOpenMemHandle failed for rank %d' % r)
+                self._opened.append(p)
+                peers.append(p)
+            self.peers = peers
+        else:
+            self.peers = [self.buf]
+        self.barrier_kind = barrier
+        self._comm = None
+        self._tick = torch.zeros(4, dtype=torch.float32, device=self.device)
+        if barrier == 'rccl' and self.size > 1:
+            from .rccl import RcclComm
+            self._comm = RcclComm.shared(group)
+
+    def barrier(self):
+        """Every rank reaches this point of its stream (no host wait for 'rccl')."""
+        if self.size == 1:
+            return
+        if self.barrier_kind == 'rccl':
+            self._comm.allreduce(self._tick, avg=False)
+        else:
+            torch.cuda.current_stream(self.device).synchronize()
+            dist.barrier(group=self.group)
+
+    def allreduce(self, t, avg=True):
+        """In-place all-reduce of a contiguous fp32 device tensor (numel % 4 == 0)."""
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError('xgmi all-reduce: contiguous fp32 device tensor expected')
+        n = t.numel()
+        if n % 4 or n > self.capacity:
+            raise ValueError('xgmi all-reduce: numel %d (capacity %d, multiple of 4)'
+                             % (n, self.capacity))
+        L, st, bf = lib(), stream_ptr(), int(self.bf16)
+        L.xgmi_pack(ptr(t), self.buf, n, bf, st)
+        self.barrier()
+        L.xgmi_reduce_scatter(self.peers, self.rank, n, bf,
+                              1.0 / self.size if avg else 1.0, st)
+        self.barrier()
+        L.xgmi_all_gather(self.peers, n, bf, ptr(t), st)
+        self.barrier()
+        return t
+
+    def close(self):
+        L = lib()
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            L.xgmi_ipc_close(p)
+        self._opened = []
+        if self.buf:
+            L.xgmi_free(self.buf)
+            self.buf = 0
+
+
+def emulated_allreduce(tensors, avg=True, wire_bf16=False):
+    """The two-shot algorithm with W local buffers as the W ranks' exchange buffers (one GPU).
+    Returns one reduced copy per emulated rank (each produced by that rank's all-gather)."""
+    W = len(tensors)
+    n = tensors[0].numel()
+    L, st, bf = lib(), stream_ptr(), int(wire_bf16)
+    dt = torch.bfloat16 if wire_bf16 else torch.float32
+    xb = [torch.zeros(n, dtype=dt, device=tensors[0].device) for _ in range(W)]
+    peers = [ptr(b) for b in xb]
+    for r in range(W):
+        L.xgmi_pack(ptr(tensors[r]), peers[r], n, bf, st)
+    for r in range(W):
+        L.xgmi_reduce_scatter(peers, r, n, bf, 1.0 / W if avg else 1.0, st)
+    outs = [torch.empty(n, dtype=torch.float32, device=tensors[0].device) for _ in range(W)]
+    for r in range(W):
+        L.xgmi_all_gather(peers, n, bf, ptr(outs[r]), st)
+    return outs

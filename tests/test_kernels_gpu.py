@@ -567,6 +567,59 @@ def test_fused_adam_matches_torch_and_writes_bf16_copies():
         opt.step(step, start=3)          # not a segment start
 
 
+@pytest.mark.parametrize('algo', ['adam', 'adamw', 'sgd'])
+def test_fused_optimizer_tiles_match_torch(algo):
+    """The one-launch step (64x64 update tiles writing both bf16 copies + elementwise rest):
+    partial k / c tiles, a C % 4 != 0 conv (elementwise + transpose), a plain vector."""
+    ops = _ops()
+    torch.manual_seed(1)
+    convs = [torch.randn(80, 96, 3, 3, device=DEV) * 0.1,     # partial k and c tiles
+             torch.randn(128, 64, 1, 1, device=DEV) * 0.1,
+             torch.randn(16, 6, 3, 3, device=DEV) * 0.1]      # C % 4 != 0
+    vec = torch.randn(10, device=DEV)
+    segs, off = [], 0
+    copies = []
+    for w in convs:
+        k, c, r, s_ = w.shape
+        krsc = torch.zeros(k, r, s_, c, dtype=torch.bfloat16, device=DEV)
+        crsk = torch.zeros(c, r, s_, k, dtype=torch.bfloat16, device=DEV)
+        segs.append(dict(off=off, numel=w.numel(), kind=1, K=k, R=r, S=s_, C=c, Cpad=c,
+                         w_krsc=krsc, w_crsk=crsk))
+        copies.append((krsc, crsk))
+        off += (w.numel() + 3) // 4 * 4
+    segs.append(dict(off=off, numel=10, kind=0))
+    total = off + 12
+    kw = dict(lr=1e-2, weight_decay=0.01)
+    opt = ops.FlatOptimizer(segs, total, DEV, algo, momentum=0.9, **kw)
+    assert opt.n_fjobs > 0 and opt.n_rest > 0
+    for sg, w in zip(segs, convs):
+        opt.p[sg['off']:sg['off'] + w.numel()] = w.permute(0, 2, 3, 1).reshape(-1)
+    opt.p[off:off + 10] = vec
+    ref = [w.clone().requires_grad_(True) for w in convs] + [vec.clone().requires_grad_(True)]
+    topt = {'adam': lambda: torch.optim.Adam(ref, **kw),
+            'adamw': lambda: torch.optim.AdamW(ref, **kw),
+            'sgd': lambda: torch.optim.SGD(ref, momentum=0.9, **kw)}[algo]()
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for t in range(4):
+        gs = [torch.randn_like(r_) for r_ in ref]
+        for r_, g_ in zip(ref, gs):
+            r_.grad = g_.clone()
+        topt.step()
+        for sg, g_ in zip(segs[:-1], gs[:-1]):
+            opt.g[sg['off']:sg['off'] + g_.numel()] = g_.permute(0, 2, 3, 1).reshape(-1)
+        opt.g[off:off + 10] = gs[-1]
+        step += 1
+        opt.step(step)
+        assert opt.g.abs().max().item() == 0
+    for sg, w, r_, (krsc, crsk) in zip(segs, convs, ref, copies):
+        k, c, r, s_ = w.shape
+        got = opt.p[sg['off']:sg['off'] + w.numel()].view(k, r, s_, c).permute(0, 3, 1, 2)
+        close(got, r_.detach(), 1e-5, 1e-6)
+        close(krsc.float(), r_.detach().permute(0, 2, 3, 1), 1e-2, 1e-3)
+        close(crsk.float(), r_.detach().permute(1, 2, 3, 0), 1e-2, 1e-3)
+    close(opt.p[off:off + 10], ref[-1].detach(), 1e-5, 1e-6)
+
+
 def test_quantize_pool_dwconv():
     ops = _ops()
     x = torch.randn(100000, device=DEV)
