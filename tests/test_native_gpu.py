@@ -25,7 +25,7 @@ def _engine(net, hw=32, **kw):
 
 
 @pytest.mark.parametrize('arch,hw', [('resnet18', 32), ('resnet50', 32), ('mobilenetv2', 32),
-                                     ('resnet50_imagenet', 64)])
+                                     ('resnet50_imagenet', 64), ('resnet50_imagenet', 224)])
 def test_train_forward_backward_matches_torch(arch, hw):
     """Every supported family incl. the ImageNet stem (7x7/2 conv + 3x3/2 max-pool)."""
     from mercury_amd import ops
