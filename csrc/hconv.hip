@@ -40,35 +40,49 @@ namespace {
 constexpr int NSLOT = 3;     // weight ring slots (prefetch distance 2)
 constexpr int HRMAX = 16;    // halo DMA pieces per wave (32 pixels per piece over 4 waves)
 
-MA_DEV float act_f(float v, int act) {
-  if (act == 1) return fmaxf(v, 0.f);
-  if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
-  return v;
+// Activation as one clamp [lo, hi] (none: -inf..inf, relu: 0..inf, relu6: 0..6) -- branch-free:
+// a per-element if-chain on the kernel-uniform selector compiled to two scalar branches per
+// element (255 in one halo transform, ~3x the transform's cost)
+MA_DEV void act_bounds(int act, float& lo, float& hi) {
+  lo = act == 0 ? -__builtin_huge_valf() : 0.f;
+  hi = act == 2 ? 6.f : __builtin_huge_valf();
 }
 
-// per-channel scale / shift of one BatchNorm for 8 channels (same arithmetic as bn.hip)
-MA_DEV void bn_coef8(const float* stats, const float* rmean, const float* rvar, const float* gamma,
-                     const float* beta, int C, int g, int ch, float inv_count, float eps,
-                     float (&sc)[8], float (&sh)[8]) {
-  float mean[8], var[8];
-  if (stats) {
-    const float* s = stats + (size_t)g * 2 * C + ch;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mean[k] = s[k] * inv_count;
-      var[k] = fmaxf(s[C + k] * inv_count - mean[k] * mean[k], 0.f);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mean[k] = rmean[ch + k];
-      var[k] = rvar[ch + k];
-    }
-  }
+// per-channel scale / shift of one BatchNorm for 8 channels (same arithmetic as bn.hip), in two
+// halves so the 16-byte loads can be issued a whole slice before they are needed
+struct BnRaw {
+  f32x4 a0, a1, b0, b1, g0, g1, e0, e1;   // (sum | mean), (sumsq | var), gamma, beta
+};
+
+MA_DEV BnRaw bn_load(const float* stats, const float* rmean, const float* rvar,
+                     const float* gamma, const float* beta, int C, int g, int ch) {
+  BnRaw r;
+  const float* a = stats ? stats + (size_t)g * 2 * C + ch : rmean + ch;
+  const float* b = stats ? stats + (size_t)g * 2 * C + C + ch : rvar + ch;
+  r.a0 = *(const f32x4*)a;
+  r.a1 = *(const f32x4*)(a + 4);
+  r.b0 = *(const f32x4*)b;
+  r.b1 = *(const f32x4*)(b + 4);
+  r.g0 = *(const f32x4*)(gamma + ch);
+  r.g1 = *(const f32x4*)(gamma + ch + 4);
+  r.e0 = *(const f32x4*)(beta + ch);
+  r.e1 = *(const f32x4*)(beta + ch + 4);
+  return r;
+}
+
+MA_DEV void bn_finish(const BnRaw& r, bool batch, float inv_count, float eps, float (&sc)[8],
+                      float (&sh)[8]) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    sc[k] = gamma[ch + k] * rsqrtf(var[k] + eps);
-    sh[k] = beta[ch + k] - mean[k] * sc[k];
+    const float a = k < 4 ? r.a0[k] : r.a1[k - 4], b = k < 4 ? r.b0[k] : r.b1[k - 4];
+    const float gm = k < 4 ? r.g0[k] : r.g1[k - 4], be = k < 4 ? r.e0[k] : r.e1[k - 4];
+    float mean = a, var = b;
+    if (batch) {
+      mean = a * inv_count;
+      var = fmaxf(b * inv_count - mean * mean, 0.f);
+    }
+    sc[k] = gm * rsqrtf(var + eps);
+    sh[k] = be - mean * sc[k];
   }
 }
 
@@ -220,16 +234,32 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   };
 
   // ---- in-place BN (+ residual / shortcut BN) + activation of a landed raw halo
+  // BN coefficients of this thread's 8 channels (logical chunk lc) of slice cb: loaded one
+  // slice ahead (kernel start for the first), so their latency hides under the DMA / taps
+  BnRaw cr1{}, cr2{};
+  auto load_coef = [&](int cb) {
+#ifdef HC_NO_COEF
+    return;
+#endif
+    if constexpr (MODE > 0) {
+      const int ch = cb * 64 + lc * 8;
+      cr1 = bn_load(pro.stats, pro.rmean, pro.rvar, pro.gamma, pro.beta, g.C, grp, ch);
+      if constexpr (MODE == 3)
+        cr2 = bn_load(pro.stats2, pro.rmean2, pro.rvar2, pro.gamma2, pro.beta2, g.C, grp, ch);
+    }
+  };
   auto transform = [&](int cb, int buf) {
+#ifdef HC_NO_TRANSFORM
+    return;
+#endif
     if constexpr (MODE > 0) {
       float sc[8], sh[8], sc2[8], sh2[8];
-      const int ch = cb * 64 + lc * 8;            // this thread's logical chunk: lc of its lane
-      bn_coef8(pro.stats, pro.rmean, pro.rvar, pro.gamma, pro.beta, g.C, grp, ch, pro.inv_count,
-               pro.eps, sc, sh);
+      bn_finish(cr1, pro.stats != nullptr, pro.inv_count, pro.eps, sc, sh);
       if constexpr (MODE == 3)
-        bn_coef8(pro.stats2, pro.rmean2, pro.rvar2, pro.gamma2, pro.beta2, g.C, grp, ch,
-                 pro.inv_count, pro.eps, sc2, sh2);
+        bn_finish(cr2, pro.stats2 != nullptr, pro.inv_count, pro.eps, sc2, sh2);
       char* hb = smem + buf * HBYTES + (tid >> 3) * 128 + (tid & 7) * 16;
+      float alo, ahi;
+      act_bounds(pro.act, alo, ahi);
       constexpr int BATCH = 8;
 #pragma unroll
       for (int i0 = 0; i0 < HRMAX; i0 += BATCH) {
@@ -256,7 +286,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
               float a = bf2f(y[k]) * sc[k] + sh[k];
               if constexpr (MODE == 2) a += bf2f(rr[k]);
               if constexpr (MODE == 3) a += bf2f(rr[k]) * sc2[k] + sh2[k];
-              o[k] = f2bf(act_f(a, pro.act));
+              o[k] = f2bf(fminf(fmaxf(a, alo), ahi));
             }
             // padding stays zero in ACTIVATION space (the conv pads the normalised input)
             const u32x4 v = hsrc[i] >= 0 ? __builtin_bit_cast(u32x4, o) : u32x4{0u, 0u, 0u, 0u};
@@ -280,6 +310,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
   if (nst > 0) {
+    load_coef(cb0);
     // prologue: the first slice's whole halo, then the weight tiles of steps 0 and 1
 #pragma unroll
     for (int j = 0; j < HRMAX; ++j)
@@ -296,6 +327,12 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
       MA_LAP(3, tl);
       if constexpr (MODE > 0) {
         transform(cb0 + cl, buf);
+        // compiler-VISIBLE drain of the transform's own memory ops (residual loads, kept-
+        // activation stores): left pending, the compiler's later register-reuse waits count
+        // only them, and -- the DMAs being invisible to it -- would drain the whole LDS-DMA
+        // ring at every tap
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+        if (cl + 1 < nsl) load_coef(cb0 + cl + 1);
         bar_lds();
       }
       const char* hb = smem + buf * HBYTES;

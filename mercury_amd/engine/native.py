@@ -131,6 +131,14 @@ class NativeEngine(object):
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
         # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
         self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
+        # input BatchNorm (+ residual / shortcut BN) folded into the halo conv's staging, on the
+        # shapes where that measured faster than a bn_apply pass + the conv ALONE
+        # (ops/hconv.fused_plan).  ('1' both batch modes, 'score' / 'train' one, '0' off.)
+        # Off by default: in the two-stream step it lost (same-box A/B, profiles/r2/
+        # ab_fuse_bn_halo.json: off 1.602, score 1.634, train 1.724 ms/step) -- its blocks take
+        # one wave per SIMD and up to 150 KB of LDS, so the other stream's kernels cannot share
+        # their CUs; the bn_apply passes it removes are cheap to co-schedule
+        self.fuse_bn_halo = os.environ.get('MERCURY_FUSE_BN_HALO', '0')
         # stride-1 3x3 forward convs on the halo-tile kernel (csrc/hconv.hip) where measured faster
         # ('1' both batch modes, 'score' / 'train' one of them, '0' off).  Default: the scoring
         # pass only -- same-box A/B of the two-stream step (profiles/r2/ab_hconv_modes.json):
@@ -274,6 +282,13 @@ class NativeEngine(object):
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
+                    # ... and the convs that take their input's BN in the halo staging
+                    fb = self.fuse_bn_halo == '1' or \
+                        self.fuse_bn_halo == ('train' if train else 'score')
+                    hb = hconv.fused_plan(sp) if fb else None
+                    if hb is not None:
+                        m.plan[u.name, 'hconv_bn'] = hb
+                        slab = max(slab, slab_bytes(sp.M, sp.K, *hb))
                     if train:
                         if u.need_dgrad and sp.K % 8 == 0:
                             dp, wp = tune.bwd_plans_for(sp, dgrad_plan(sp), wgrad_plan(sp))
@@ -394,21 +409,73 @@ class NativeEngine(object):
                      group_rows=sp.group_rows or sp.M, act=act, eps=BN_EPS, running=running,
                      res=res, **kw)
 
+    # -- BatchNorm folded into the halo conv (csrc/hconv.hip MODE 1-3): a BN output that the
+    # next conv can stage itself stays "pending" -- (raw conv output, its BN unit, activation,
+    # identity residual or shortcut BN) -- and that conv applies it while loading its halo,
+    # writing the activation back once (``keep``) where the residual / shortcut / backward
+    # needs it.  Policy and plans: ``hconv.fuse_ok`` / ``m.plan[name, 'hconv_bn']``.
+    def _pending(self, u, y, act, res=None, unit2=None, y2=None):
+        return dict(unit=u, y=y, act=act, res=res, unit2=unit2, y2=y2)
+
+    def _can_take(self, m, u):
+        return (u.name, 'hconv_bn') in m.plan and not u.depthwise
+
+    def _hconv_pending(self, m, u, pend, y, stats, keep):
+        """conv ``u`` on the pending activation ``pend``: hconv with the BN applied in staging."""
+        sp = m.spec[u.name]
+        pu = pend['unit']
+        su = m.spec[pu.name]
+        batch = m.train or m.group_imgs
+        pro = dict(gamma=self._gamma(pu), beta=self._beta(pu), act=pend['act'], eps=BN_EPS,
+                   keep=keep, count=su.group_rows or su.M, group_imgs=m.group_imgs or m.N)
+        if batch:
+            pro['stats'] = m.stats[pu.name]
+        else:
+            pro.update(rmean=pu.bn.running_mean, rvar=pu.bn.running_var)
+        if pend['res'] is not None:
+            pro['res'] = pend['res']
+        if pend['unit2'] is not None:
+            u2 = pend['unit2']
+            pro.update(y2=pend['y2'], gamma2=self._gamma(u2), beta2=self._beta(u2))
+            if batch:
+                pro['stats2'] = m.stats[u2.name]
+            else:
+                pro.update(rmean2=u2.bn.running_mean, rvar2=u2.bn.running_var)
+        hconv.hconv_fwd(pend['y'], self.w_krsc[u.name], y, sp, m.plan[u.name, 'hconv_bn'],
+                        stats=stats, slab=m.slab,
+                        bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
+
     def forward(self, m, x=None):
         """Forward through all blocks; returns the final activation buffer."""
         x = m.input if x is None else x
         stats_on = m.train or m.group_imgs
+        pend = None          # the previous block's output, not yet materialised in x's buffer
+        nblk = len(self.lw.blocks)
         for bi, blk in enumerate(self.lw.blocks):
             inp = x
             nu = len(blk.units)
             pro = None
             for i, u in enumerate(blk.units):
                 y = m.buf[u.name, 'y']
-                self._conv_fwd(m, u, inp, y, m.stats[u.name] if stats_on else None, pro=pro)
+                st = m.stats[u.name] if stats_on else None
+                if pend is not None:
+                    # BN (+ residual / shortcut BN) + act of the input applied while staging;
+                    # ``keep`` materialises x (block input) for the residual, shortcut and
+                    # backward; intra-block activations are kept only for the backward
+                    keep = x if i == 0 else (m.buf[blk.units[i - 1].name, 'a'] if m.train
+                                             else None)
+                    self._hconv_pending(m, u, pend, y, st, keep)
+                    pend = None
+                else:
+                    self._conv_fwd(m, u, inp, y, st, pro=pro)
                 if i < nu - 1:
+                    nxt = blk.units[i + 1]
+                    if self._can_take(m, nxt) and u.act in ('relu', 'relu6', 'none'):
+                        pend = self._pending(u, y, u.act)
+                        continue
                     # intra-block BN + activation: inside the next conv's operand load when it
                     # can take it, else its own pass
-                    pro = self._pro_for(m, u, blk.units[i + 1])
+                    pro = self._pro_for(m, u, nxt)
                     if pro is not None:
                         inp = y
                         continue
@@ -425,7 +492,17 @@ class NativeEngine(object):
                         res, ru = m.buf[sc.name, 'y'], sc
                     elif blk.identity:
                         res = x
-                    self._bn_apply(m, u, y, out, blk.final_act, res=res, res_unit=ru)
+                    nb = self.lw.blocks[bi + 1] if bi + 1 < nblk else None
+                    if (nb is not None and not blk.pool and nb.units and
+                            self._can_take(m, nb.units[0]) and
+                            blk.final_act in ('relu', 'relu6', 'none')):
+                        # the next block's first conv applies this BN (+ residual) and writes
+                        # ``out`` through its keep
+                        pend = self._pending(u, y, blk.final_act,
+                                             res=res if ru is None else None,
+                                             unit2=ru, y2=res if ru is not None else None)
+                    else:
+                        self._bn_apply(m, u, y, out, blk.final_act, res=res, res_unit=ru)
             if blk.pool:
                 N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
                 ops.pool2d_fwd(m.buf[bi, 'pre'], m.buf[bi, 'out'], N, h, w, K, P_, Q_, k, st, pd,

@@ -193,6 +193,13 @@ MEASURED = {
 }
 
 
+# stride-2 3x3 convs (fused-BN use only): best plain plans of the same sweeps
+MEASURED_S2 = {
+    (32, 32, 64, 128): (64, 64, 1), (32, 16, 128, 256): (64, 64, 1),
+    (32, 8, 256, 512): (64, 64, 4), (320, 8, 256, 512): (64, 128, 1),
+}
+
+
 def engine_plan(spec: ConvSpec):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured winners,
     else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every measured
@@ -207,6 +214,26 @@ def engine_plan(spec: ConvSpec):
     if spec.C >= 128:
         return plan(spec)
     return None
+
+
+def fused_plan(spec: ConvSpec):
+    """Plan for running this conv with its INPUT's BatchNorm (+ residual / shortcut BN) +
+    activation applied in the halo staging, or None (bn_apply pass + plain conv instead).
+    Measured (bench/hconv_sweep.py, hconv_bn vs igemm + bn_apply; profiles/r2/
+    hconv_sweep_bn_b*.jsonl): a win on every 3x3 shape at the train batch (32: 130.6 vs 146.9 us
+    over the ResNet-18 layers) and on the >= 256-channel shapes at the scoring batch (320:
+    layer3 55.0 vs 59.5, layer4 65.4 vs 72.9 us), a loss on the 64/128-channel scoring shapes.
+    The kept activation must cover the input exactly once (keep_ok)."""
+    if not supported(spec) or not keep_ok(spec):
+        return None
+    if spec.N > 64 and spec.C < 256:
+        return None
+    p = (MEASURED if spec.stride == 1 else MEASURED_S2).get((spec.N, spec.H, spec.C, spec.K))
+    if p is not None:
+        g = geometry_cached(spec, p[0], p[1])
+        if g is not None and lds_bytes(g, *p) <= LDS_MAX:
+            return p
+    return plan(spec)
 
 
 def _pro_args(pro, spec):

@@ -50,7 +50,7 @@ def coordinates(eng):
     out = {}
     for m in eng.modes.values():
         for (name, kind), _ in m.plan.items():
-            if kind in ('wgrad', 'hconv'):       # (halo-conv plans are measured, not tuned here)
+            if kind in ('wgrad', 'hconv', 'hconv_bn'):   # (halo-conv plans: measured, not tuned)
                 continue
             sp = m.spec[name]
             ck = 'fwd' if kind == 'fwd' else 'bwd'
