@@ -5,7 +5,8 @@
 Per ResNet-18 CIFAR conv shape with >= 64 input channels, one JSON line:
   igemm_us       generic implicit GEMM at its heuristic plan (plain input)
   bn_apply_us    the standalone BN + ReLU pass over the conv input that igemm needs first
-  hconv_us       halo conv, plain input, best plan over tiles x 64-channel splits
+  hconv_us       halo conv, plain input, best plan over tiles x 64-channel splits (split 0:
+                 the persistent kernel)
   hconv_bn_us    halo conv with the producer's BN + ReLU applied while staging (+ the kept
                  activation where the halos tile the input) -- replaces bn_apply + igemm
 """
@@ -62,6 +63,8 @@ def main():
             for s in (1, 2, 4):
                 if s <= C // 64 and H.lds_bytes(g, bm, bn, s) <= H.LDS_MAX:
                     cands.append((bm, bn, s))
+            if H.persistent_ok(sp, bm, bn) and H.lds_bytes(g, bm, bn, 0) <= H.LDS_MAX:
+                cands.append((bm, bn, 0))      # persistent kernel
         hp = H.plan(sp)
         ip = fwd_plan(sp)
         slab = torch.zeros(max([slab_bytes(sp.M, K, *c) for c in cands + [ip]] + [4]) // 4 + 1,

@@ -44,10 +44,25 @@ def main():
     for _ in range(5):
         H.hconv_fwd(x, wk, y, sp, plan, stats=stats, slab=slab, pro=pro)
     torch.cuda.synchronize()
-    nb = (sp.M // plan[0]) * ((K + plan[1] - 1) // plan[1]) * plan[2]
+    ntiles = (sp.M // plan[0]) * ((K + plan[1] - 1) // plan[1])
+    nb = min(ntiles, 256) if plan[2] == 0 else ntiles * plan[2]
     v = np.array(ops.lib().hconv_stamps(min(nb, 8192)), dtype=np.int64).reshape(-1, 12)
     if v.size == 0:
         print('not a stamps build')
+        return
+    if plan[2] == 0:
+        # persistent kernel: prologue, loop, per-phase sums of wave 0 over all steps
+        f = lambda q: '%8d %8d' % (np.median(q), np.percentile(q, 90))
+        print('shape', a[:5], 'plan', plan, 'blocks', len(v), 'tiles/block %.2f' % (ntiles / len(v)))
+        print('  prologue  med/p90 %s' % f(v[:, 1] - v[:, 0]))
+        print('  loop      med/p90 %s' % f(v[:, 2] - v[:, 1]))
+        names = ('mfma-half-1 issue', 'vmcnt wait', 'barrier', 'DMA issue', 'reads+mfma-half-2',
+                 'epilogue')
+        for q, nm in enumerate(names):
+            print('  %-20s med/p90 %s' % (nm, f(v[:, 4 + q])))
+        t0 = v[:, 0] - v[:, 0].min()
+        print('  block start spread med/p90/max %d %d %d, kernel span %d' % (
+            np.median(t0), np.percentile(t0, 90), t0.max(), v[:, 3].max() - v[:, 0].min()))
         return
     pro_, loop, epi = v[:, 1] - v[:, 0], v[:, 2] - v[:, 1], v[:, 3] - v[:, 2]
     t0 = v[:, 0] - v[:, 0].min()

@@ -33,6 +33,8 @@
 // chunk c ^ (row & 7)).  MFMA v_mfma_f32_16x16x32_bf16 with swapped operands (lane l: output
 // pixel l&15, four consecutive channels), so the shared epilogue of conv_epi.h applies as is:
 // ghost-BN statistics, split-K (over 64-channel slices) reduced in-launch by the last slice.
+#include <cstdlib>
+
 #include "conv_epi.h"
 
 namespace {
@@ -417,6 +419,523 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   MA_STAMP(3);
 }
 
+// ---------------------------------------------------------------- persistent variant
+// One block per CU walks a strided list of output tiles as ONE continuous step stream
+// (tile, 64-channel slice, tap), so the per-tile prologue (halo + first weight tiles from HBM)
+// and the epilogue overlap the neighbouring tiles' MFMAs instead of serialising each block:
+//   * the next slice's halo -- the next TILE's when this is a tile's last slice -- is issued in
+//     pieces during taps 0..PHP-1 into the other of two halo buffers;
+//   * weights run PDW = 5 steps ahead in a 6-slot ring (the single in-order vmcnt makes a
+//     wait for a weight tile also wait for every older halo piece: 5 steps cover HBM latency);
+//   * fragments of step s + 1 are read from LDS while step s's MFMAs execute;
+//   * the epilogue stages through its own LDS area with raw barriers and issues a FIXED number
+//     of stores / stat atomics per wave (E), so the following taps' counted waits stay exact
+//     and nothing drains the in-flight DMAs.
+// The tile-invariant part of each halo slot's source offset is computed once; a new tile only
+// adds its (image, row) base.  Plain input only (MODE 0), no bias / accumulate / split-K, whole
+// tiles (M % BM == 0, K % BN == 0, ghost-BN groups a multiple of BM): the host checks.
+constexpr int PDW = 5;              // weight prefetch distance (steps)
+constexpr int PSLOT = PDW + 1;      // weight ring slots
+constexpr int PHP = 4;              // taps of a slice carrying the next slice's halo pieces
+
+// epilogue of one persistent tile: bf16 round, ghost-BN sums (DPP rows -> LDS -> one atomic
+// pair per column), LDS-staged coalesced 16-byte row stores.  VMEM instructions per wave:
+// BM*BN/(8*NT) stores + 2 atomics on the waves with 64 w < BN (STATS).
+template <int BM, int BN, int WM, bool STATS>
+MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / 64], char* es,
+                        const EpiParams& e, int m0, int n0) {
+  constexpr int WN = 4 / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
+  constexpr int CPR = BN / 8, ST = BM * CPR / NT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  float* red = (float*)es;                          // [WM][2][BN] per-wave-row partials
+  bf16* tile = (bf16*)(es + 16 * BN * 4);           // [BM][LDT]
+  bar_lds();                                        // every wave's reads of the area are done
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int nl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int ml = wm * (BM / WM) + tm * 16 + (lane & 15);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
+      *(bf16x4*)(tile + ml * LDT + nl) = o;
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = bf2f(o[j]);
+          s[j] += f;
+          ss[j] += f * f;
+        }
+      }
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] = row16_sum(s[j]);
+        ss[j] = row16_sum(ss[j]);
+      }
+      if ((lane & 15) == 0) {
+        float* r = red + wm * 2 * BN + nl;
+        *(f32x4*)r = f32x4{s[0], s[1], s[2], s[3]};
+        *(f32x4*)(r + BN) = f32x4{ss[0], ss[1], ss[2], ss[3]};
+      }
+    }
+  }
+  bar_lds();
+  if constexpr (STATS) {
+    if (tid < BN) {                                 // whole waves (BN = 64 or 128)
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) {
+        a += red[q * 2 * BN + tid];
+        b += red[q * 2 * BN + BN + tid];
+      }
+      float* dst = e.stats + (size_t)(m0 / e.group_rows) * 2 * e.stats_ld + n0 + tid;
+      atomicAdd(dst, a);
+      atomicAdd(dst + e.stats_ld, b);
+    }
+  }
+  const int ch = tid % CPR;
+#pragma unroll
+  for (int it = 0; it < ST; ++it) {
+    const int rl = (tid + it * NT) / CPR;
+    const bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
+    *(bf16x8*)(e.out + (size_t)(m0 + rl) * e.ldo + n0 + ch * 8) = v;
+  }
+}
+
+// raw buffer resource over [base, base + bytes): an LDS-DMA whose offset is past the end
+// lands ZEROS (the padding halo pixels need no zero page and no second pointer)
+MA_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+}
+// 16 bytes per lane, buffer -> LDS (lane l lands at the wave-uniform LDS address + 16 l)
+MA_DEV void bdma16(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               ::"v"(off), "s"(r), "s"(lds) : "memory");
+}
+constexpr unsigned OOB = 0x7ffffff0u;   // offset past every tensor: zeros
+
+// vmcnt immediate at tap t: VMEM ops issued after step s + 1's weight tile (issued at step
+// s + 1 - PDW) -- the issues of the PDW - 2 steps before s: BI weight pieces each (a step x of
+// this slice issues for x + PDW, in the next slice when x + PDW >= T: only if one follows, hn),
+// PHI halo pieces on carrying taps x < PHP of a slice that prefetches a halo (hd)
+template <int t, int T, int BI, int PHI, bool hd, bool hn>
+constexpr int tap_wait() {
+  int n = 0;
+  for (int x = t - (PDW - 2); x < t; ++x) {
+    if (x < 0) {
+      n += BI;
+    } else {
+      if (x + PDW < T || hn) n += BI;
+      if (x < PHP && hd) n += PHI;
+    }
+  }
+  return n;
+}
+
+// counted wait after which the epilogue's E VMEM ops (issued after the waited-for DMA) may be
+// outstanding: E = ST stores + 2 stat atomics on the waves that issue them
+template <int N, int ST, bool STATS>
+MA_DEV void wait_epi(bool epi, bool ew) {
+  if (!epi) vm_wait<N>();
+  else if (STATS && ew) vm_wait<N + ST + 2>();
+  else vm_wait<N + ST>();
+}
+
+// the wait of tap t (t is a constant once the tap loop is unrolled: the switch folds)
+template <int T, int BI, int PHI, int ST, bool STATS>
+MA_DEV void wait_tap(int t, bool hd, bool hn, bool epi, bool ew) {
+  static_assert(T == 9, "3x3 taps");
+#define WT(tt)                                                                              \
+  case tt:                                                                                  \
+    if (hd) {                                                                               \
+      if (hn) wait_epi<tap_wait<tt, T, BI, PHI, true, true>(), ST, STATS>(epi, ew);         \
+      else wait_epi<tap_wait<tt, T, BI, PHI, true, false>(), ST, STATS>(epi, ew);           \
+    } else {                                                                                \
+      if (hn) wait_epi<tap_wait<tt, T, BI, PHI, false, true>(), ST, STATS>(epi, ew);        \
+      else wait_epi<tap_wait<tt, T, BI, PHI, false, false>(), ST, STATS>(epi, ew);          \
+    }                                                                                       \
+    break;
+  switch (t) { WT(0) WT(1) WT(2) WT(3) WT(4) WT(5) WT(6) WT(7) WT(8) }
+#undef WT
+}
+
+template <int BM, int BN, int WM, int NHB, int HRC, bool STATS>
+__global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __restrict__ src,
+                                                              const bf16* __restrict__ wt,
+                                                              HconvGeom g, EpiParams e) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  constexpr int BI = BN / 32;                       // weight DMA pieces per wave per step
+  constexpr int SLOT = BN * 128;
+  constexpr int R = 3, T = R * R;
+  constexpr int ST = BM * BN / (8 * NT);
+  constexpr int PHI = HRC / PHP;                    // halo pieces per wave on a carrying tap
+  static_assert(PHP <= T - 3, "a slice's halo lands >= 2 steps before its first read");
+  static_assert(HRC % PHP == 0 && HRC <= HRMAX, "halo piece capacity");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const bool ew = wu * 64 < BN;                     // this wave issues the stat atomics
+  const int ntn = g.K / BN;
+  const int PQ = g.P * g.Q;
+  const int ntiles = (g.N * PQ / BM) * ntn;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int my = b < ntiles ? (ntiles - 1 - b) / G + 1 : 0;
+  if (my == 0) return;
+  MA_STAMP(0);
+#ifdef MERCURY_STAMPS
+  // per-step phase sums of wave 0 (shader clocks): [0] first MFMA half issue, [1] vmcnt wait,
+  // [2] barrier, [3] DMA issue, [4] reads + second MFMA half, [5] epilogue
+  unsigned long long lap[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
+  const int nsl = g.C >> 6;
+  const int Kt = T * g.C;
+  const int HR = (g.HPIX + 31) >> 5;
+  const int HBYTES = HR * 32 * 128;
+  const int lc = (lane & 7) ^ (lane >> 3);
+  const int per_img = g.HT * g.HWP;
+  const auto rs_src = buf_rsrc(src, (unsigned)((size_t)g.N * g.H * g.W * g.C * 2));
+  const auto rs_wt = buf_rsrc(wt, (unsigned)((size_t)g.K * Kt * 2));
+
+  // ---- tile-invariant halo slots: byte offset from the tile's (image, row) base, and the
+  // slot's input-row step (HROW_NONE for padding columns / unused slots: never in range).
+  // The host keeps N a multiple of IMG, so only the row test depends on the tile.
+  constexpr int HROW_NONE = 0x4000;
+  int hbase[HRC], hrow[HRC];
+#pragma unroll
+  for (int i = 0; i < HRC; ++i) {
+    hbase[i] = 0;
+    hrow[i] = HROW_NONE;
+    const int pix = (tid >> 3) + 32 * i;
+    if (i < HR && pix < g.HPIX) {
+      const int img = pix / per_img, rem = pix - img * per_img;
+      const int hr = rem / g.HWP, col = rem - hr * g.HWP;
+      int hc;
+      bool ok;
+      if (g.HALF) {
+        hc = col < g.HALF ? 2 * col : 2 * (col - g.HALF) + 1;
+        ok = col < g.HALF ? col < (g.HWd + 1) / 2 : col - g.HALF < g.HWd / 2;
+      } else {
+        hc = col;
+        ok = col < g.HWd;
+      }
+      const int ww = hc * g.HS - g.pad;
+      if (ok && (unsigned)ww < (unsigned)g.W) {
+        hbase[i] = (((img * g.H + hr * g.HS) * g.W + ww) * g.C + lc * 8) * 2;
+        hrow[i] = hr * g.HS;
+      }
+    }
+  }
+  unsigned hoff[HRC];                                // byte offsets of the current halo (OOB: pad)
+  const float rntn = 1.f / (float)ntn, rpq = 1.f / (float)PQ, rq = 1.f / (float)g.Q;
+  auto tile_of = [&](int k, int& m0, int& n0) {
+    const int t = xcd_tile(k * G + b, ntiles);
+    const int mt = udiv24(t, ntn, rntn), nt = t - mt * ntn;
+    m0 = mt * BM;
+    n0 = nt * BN;
+  };
+  auto set_halo = [&](int m0) {
+    const int n0i = udiv24(m0, PQ, rpq);
+    const int p0 = udiv24(m0 - n0i * PQ, g.Q, rq);
+    const int h0 = p0 * g.stride - g.pad;
+    const int toff = (n0i * g.H + h0) * g.W * g.C * 2;
+#pragma unroll
+    for (int i = 0; i < HRC; ++i)
+      hoff[i] = (unsigned)(h0 + hrow[i]) < (unsigned)g.H ? (unsigned)(hbase[i] + toff) : OOB;
+  };
+  // A-fragment byte offsets in a halo buffer, per (tap, fragment row block): the swizzled chunk
+  // of the k = 0..31 half (the other half is the same ^ 64)
+  const int c16 = (lane >> 4) << 4;
+  int aoff[T][TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int row = wm * (BM / WM) + tm * 16 + (lane & 15);
+    const int img = row / (g.TR * g.Q), rem = row - img * g.TR * g.Q;
+    const int tr = rem / g.Q, q = rem - tr * g.Q;
+    const int hc = q * g.SR;
+    const int col = g.HALF ? ((hc & 1) * g.HALF + (hc >> 1)) : hc;
+    const int apix = img * per_img + tr * g.SR * g.HWP + col;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int r = t / R, ss = t % R;
+      const int p = apix + (g.HALF ? r * g.HWP + (ss >> 1) + (ss & 1) * g.HALF : r * g.HWP + ss);
+      aoff[t][tm] = (p << 7) + (c16 ^ ((p & 7) << 4));
+    }
+  }
+  unsigned boff[BI];                                 // weight rows this lane fetches (bytes)
+#pragma unroll
+  for (int j = 0; j < BI; ++j) boff[j] = ((8 * (w + 4 * j) + (lane >> 3)) * Kt + lc * 8) * 2;
+  // B-fragment byte offsets inside a ring slot (tap-invariant)
+  int bfo[2][TN];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int row = wn * (BN / WN) + tn * 16 + (lane & 15);
+      bfo[kk][tn] = (row * 8 + ((kk * 4 + (lane >> 4)) ^ (row & 7))) * 16;
+    }
+  const unsigned s_halo = lds_addr(smem);
+  const unsigned s_ring = s_halo + NHB * HBYTES;
+  const unsigned s_dump = s_ring + PSLOT * SLOT + wu * 1024;
+
+  auto issue_h = [&](int cb, int buf, int j) {
+    // (HR through an empty asm: hoisted, the 16 `j < HR` tests were kept as lane masks and
+    // spilled to VGPR lanes)
+    int hr = HR;
+    asm volatile("" : "+s"(hr));
+    bdma16(rs_src, hoff[j] + cb * 128, j < hr ? s_halo + buf * HBYTES + (32 * j + 8 * wu) * 128
+                                              : s_dump);
+  };
+  auto issue_b = [&](int n0, int cb, int t, int slot) {
+    const unsigned k = (unsigned)((n0 * Kt + t * g.C + cb * 64) * 2);
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      bdma16(rs_wt, boff[j] + k, s_ring + slot * SLOT + 8 * (wu + 4 * j) * 128);
+  };
+  // fragments of (halo buffer, ring slot, tap); the k = 0..31 half first (the next step's
+  // first MFMAs need only that)
+  auto read_frags = [&](bf16x8 (&fa)[2][TM], bf16x8 (&fb)[2][TN], int hbuf, int slot, int tap) {
+    const char* bs = smem + NHB * HBYTES + slot * SLOT;
+    const char* hb = smem + hbuf * HBYTES;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) fa[0][tm] = *(const bf16x8*)(hb + aoff[tap][tm]);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) fb[0][tn] = *(const bf16x8*)(bs + bfo[0][tn]);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+      fa[1][tm] = *(const bf16x8*)(hb + (aoff[tap][tm] ^ 64));   // chunk + 4 = swizzled ^ 4
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) fb[1][tn] = *(const bf16x8*)(bs + bfo[1][tn]);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- slice cursors.  Slice sigma = (tile k, 64-channel slice cl); the block walks
+  // NS = my * nsl of them.  Halo of slice sigma + D (D = NHB - 1) is prefetched during slice
+  // sigma into buffer (sigma + D) % NHB, the weights of the next slice during its last taps.
+  constexpr int D = NHB - 1;
+  const int NS = my * nsl;
+  int m0, n0;                                        // tile of the current slice
+  tile_of(0, m0, n0);
+  int kD = 0, clD = 0;                               // slice whose halo hoff describes
+  auto advance_d = [&]() {                           // kD, clD -> next slice (+ its halo slots)
+    if (++clD == nsl) {
+      clD = 0;
+      if (++kD < my) {
+        int mD, nD;
+        tile_of(kD, mD, nD);
+        set_halo(mD);
+      }
+    }
+  };
+  // ---- prologue: halos of slices 0 .. D-1, weight tiles of steps 0..PDW-1, fragments of step 0
+  set_halo(m0);
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (d < NS) {
+#pragma unroll
+      for (int j = 0; j < HRC; ++j)
+        if (j < HR) issue_h(clD, d, j);
+    }
+    advance_d();
+  }
+  // (kD, clD) = slice D: prefetched during slice 0
+  static_assert(PDW < T, "prologue weight tiles lie in slice 0");
+#pragma unroll
+  for (int t = 0; t < PDW; ++t) issue_b(n0, 0, t, t);
+  vm_wait<0>();
+  bar_raw();
+  bf16x8 fa[2][TM], fb[2][TN];
+  read_frags(fa, fb, 0, 0, 0);
+  MA_STAMP(1);
+
+  constexpr int NM = TM * TN;
+  // MFMAs [i0, i1) of half kk of the current step (fragments already in registers)
+  auto mma = [&](int kk, int i0, int i1) {
+#pragma unroll
+    for (int i = 0; i < NM; ++i)
+      if (i >= i0 && i < i1)
+        acc[i / TN][i % TN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            fb[kk][i % TN], fa[kk][i / TN], acc[i / TN][i % TN], 0, 0, 0);
+  };
+
+  // Step s (tap t of a slice): wait for step s + 1's weight tile, barrier, issue the DMAs of
+  // step s + PDW and this slice's share of halo pieces, read step s + 1's fragments.  The 2 NM
+  // MFMAs of step s are spread over all of it (the wait, the barrier and every DMA issue stall
+  // the wave; MFMAs issued before them keep the matrix pipe busy).  Newer than the awaited tile
+  // at the wait: tap_wait() pieces and, on taps <= PDW - 2 of a tile's first slice, the
+  // previous tile's epilogue (E) -- every count is a compile-time immediate per tap.
+  int s0 = 0, cl = 0, k = 0, buf = 0, bufD = D % NHB, sb = 0;   // sb = s0 % PSLOT
+  for (int sig = 0; sig < NS; ++sig, s0 += T) {
+    const bool last_sl = cl + 1 == nsl;
+    const bool hn = sig + 1 < NS;                    // a slice follows this one
+    const bool hd = sig + D < NS;                    // this slice prefetches a halo
+    int m0n = m0, n0n = n0;
+    const int cbn = last_sl ? 0 : cl + 1;
+    if (last_sl && hn) tile_of(k + 1, m0n, n0n);
+    const bool epi = cl == 0 && k > 0;
+    const int cbD = clD;
+    const int bnext = buf + 1 == NHB ? 0 : buf + 1;
+    auto slot_of = [&](int u) {                      // ring slot of step s0 + u, u < 2 PSLOT
+      const int v = sb + u;
+      return v >= 2 * PSLOT ? v - 2 * PSLOT : (v >= PSLOT ? v - PSLOT : v);
+    };
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const bool go = t < T - 1 || hn;               // step s + 1 exists
+      mma(0, 0, NM / 2);
+      MA_LAP(0, tl);
+      if (go) {
+        wait_tap<T, BI, PHI, ST, STATS>(t, hd, hn, epi && t <= PDW - 2, ew);
+      }
+      MA_LAP(1, tl);
+      mma(0, NM / 2, 3 * NM / 4);
+      if (go) bar_raw();
+      MA_LAP(2, tl);
+      mma(0, 3 * NM / 4, NM);
+      if (go) {
+        if (hd && t < PHP) {
+#pragma unroll
+          for (int q = 0; q < PHI; ++q) issue_h(cbD, bufD, t * PHI + q);
+        }
+        if (t + PDW < T) issue_b(n0, cl, t + PDW, slot_of(t + PDW));
+        else if (hn) issue_b(n0n, cbn, t + PDW - T, slot_of(t + PDW));
+      }
+      MA_LAP(3, tl);
+      bf16x8 na[2][TM], nb[2][TN];
+      // step s + 1's fragments interleaved with the k = 32..63 half of step s (unconditional,
+      // so reads and MFMAs share one basic block; the block's last step reads a stale slot it
+      // never uses)
+      read_frags(na, nb, t + 1 < T ? buf : bnext, slot_of(t + 1), t + 1 < T ? t + 1 : 0);
+      mma(1, 0, NM);
+      constexpr int NR = 2 * (TM + TN);
+      constexpr int RPM = (NR + NM - 1) / NM;        // reads per MFMA gap
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, RPM, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) fa[kk][tm] = na[kk][tm];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) fb[kk][tn] = nb[kk][tn];
+      }
+#ifdef MERCURY_STAMPS
+      asm volatile("s_nop 0" ::"v"(acc[0][0]));
+#endif
+      MA_LAP(4, tl);
+      if (t == T - 1 && last_sl) {
+        // staged in this slice's halo buffer: fully read, refilled only from the next slice on
+        epi_persist<BM, BN, WM, STATS>(acc, smem + buf * HBYTES, e, m0, n0);
+        MA_LAP(5, tl);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // next slice; the halo cursor moves to the slice after the one just prefetched (its slots
+    // are recomputed only here, after this slice's last halo piece was issued)
+    if (hd) advance_d();
+    m0 = m0n;
+    n0 = n0n;
+    buf = bnext;
+    bufD = bufD + 1 == NHB ? 0 : bufD + 1;
+    sb = (sb + T) % PSLOT;
+    if (last_sl) {
+      cl = 0;
+      ++k;
+    } else {
+      ++cl;
+    }
+  }
+  MA_STAMP(2);
+#ifdef MERCURY_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 8192)
+    for (int q = 0; q < 6; ++q) g_stamps[blockIdx.x][4 + q] = lap[q];
+#endif
+  MA_STAMP(3);
+}
+
+// LDS of the persistent kernel: two halo buffers (each also the epilogue's staging area, so it
+// must hold Smem::RED_BYTES), the weight ring, the DMA sink
+template <int BM, int BN>
+int persist_lds_bytes(const HconvGeom& g) {
+  const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
+  if (hbytes < Smem<BM, BN>::RED_BYTES) return 1 << 30;
+  return 2 * hbytes + PSLOT * BN * 128 + 4096;
+}
+
+template <int BM, int BN, int WM, int HRC>
+void launch_persist_k(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                      int grid, int bytes, hipStream_t st) {
+  static bool attr[2] = {false, false};
+  const bool stats = e.stats != nullptr;
+  if (!attr[stats]) {
+    (void)hipFuncSetAttribute(stats ? (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, true>
+                                    : (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr[stats] = true;
+  }
+  if (stats)
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, true>), dim3(grid), dim3(NT),
+                       bytes, st, src, wt, g, e);
+  else
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, false>), dim3(grid), dim3(NT),
+                       bytes, st, src, wt, g, e);
+}
+
+// grid = one block per CU; the halo piece capacity (8, 12 or 16 per wave) is the smallest that
+// holds the tile's halo, so carrying taps issue few pieces into the sink
+template <int BM, int BN, int WM>
+int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                   hipStream_t st) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  // blocks: half the CUs by default -- the scoring convs run beside the training stream, and a
+  // grid on every CU (143 KB of LDS each) locks the training kernels out for its whole length.
+  // Measured, ResNet-18 step (bench.py, same box): 256 blocks 1.653 ms, 192 1.590, 160 1.550,
+  // 128 1.525, 96 1.720, 64 2.037; per-tile kernels 1.607.  MERCURY_HCONV_PERSIST_GRID overrides.
+  static int gmax = -1;
+  if (gmax < 0) {
+    const char* ev = getenv("MERCURY_HCONV_PERSIST_GRID");
+    gmax = ev ? atoi(ev) : cus / 2;
+    if (gmax <= 0 || gmax > cus) gmax = cus;
+  }
+  const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
+  const int grid = ntiles < gmax ? ntiles : gmax;
+  const int bytes = persist_lds_bytes<BM, BN>(g);
+  if (bytes > 160 * 1024) return 0;
+  const int hr = (g.HPIX + 31) >> 5;
+  if (hr <= 8)
+    launch_persist_k<BM, BN, WM, 8>(src, wt, g, e, grid, bytes, st);
+  else if (hr <= 12)
+    launch_persist_k<BM, BN, WM, 12>(src, wt, g, e, grid, bytes, st);
+  else
+    launch_persist_k<BM, BN, WM, 16>(src, wt, g, e, grid, bytes, st);
+  return 1;
+}
+
 template <int BM, int BN, int WM, int MODE>
 void launch_one(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                 const HconvPro& pro, dim3 grid, hipStream_t st) {
@@ -474,12 +993,25 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   const int M = g.N * g.P * g.Q;
   const int gx = ((M + bm - 1) / bm) * ((g.K + bn - 1) / bn);
   const int nchunks = g.C >> 6;
+  const bool persist = splits == 0;
   splits = splits < 1 ? 1 : (splits > nchunks ? nchunks : splits);
   g.chunks_per_split = (nchunks + splits - 1) / splits;
   int gy = (nchunks + g.chunks_per_split - 1) / g.chunks_per_split;
   if (gx > 1024) gy = 1, g.chunks_per_split = nchunks;    // tile counters: SEM_INTS
   if (gy == 1) e.slab = nullptr;
   if (((g.HPIX + 31) >> 5) > HRMAX || g.R != 3) return 0;
+  if (persist) {
+    // persistent plan (splits == 0): plain whole tiles only, else the per-tile kernel below
+    const bool ok = pro.mode == 0 && e.bias == nullptr && !e.accumulate &&
+                    e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
+                    (e.stats == nullptr || e.group_rows % bm == 0);
+#define HP_CASE(BM_, BN_, WM_) \
+  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM_>(src, wt, g, e, st)) return 1;
+    HP_CASE(256, 64, 4)
+    HP_CASE(128, 64, 2)
+    HP_CASE(64, 64, 1)
+#undef HP_CASE
+  }
   const dim3 grid(gx, gy);
 #define HC_CASE(BM_, BN_, WM_)                                  \
   if (bm == BM_ && bn == BN_) {                                 \

@@ -11,6 +11,7 @@ Reference: the conv/BN/ReLU stack of `pytorch_model.py:19-36,72-97`.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -20,6 +21,8 @@ from .conv import ConvSpec, slab_bytes
 HRMAX_PIX = 512                 # halo pixels per tile (csrc/hconv.hip HRMAX pieces x 32 pixels)
 LDS_MAX = 160 * 1024            # one workgroup may take the whole 160 KiB of a CU
 NSLOT = 3                       # weight ring slots (csrc/hconv.hip)
+PSLOT = 6                       # persistent kernel's weight ring (csrc PSLOT)
+PERSIST_TILES = ((256, 64), (128, 64), (64, 64))   # (BN = 128 rings exceed 160 KiB)
 TILES = ((256, 64, 4), (128, 64, 2), (64, 64, 1), (256, 128, 4), (128, 128, 2), (64, 128, 1))
 _WM = {(bm, bn): wm for bm, bn, wm in TILES}
 _ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
@@ -42,13 +45,30 @@ def supported(spec: ConvSpec):
 def lds_bytes(g, bm, bn, splits):
     """Dynamic LDS of one block (csrc/hconv.hip launch_one): one halo buffer per tile, two when
     a block walks several 64-channel slices (the next slice's halo is prefetched), the weight
-    ring, a 4 KB DMA sink; at least the epilogue's staging area."""
+    ring, a 4 KB DMA sink; at least the epilogue's staging area.  ``splits == 0`` is the
+    persistent kernel (launch_persist): two halo buffers (each large enough to stage the
+    epilogue), a 4-slot ring and the sink."""
     nch = g['C'] // 64
-    per = -(-nch // max(1, min(splits, nch)))
     hbytes = -(-g['HPIX'] // 32) * 32 * 128
-    main = (2 if per > 1 else 1) * hbytes + NSLOT * bn * 128 + 4096
     red = 16 * bn * 4 + bm * (bn + 8) * 2
+    if splits == 0:
+        if hbytes < red:                       # a halo buffer doubles as the epilogue's staging
+            return 1 << 30
+        return 2 * hbytes + PSLOT * bn * 128 + 4096
+    per = -(-nch // max(1, min(splits, nch)))
+    main = (2 if per > 1 else 1) * hbytes + NSLOT * bn * 128 + 4096
     return max(main, red)
+
+
+def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
+    """The persistent kernel runs this conv (else the launcher falls back to the per-tile
+    kernel): plain input, no bias, whole tiles, ghost-BN groups made of whole tiles."""
+    if pro is not None or bias is not None or (bm, bn) not in PERSIST_TILES:
+        return False
+    if spec.M % bm or spec.K % bn:
+        return False
+    grp = spec.group_rows or spec.M
+    return not stats or grp % bm == 0
 
 
 def _tile_shape(spec: ConvSpec, bm):
@@ -200,13 +220,46 @@ MEASURED_S2 = {
 }
 
 
+# Persistent-kernel winners (splits 0; bench/hconv_sweep.py at B=320, profiles/r2/
+# hconv_sweep_b320_persistent.jsonl): layer1 38.7 vs 53.9 us (best per-tile plan), layer2 35.4
+# vs 39.6, layer3 39.9 vs 40.9, the layer3 -> 4 stride-2 conv 33.6 vs igemm's 36.9 us.
+MEASURED_PERSIST = {
+    (320, 32, 64, 64): (256, 64, 0), (320, 16, 128, 128): (256, 64, 0),
+    (320, 8, 256, 256): (128, 64, 0),
+}
+MEASURED_PERSIST_S2 = {(320, 8, 256, 512): (64, 64, 0)}
+# slower than the per-tile / igemm plans in isolation, candidates beside the training stream
+# (MERCURY_HCONV_PERSIST=all)
+PERSIST_EXTRA = {(320, 4, 512, 512): (128, 64, 0), (320, 32, 64, 128): (64, 64, 0),
+                 (320, 16, 128, 256): (64, 64, 0)}
+
+
+def _persist_enabled():
+    return os.environ.get('MERCURY_HCONV_PERSIST', '1') != '0'
+
+
 def engine_plan(spec: ConvSpec):
-    """The plan the engine runs hconv with for this conv, or None (use igemm): measured winners,
-    else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every measured
-    shape)."""
-    if not supported(spec) or spec.stride != 1:
+    """The plan the engine runs hconv with for this conv, or None (use igemm): measured
+    persistent-kernel winners (MERCURY_HCONV_PERSIST=0 turns them off), measured per-tile
+    winners, else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every
+    measured shape)."""
+    if not supported(spec):
         return None
-    p = MEASURED.get((spec.N, spec.H, spec.C, spec.K))
+    key = (spec.N, spec.H, spec.C, spec.K)
+    if _persist_enabled():
+        p = (MEASURED_PERSIST if spec.stride == 1 else MEASURED_PERSIST_S2).get(key)
+        if p is None and os.environ.get('MERCURY_HCONV_PERSIST') == 'all':
+            p = PERSIST_EXTRA.get(key)
+        bm_env = int(os.environ.get('MERCURY_HCONV_PERSIST_BM', '0'))
+        if p is not None and bm_env:
+            p = (min(bm_env, p[0]), p[1], 0)
+        if p is not None and persistent_ok(spec, p[0], p[1]):
+            g = geometry_cached(spec, p[0], p[1])
+            if g is not None and lds_bytes(g, *p) <= LDS_MAX:
+                return p
+    if spec.stride != 1:
+        return None
+    p = MEASURED.get(key)
     if p is not None:
         g = geometry_cached(spec, p[0], p[1])
         if g is not None and lds_bytes(g, *p) <= LDS_MAX:

@@ -160,3 +160,51 @@ def test_hconv_matches_igemm_on_scoring_shapes():
         torch.cuda.synchronize()
         close(outs[1], outs[0], rtol=1e-2, atol=1e-2)
         close(sts[1], sts[0], rtol=1e-3, atol=0.5)
+
+
+PERSIST_CASES = [
+    # N, H, C, K, stride, (bm, bn), ghost images (0: one group)
+    (320, 32, 64, 64, 1, (128, 64), 32),     # layer1 scoring shape: 10 tiles per block
+    (320, 32, 64, 64, 1, (256, 64), 32),     # 256-row tiles (4 x 1 waves)
+    (320, 16, 128, 128, 1, (256, 64), 32),   # IMG = 1, TR = 16, two slices
+    (96, 32, 64, 64, 1, (64, 64), 0),        # uneven tiles per block, no ghost groups
+    (160, 16, 128, 128, 1, (128, 64), 32),   # two slices per tile, two N tiles
+    (128, 32, 64, 128, 2, (64, 64), 32),     # stride 2 (even / odd column halves)
+    (320, 8, 256, 256, 1, (128, 64), 32),    # IMG = 2, four slices, four N tiles
+    (320, 4, 512, 512, 1, (64, 64), 32),     # IMG = 4, eight slices
+]
+
+
+@pytest.mark.parametrize('with_stats', [True, False])
+@pytest.mark.parametrize('case', PERSIST_CASES)
+def test_hconv_persistent(case, with_stats):
+    """Persistent plan (splits == 0): one block per CU walking a strided tile list as one
+    continuous DMA / MFMA pipeline -- output and ghost-BN sums vs torch fp32."""
+    from mercury_amd import ops
+    from mercury_amd.ops import hconv as H
+    from mercury_amd.ops.conv import ConvSpec
+    ops.lib()
+    N, Hh, C, K, st, (bm, bn), gimgs = case
+    spec = ConvSpec(N, Hh, Hh, C, K, 3, 3, st, 1)
+    G = N // gimgs if gimgs else 1
+    if gimgs:
+        spec.group_rows = gimgs * spec.P * spec.Q
+    geo = H.geometry(spec, bm, bn)
+    assert geo is not None and H.lds_bytes(geo, bm, bn, 0) <= H.LDS_MAX
+    assert H.persistent_ok(spec, bm, bn, stats=with_stats)
+    g = torch.Generator(device='cpu').manual_seed(5)
+    x = bf(torch.randn(N, C, Hh, Hh, generator=g))
+    w = bf(torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9))
+    ref = F.conv2d(x, w, stride=st, padding=1)
+    wk, _ = ops.pack_conv_weight(w.to(DEV))
+    out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
+    ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
+    H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, (bm, bn, 0), stats=ostats)
+    torch.cuda.synchronize()
+    got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
+    assert not torch.isnan(got).any()
+    close(got, ref)
+    if with_stats:
+        rg = bf(ref).view(G, -1, K, spec.P, spec.Q)
+        close(ostats[:, 0].cpu(), rg.sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+        close(ostats[:, 1].cpu(), rg.pow(2).sum((1, 3, 4)), rtol=1e-2, atol=0.5)
