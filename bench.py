@@ -82,7 +82,7 @@ def diagnostics(eng, steps, ws):
           'comm_ranks': eng.comm.size if eng.comm is not None else
           (dist.get_world_size() if dist.is_initialized() else 1),
           'buckets_bytes': [4 * (e - s) for s, e in sorted(plan.values(), reverse=True)],
-          'wire': 'bf16' if eng.wire_bf16 else 'fp32',
+          'wire': 'ternary' if eng.grad_compress else ('bf16' if eng.wire_bf16 else 'fp32'),
           'allreduce_ms_per_step': med.get('comm'), 'comm_exposed_ms': med.get('comm_exposed'),
           'overlap_frac': med.get('overlap')}
     torch.cuda.synchronize()
@@ -113,6 +113,8 @@ def main():
                     help='DP all-reduce: own RCCL communicator on a comm stream, the direct-xGMI '
                          'two-shot over IPC-mapped peer buffers, or the torch ProcessGroup')
     ap.add_argument('--wire-bf16', action='store_true', help='bf16 gradients on the wire')
+    ap.add_argument('--compress', default='none', choices=('none', 'ternary'),
+                    help='ternary-compressed gradient all-reduce (parallel/compress.py)')
     ap.add_argument('--sampler', default='alias', choices=('alias', 'cdf', 'groupwise'),
                     help="pool draw kernel, or 'groupwise': draws from the HBM importance table "
                          'over the current contiguous-slice group (Groupwise_Sampler)')
@@ -155,7 +157,8 @@ def main():
                            lr=0.001 * ws, seed=7 + rank, importance=importance, world_size=ws,
                            use_graphs=not args.no_graphs, image_hw=hw,
                            force_buckets=args.force_buckets, comm=args.comm,
-                           wire_bf16=args.wire_bf16, sampler=args.sampler)
+                           wire_bf16=args.wire_bf16, sampler=args.sampler,
+                           grad_compress=args.compress)
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)

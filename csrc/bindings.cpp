@@ -395,6 +395,16 @@ PYBIND11_MODULE(_C, m) {
     quantize_launch(P<const float>(x), P<float>(out), P<float>(ws), n, seed, counter, S(st));
     check_launch("quantize");
   });
+  m.def("tern_pack", [](uintptr_t x, long long n, uintptr_t ws, uint32_t seed, uint64_t counter,
+                        uintptr_t words, uintptr_t st) {
+    tern_pack_launch(P<const float>(x), n, P<float>(ws), seed, counter, P<uint32_t>(words), S(st));
+    check_launch("tern_pack");
+  });
+  m.def("tern_unpack", [](uintptr_t msgs, int W, long long n, float scale, uintptr_t out,
+                          uintptr_t st) {
+    tern_unpack_launch(P<const uint32_t>(msgs), W, n, scale, P<float>(out), S(st));
+    check_launch("tern_unpack");
+  });
   m.def("pool2d_fwd", [](uintptr_t x, uintptr_t y, uintptr_t argmax, int N, int H, int W, int C,
                          int Pp, int Q, int k, int stride, int pad, int is_max, uintptr_t st) {
     PoolArgs a{P<const bf16>(x), P<bf16>(y), P<int>(argmax), N, H, W, C, Pp, Q, k, stride, pad, is_max};

@@ -95,6 +95,64 @@ __global__ __launch_bounds__(NT) void quantize_kernel(const float* x, float* y, 
   y[i] = (v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f)) * m * keep;
 }
 
+// Ternary gradient wire (the quantiser above as a compressed all-reduce): element i of a
+// bucket travels as 2 bits c in {0: 0, 1: +1, 2: -1} drawn with P(|c| = 1) = |x| / max|x|, and
+// the bucket's max|x| as one fp32 word -- 16 elements per int32 word, message = 1 + n/16 words.
+// Unbiased per rank (E[scale * c] = x); the receiver sums scale_r * c_r over the W messages.
+__global__ __launch_bounds__(NT) void tern_pack_kernel(const float* x, long long n,
+                                                       const float* amax, uint32_t seed,
+                                                       uint64_t counter, uint32_t* words) {
+  const long long j = (long long)blockIdx.x * NT + threadIdx.x;   // word index
+  const long long nw = (n + 15) / 16;
+  const float m = *amax;
+  if (j == 0) words[0] = __float_as_uint(m);
+  if (j >= nw) return;
+  uint32_t w = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long e0 = j * 16 + q * 4;
+    const u32x4 r = philox4x32(u32x4{(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)counter,
+                                     (uint32_t)(counter >> 32)}, seed, 0x85EBCA6Bu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long e = e0 + k;
+      if (e < n) {
+        const float v = x[e];
+        const uint32_t rk = k == 0 ? r.x : (k == 1 ? r.y : (k == 2 ? r.z : r.w));
+        const bool keep = m > 0.f && u01(rk) < fabsf(v) / m;
+        const uint32_t c = keep ? (v > 0.f ? 1u : (v < 0.f ? 2u : 0u)) : 0u;
+        w |= c << (2 * (q * 4 + k));
+      }
+    }
+  }
+  words[1 + j] = w;
+}
+
+// out[i] = scale * sum_r max_r * c_r[i] over W gathered messages of nw words each
+__global__ __launch_bounds__(NT) void tern_unpack_kernel(const uint32_t* msgs, int W, long long nw,
+                                                         long long n, float scale, float* out) {
+  const long long j = (long long)blockIdx.x * NT + threadIdx.x;
+  if (j >= nw - 1) return;
+  float acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+  for (int r = 0; r < W; ++r) {
+    const uint32_t* m = msgs + (size_t)r * nw;
+    const float mx = __uint_as_float(m[0]);
+    const uint32_t w = m[1 + j];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t c = (w >> (2 * k)) & 3u;
+      acc[k] += c == 1u ? mx : (c == 2u ? -mx : 0.f);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const long long e = j * 16 + k;
+    if (e < n) out[e] = acc[k] * scale;
+  }
+}
+
 __global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* x, bf16* y, int N, int C, int H,
                                                            int W, int Cpad) {
   const long long total = (long long)N * H * W * Cpad;
@@ -124,6 +182,22 @@ void quantize_launch(const float* x, float* out, float* absmax_ws, long long n, 
                      n, absmax_ws);
   hipLaunchKernelGGL(quantize_kernel, dim3((unsigned)blocks), dim3(NT), 0, st, x, out, absmax_ws, n,
                      seed, counter);
+}
+void tern_pack_launch(const float* x, long long n, float* absmax_ws, uint32_t seed,
+                      uint64_t counter, uint32_t* words, hipStream_t st) {
+  hipMemsetAsync(absmax_ws, 0, sizeof(float), st);
+  const long long blocks = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks > 1024 ? 1024 : blocks)), dim3(NT), 0, st,
+                     x, n, absmax_ws);
+  const long long nw = (n + 15) / 16;
+  hipLaunchKernelGGL(tern_pack_kernel, dim3((unsigned)((nw + NT - 1) / NT)), dim3(NT), 0, st, x, n,
+                     absmax_ws, seed, counter, words);
+}
+void tern_unpack_launch(const uint32_t* msgs, int W, long long n, float scale, float* out,
+                        hipStream_t st) {
+  const long long nw = 1 + (n + 15) / 16;
+  hipLaunchKernelGGL(tern_unpack_kernel, dim3((unsigned)((nw - 1 + NT - 1) / NT)), dim3(NT), 0, st,
+                     msgs, W, nw, n, scale, out);
 }
 void nchw_to_nhwc8_launch(const float* x, bf16* y, int N, int C, int H, int W, int Cpad,
                           hipStream_t st) {

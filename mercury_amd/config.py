@@ -50,6 +50,8 @@ class Config:
     parity: bool = False            # reference quirks: per-param init all-reduce, 10 separate scoring forwards
     bucket_mb: float = 0.0          # 0 -> default_bucket_bytes(W)
     wire_bf16: bool = False         # bf16 gradient all-reduce
+    grad_compress: str = 'none'     # 'ternary': stochastic 2-bit gradient wire (quantize_tensor,
+                                    # util.py:65-70; parallel/compress.py), native DP path
     overlap: bool = True            # scoring of step t+1 overlaps backward/all-reduce of step t
     use_graphs: bool = True
     comm: str = 'auto'              # native DP all-reduce: 'rccl' (own communicator + comm stream),

@@ -68,7 +68,7 @@ class NativeEngine(object):
                  importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
                  sampler='alias', exchange_scores=False, global_table=True, score='loss',
                  global_ema=False, autotune=None, force_buckets=False, comm='auto',
-                 wire_bf16=False, debug=False, check_order=False):
+                 wire_bf16=False, debug=False, check_order=False, grad_compress=None):
         ops.lib()
         if autotune is not None:
             tune.enable(autotune)
@@ -106,6 +106,13 @@ class NativeEngine(object):
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
+        if grad_compress not in (None, 'none', 'ternary'):
+            raise ValueError("grad_compress must be None, 'none' or 'ternary'")
+        if grad_compress == 'ternary' and (wire_bf16 or comm == 'xgmi'):
+            raise ValueError('grad_compress=ternary is its own wire format (no bf16 / xgmi)')
+        self.grad_compress = grad_compress if grad_compress != 'none' else None
+        self.tern = None                 # ternary-compressed all-reduce (parallel/compress.py)
+        self._tern_ctr = 0
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
         self.units = []
         for blk in self.lw.blocks:
@@ -175,6 +182,10 @@ class NativeEngine(object):
             from ..parallel.xgmi import XgmiAllReduce
             cap = max(e - s_ for s_, e in self.bucket_plan().values())
             self.xgmi = XgmiAllReduce(cap, self.device, wire_bf16=wire_bf16)
+        if self.dp and self.grad_compress == 'ternary':
+            from ..parallel.compress import TernaryAllReduce
+            cap = max(e - s_ for s_, e in self.bucket_plan().values())
+            self.tern = TernaryAllReduce(cap, self.device, comm=self.comm, seed=seed)
 
     # ------------------------------------------------------------------ parameters
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
@@ -1036,7 +1047,12 @@ class NativeEngine(object):
         """Issue bucket ``i``'s gradient all-reduce behind train segment ``si``."""
         s, e = bucket
         g = self.opt.g[s:e]
+        if self.tern is not None:
+            self._tern_ctr += 1          # a fresh Philox stream per (step, bucket)
         if self.s_comm is None:          # torch ProcessGroup (gloo / CPU tests)
+            if self.tern is not None:
+                self.tern.allreduce(g, self._tern_ctr)
+                return None
             return [dist.all_reduce(g, op=self._avg_op, async_op=True), s, e, False]
         ev = torch.cuda.Event()
         ev.record(s0)
@@ -1050,6 +1066,10 @@ class NativeEngine(object):
                 # direct two-shot over xGMI (all peers' exchange buffers mapped by IPC); the
                 # bf16 wire option lives in its exchange buffers
                 self.xgmi.allreduce(g, avg=True)
+            elif self.tern is not None:
+                # 2-bit stochastic ternary codes + one scale per rank, all-gathered (1/16 of
+                # the fp32 bytes), decoded to the same mean on every rank
+                self.tern.allreduce(g, self._tern_ctr)
             elif self.wire_bf16:
                 # bf16 on the wire: half the bytes over xGMI; the sum is rounded once per hop
                 if self.wire is None:
@@ -1187,6 +1207,7 @@ class NativeTrainer(Trainer):
             bucket_bytes=int(cfg.bucket_mb * (1 << 20)) or None, use_graphs=cfg.use_graphs,
             sampler=cfg.sampler, exchange_scores=cfg.exchange_scores,
             score=cfg.score, global_ema=cfg.global_ema, wire_bf16=cfg.wire_bf16,
+            grad_compress=cfg.grad_compress,
             comm=cfg.comm, debug=cfg.debug, check_order=cfg.check_order,
             force_buckets=cfg.force_buckets)
         self.engine.set_shard(x, y)

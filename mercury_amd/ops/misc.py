@@ -15,6 +15,25 @@ def quantize(x, out=None, ws=None, seed=0, counter=0):
     return out
 
 
+def tern_pack(x, words, ws, seed=0, counter=0):
+    """x fp32 [n] -> int32 message [1 + ceil(n/16)] (parallel/compress.py layout)."""
+    _chk(x, torch.float32, 'x')
+    n = x.numel()
+    _chk(words, torch.int32, 'words', 1 + (n + 15) // 16)
+    lib().tern_pack(ptr(x), n, ptr(ws), int(seed) & 0xffffffff, int(counter), ptr(words),
+                    stream_ptr())
+    return words
+
+
+def tern_unpack(msgs, W, n, out, scale=None):
+    """out[n] = scale * sum over W messages of max_r * code_r (scale defaults to 1/W)."""
+    _chk(msgs, torch.int32, 'msgs', W * (1 + (n + 15) // 16))
+    _chk(out, torch.float32, 'out', n)
+    lib().tern_unpack(ptr(msgs), W, n, 1.0 / W if scale is None else float(scale), ptr(out),
+                      stream_ptr())
+    return out
+
+
 def pool2d_fwd(x, y, N, H, W, C, P, Q, k, stride, pad, is_max=True, argmax=None):
     lib().pool2d_fwd(ptr(x), ptr(y), ptr(argmax), N, H, W, C, P, Q, k, stride, pad, int(is_max),
                      stream_ptr())
