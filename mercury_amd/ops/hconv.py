@@ -248,7 +248,8 @@ def engine_plan(spec: ConvSpec):
     key = (spec.N, spec.H, spec.C, spec.K)
     if _persist_enabled():
         p = (MEASURED_PERSIST if spec.stride == 1 else MEASURED_PERSIST_S2).get(key)
-        if p is None and os.environ.get('MERCURY_HCONV_PERSIST') == 'all':
+        mode = os.environ.get('MERCURY_HCONV_PERSIST', '1')
+        if p is None and (mode == 'all' or (mode == 'l4' and spec.stride == 1)):
             p = PERSIST_EXTRA.get(key)
         bm_env = int(os.environ.get('MERCURY_HCONV_PERSIST_BM', '0'))
         if p is not None and bm_env:
