@@ -564,10 +564,11 @@ MA_DEV void wait_tap(int t, bool hd, bool hn, bool epi, bool ew) {
 #undef WT
 }
 
-template <int BM, int BN, int WM, int NHB, int HRC, bool STATS>
+template <int BM, int BN, int WM, int NHB, int HRC, bool STATS, int MODE>
 __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __restrict__ src,
                                                               const bf16* __restrict__ wt,
-                                                              HconvGeom g, EpiParams e) {
+                                                              HconvGeom g, EpiParams e,
+                                                              HconvPro pro) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr int BI = BN / 32;                       // weight DMA pieces per wave per step
@@ -577,6 +578,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
   constexpr int PHI = HRC / PHP;                    // halo pieces per wave on a carrying tap
   static_assert(PHP <= T - 3, "a slice's halo lands >= 2 steps before its first read");
   static_assert(HRC % PHP == 0 && HRC <= HRMAX, "halo piece capacity");
+  static_assert(MODE == 0 || MODE == 1, "persistent kernel: plain or BN + activation input");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
     }
   }
   unsigned hoff[HRC];                                // byte offsets of the current halo (OOB: pad)
+  int hgrp = 0;                                      // ... and its statistics group (MODE 1)
   const float rntn = 1.f / (float)ntn, rpq = 1.f / (float)PQ, rq = 1.f / (float)g.Q;
   auto tile_of = [&](int k, int& m0, int& n0) {
     const int t = xcd_tile(k * G + b, ntiles);
@@ -647,6 +650,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
     const int p0 = udiv24(m0 - n0i * PQ, g.Q, rq);
     const int h0 = p0 * g.stride - g.pad;
     const int toff = (n0i * g.H + h0) * g.W * g.C * 2;
+    if constexpr (MODE == 1) hgrp = n0i / pro.group_imgs;   // a tile's images share a group
 #pragma unroll
     for (int i = 0; i < HRC; ++i)
       hoff[i] = (unsigned)(h0 + hrow[i]) < (unsigned)g.H ? (unsigned)(hbase[i] + toff) : OOB;
@@ -685,6 +689,44 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
   const unsigned s_halo = lds_addr(smem);
   const unsigned s_ring = s_halo + NHB * HBYTES;
   const unsigned s_dump = s_ring + PSLOT * SLOT + wu * 1024;
+  // MODE 1: per-(statistics group, 8-channel chunk) BN scale[8] | shift[8] of the input, built
+  // once per block in LDS, so the halo transform reads no global memory (a compiler-visible
+  // load there would make hipcc drain every in-flight DMA)
+  float* const coef = (float*)(smem + NHB * HBYTES + PSLOT * SLOT + 4096);
+  float csc[8], csh[8];                               // this thread's chunk of the slice
+
+  // in-place BN + activation of this thread's own DMA'd chunks (pieces j0 <= j < j1) of a landed
+  // halo (buffer hb_i, 64-channel slice cb, statistics group grp); padding pixels stay zero
+  auto xform = [&](int hb_i, int j0, int j1) {
+    if constexpr (MODE == 1) {
+      float lo, hi;
+      act_bounds(pro.act, lo, hi);
+      char* hb = smem + hb_i * HBYTES + (tid >> 3) * 128 + (tid & 7) * 16;
+#pragma unroll
+      for (int j = 0; j < HRC; ++j) {
+        if (j < j0 || j >= j1 || j >= HR || hoff[j] == OOB) continue;
+        u32x4* lp = (u32x4*)(hb + j * 4096);
+        const bf16x8 y = __builtin_bit_cast(bf16x8, *lp);
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(fminf(fmaxf(bf2f(y[q]) * csc[q] + csh[q], lo), hi));
+        *lp = __builtin_bit_cast(u32x4, o);
+      }
+    }
+  };
+  auto load_coef_lds = [&](int cb, int grp) {
+    if constexpr (MODE == 1) {
+      const f32x4* c = (const f32x4*)(coef + ((size_t)grp * (g.C >> 3) + cb * 8 + lc) * 16);
+      const f32x4 a = c[0], b2 = c[1], d = c[2], f = c[3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        csc[q] = a[q];
+        csc[4 + q] = b2[q];
+        csh[q] = d[q];
+        csh[4 + q] = f[q];
+      }
+    }
+  };
 
   auto issue_h = [&](int cb, int buf, int j) {
     // (HR through an empty asm: hoisted, the 16 `j < HR` tests were kept as lane masks and
@@ -740,23 +782,42 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
       }
     }
   };
-  // ---- prologue: halos of slices 0 .. D-1, weight tiles of steps 0..PDW-1, fragments of step 0
+  // ---- prologue: the BN table (MODE 1), slice 0's halo, weight tiles of steps 0..PDW-1,
+  // fragments of step 0
+  static_assert(D == 1, "one halo prefetched ahead");
+  static_assert(PDW < T, "prologue weight tiles lie in slice 0");
+  if constexpr (MODE == 1) {
+    const int G = pro.stats ? g.N / pro.group_imgs : 1;
+    for (int i = tid; i < G * g.C; i += NT) {
+      const int gi = i / g.C, c = i - gi * g.C;
+      float mean, var;
+      if (pro.stats) {
+        mean = pro.stats[(size_t)gi * 2 * g.C + c] * pro.inv_count;
+        var = fmaxf(pro.stats[(size_t)gi * 2 * g.C + g.C + c] * pro.inv_count - mean * mean, 0.f);
+      } else {
+        mean = pro.rmean[c];
+        var = pro.rvar[c];
+      }
+      const float sc = pro.gamma[c] * rsqrtf(var + pro.eps);
+      float* t = coef + ((size_t)gi * (g.C >> 3) + (c >> 3)) * 16 + (c & 7);
+      t[0] = sc;
+      t[8] = pro.beta[c] - mean * sc;
+    }
+  }
   set_halo(m0);
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    if (d < NS) {
-#pragma unroll
-      for (int j = 0; j < HRC; ++j)
-        if (j < HR) issue_h(clD, d, j);
-    }
-    advance_d();
-  }
-  // (kD, clD) = slice D: prefetched during slice 0
-  static_assert(PDW < T, "prologue weight tiles lie in slice 0");
+  for (int j = 0; j < HRC; ++j)
+    if (j < HR) issue_h(0, 0, j);
 #pragma unroll
   for (int t = 0; t < PDW; ++t) issue_b(n0, 0, t, t);
   vm_wait<0>();
-  bar_raw();
+  if constexpr (MODE == 1) {
+    bar_lds();                                        // the table is complete
+    load_coef_lds(0, hgrp);
+    xform(0, 0, HRC);
+  }
+  advance_d();                                        // (kD, clD) = slice 1: prefetched in slice 0
+  bar_lds();
   bf16x8 fa[2][TM], fb[2][TN];
   read_frags(fa, fb, 0, 0, 0);
   MA_STAMP(1);
@@ -801,8 +862,21 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
         wait_tap<T, BI, PHI, ST, STATS>(t, hd, hn, epi && t <= PDW - 2, ew);
       }
       MA_LAP(1, tl);
+      if constexpr (MODE == 1) {
+        // the next slice's halo pieces issued at tap t - (PDW - 1) have landed (this wave's
+        // own): normalise them in place; the tap-(T-1) barrier publishes the writes
+        constexpr int XT = PDW - 1;
+        static_assert(XT + PHP <= T - 1, "transform before the last tap's barrier");
+        if (hd && t >= XT && t < XT + PHP) {
+          if (t == XT) load_coef_lds(cbD, hgrp);
+          xform(bufD, (t - XT) * PHI, (t - XT + 1) * PHI);
+        }
+      }
       mma(0, NM / 2, 3 * NM / 4);
-      if (go) bar_raw();
+      if (go) {
+        if (MODE == 1 && t == T - 1) bar_lds();
+        else bar_raw();
+      }
       MA_LAP(2, tl);
       mma(0, 3 * NM / 4, NM);
       if (go) {
@@ -872,38 +946,50 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
 }
 
 // LDS of the persistent kernel: two halo buffers (each also the epilogue's staging area, so it
-// must hold Smem::RED_BYTES), the weight ring, the DMA sink
+// must hold Smem::RED_BYTES), the weight ring, the DMA sink, and (MODE 1) the BN table of
+// G x C scale / shift pairs
 template <int BM, int BN>
-int persist_lds_bytes(const HconvGeom& g) {
+int persist_lds_bytes(const HconvGeom& g, const HconvPro& pro) {
   const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
   if (hbytes < Smem<BM, BN>::RED_BYTES) return 1 << 30;
-  return 2 * hbytes + PSLOT * BN * 128 + 4096;
+  const int groups = pro.mode == 1 ? (pro.stats ? g.N / pro.group_imgs : 1) : 0;
+  return 2 * hbytes + PSLOT * BN * 128 + 4096 + groups * g.C * 8;
 }
 
-template <int BM, int BN, int WM, int HRC>
+template <int BM, int BN, int WM, int HRC, int MODE>
 void launch_persist_k(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
-                      int grid, int bytes, hipStream_t st) {
+                      const HconvPro& pro, int grid, int bytes, hipStream_t st) {
   static bool attr[2] = {false, false};
   const bool stats = e.stats != nullptr;
   if (!attr[stats]) {
-    (void)hipFuncSetAttribute(stats ? (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, true>
-                                    : (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(
+        stats ? (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, true, MODE>
+              : (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, false, MODE>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr[stats] = true;
   }
   if (stats)
-    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, true>), dim3(grid), dim3(NT),
-                       bytes, st, src, wt, g, e);
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, true, MODE>), dim3(grid),
+                       dim3(NT), bytes, st, src, wt, g, e, pro);
   else
-    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, false>), dim3(grid), dim3(NT),
-                       bytes, st, src, wt, g, e);
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, false, MODE>), dim3(grid),
+                       dim3(NT), bytes, st, src, wt, g, e, pro);
+}
+
+template <int BM, int BN, int WM, int HRC>
+void launch_persist_m(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                      const HconvPro& pro, int grid, int bytes, hipStream_t st) {
+  if (pro.mode == 1)
+    launch_persist_k<BM, BN, WM, HRC, 1>(src, wt, g, e, pro, grid, bytes, st);
+  else
+    launch_persist_k<BM, BN, WM, HRC, 0>(src, wt, g, e, pro, grid, bytes, st);
 }
 
 // grid = one block per CU; the halo piece capacity (8, 12 or 16 per wave) is the smallest that
 // holds the tile's halo, so carrying taps issue few pieces into the sink
 template <int BM, int BN, int WM>
 int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
-                   hipStream_t st) {
+                   const HconvPro& pro, hipStream_t st) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -924,15 +1010,15 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   }
   const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
   const int grid = ntiles < gmax ? ntiles : gmax;
-  const int bytes = persist_lds_bytes<BM, BN>(g);
+  const int bytes = persist_lds_bytes<BM, BN>(g, pro);
   if (bytes > 160 * 1024) return 0;
   const int hr = (g.HPIX + 31) >> 5;
   if (hr <= 8)
-    launch_persist_k<BM, BN, WM, 8>(src, wt, g, e, grid, bytes, st);
+    launch_persist_m<BM, BN, WM, 8>(src, wt, g, e, pro, grid, bytes, st);
   else if (hr <= 12)
-    launch_persist_k<BM, BN, WM, 12>(src, wt, g, e, grid, bytes, st);
+    launch_persist_m<BM, BN, WM, 12>(src, wt, g, e, pro, grid, bytes, st);
   else
-    launch_persist_k<BM, BN, WM, 16>(src, wt, g, e, grid, bytes, st);
+    launch_persist_m<BM, BN, WM, 16>(src, wt, g, e, pro, grid, bytes, st);
   return 1;
 }
 
@@ -1002,11 +1088,13 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   if (((g.HPIX + 31) >> 5) > HRMAX || g.R != 3) return 0;
   if (persist) {
     // persistent plan (splits == 0): plain whole tiles only, else the per-tile kernel below
-    const bool ok = pro.mode == 0 && e.bias == nullptr && !e.accumulate &&
+    const bool ok = (pro.mode == 0 || (pro.mode == 1 && pro.keep == nullptr)) &&
+                    e.bias == nullptr && !e.accumulate &&
                     e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
                     (e.stats == nullptr || e.group_rows % bm == 0);
 #define HP_CASE(BM_, BN_, WM_) \
-  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM_>(src, wt, g, e, st)) return 1;
+  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM_>(src, wt, g, e, pro, st)) \
+    return 1;
     HP_CASE(256, 64, 4)
     HP_CASE(128, 64, 2)
     HP_CASE(64, 64, 1)

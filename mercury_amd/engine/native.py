@@ -153,6 +153,12 @@ class NativeEngine(object):
         # per-SIMD blocks are faster alone but crowd the concurrently running train kernels out
         # of the CUs they share
         self.use_hconv = os.environ.get('MERCURY_HCONV', 'score')
+        # the scoring pass's intra-block BN + ReLU inside the persistent halo conv's staging.
+        # Off by default: same-box A/B (profiles/r2/ab_persist_bn.json) 1.528 off vs 1.551 ms
+        # on -- the in-LDS transform costs the persistent blocks more than the 8 bn_apply passes
+        # it removes cost the step
+        self.persist_bn = os.environ.get('MERCURY_PERSIST_BN', '0') == '1'
+
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
         self.sampler = sampler
@@ -297,6 +303,11 @@ class NativeEngine(object):
                     fb = self.fuse_bn_halo == '1' or \
                         self.fuse_bn_halo == ('train' if train else 'score')
                     hb = hconv.fused_plan(sp) if fb else None
+                    # scoring pass: an intra-block conv on the persistent kernel takes its
+                    # input's BN + activation in the halo staging (no residual there)
+                    if hb is None and not train and group_imgs and self.persist_bn and \
+                            u is not blk.units[0] and u is not blk.shortcut:
+                        hb = hconv.persist_bn_plan(sp, group_imgs)
                     if hb is not None:
                         m.plan[u.name, 'hconv_bn'] = hb
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hb))

@@ -42,6 +42,14 @@ def supported(spec: ConvSpec):
             and (spec.K <= 64 or spec.K % 128 == 0))
 
 
+def persist_table_bytes(spec: ConvSpec, pro):
+    """LDS of the persistent kernel's BN table (BN-applying input): G x C scale / shift."""
+    if pro is None:
+        return 0
+    G = spec.N // (pro.get('group_imgs') or spec.N) if pro.get('stats') is not None else 1
+    return G * spec.C * 8
+
+
 def lds_bytes(g, bm, bn, splits):
     """Dynamic LDS of one block (csrc/hconv.hip launch_one): one halo buffer per tile, two when
     a block walks several 64-channel slices (the next slice's halo is prefetched), the weight
@@ -62,8 +70,11 @@ def lds_bytes(g, bm, bn, splits):
 
 def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
     """The persistent kernel runs this conv (else the launcher falls back to the per-tile
-    kernel): plain input, no bias, whole tiles, ghost-BN groups made of whole tiles."""
-    if pro is not None or bias is not None or (bm, bn) not in PERSIST_TILES:
+    kernel): plain input or the input's BN + activation (no residual, no kept activation), no
+    bias, whole tiles, ghost-BN groups made of whole tiles."""
+    if pro is not None and any(pro.get(k) is not None for k in ('res', 'y2', 'keep')):
+        return False
+    if bias is not None or (bm, bn) not in PERSIST_TILES:
         return False
     if spec.M % bm or spec.K % bn:
         return False
@@ -270,6 +281,19 @@ def engine_plan(spec: ConvSpec):
     return None
 
 
+def persist_bn_plan(spec: ConvSpec, group_imgs):
+    """The persistent plan with the input's BN + activation in the halo staging (no residual),
+    or None.  Scoring pass only (MERCURY_PERSIST_BN, engine)."""
+    p = engine_plan(spec)
+    if p is None or p[2] != 0:
+        return None
+    pro = dict(stats=True, group_imgs=group_imgs)
+    g = geometry_cached(spec, p[0], p[1])
+    if g is None or lds_bytes(g, *p) + persist_table_bytes(spec, pro) > LDS_MAX:
+        return None
+    return p
+
+
 def fused_plan(spec: ConvSpec):
     """Plan for running this conv with its INPUT's BatchNorm (+ residual / shortcut BN) +
     activation applied in the halo staging, or None (bn_apply pass + plain conv instead).
@@ -338,8 +362,11 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
         raise ValueError('hconv does not support this conv')
     bm, bn, splits = p[:3]
     g = geometry_cached(spec, bm, bn)
-    if g is None or lds_bytes(g, bm, bn, splits) > LDS_MAX:
+    extra = persist_table_bytes(spec, pro) if splits == 0 else 0
+    if g is None or lds_bytes(g, bm, bn, splits) + extra > LDS_MAX:
         raise ValueError('hconv: tile %dx%d does not fit this conv' % (bm, bn))
+    if splits == 0 and not persistent_ok(spec, bm, bn, stats is not None, bias, pro):
+        raise ValueError('hconv: the persistent plan does not take this conv')
     if pro is not None and pro.get('keep') is not None and not keep_ok(spec):
         raise ValueError('hconv: keep needs a padded 3x3 conv whose halos tile the input')
     if splits > 1:

@@ -175,11 +175,12 @@ PERSIST_CASES = [
 ]
 
 
-@pytest.mark.parametrize('with_stats', [True, False])
+@pytest.mark.parametrize('with_stats', [True, False, 'bn'])
 @pytest.mark.parametrize('case', PERSIST_CASES)
 def test_hconv_persistent(case, with_stats):
     """Persistent plan (splits == 0): one block per CU walking a strided tile list as one
-    continuous DMA / MFMA pipeline -- output and ghost-BN sums vs torch fp32."""
+    continuous DMA / MFMA pipeline -- output and ghost-BN sums vs torch fp32.  'bn': the input's
+    ghost-group BN + ReLU applied in the halo staging (MODE 1)."""
     from mercury_amd import ops
     from mercury_amd.ops import hconv as H
     from mercury_amd.ops.conv import ConvSpec
@@ -193,13 +194,27 @@ def test_hconv_persistent(case, with_stats):
     assert geo is not None and H.lds_bytes(geo, bm, bn, 0) <= H.LDS_MAX
     assert H.persistent_ok(spec, bm, bn, stats=with_stats)
     g = torch.Generator(device='cpu').manual_seed(5)
-    x = bf(torch.randn(N, C, Hh, Hh, generator=g))
+    x = bf(torch.randn(N, C, Hh, Hh, generator=g) * 1.5 + 0.3)
     w = bf(torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9))
-    ref = F.conv2d(x, w, stride=st, padding=1)
+    pro, a = None, x
+    if with_stats == 'bn':
+        gi = gimgs or N
+        cnt = gi * Hh * Hh
+        xg = x.view(N // gi, gi, C, Hh, Hh)
+        st_in = torch.stack([xg.sum((1, 3, 4)), xg.pow(2).sum((1, 3, 4))], 1).contiguous()
+        gamma = torch.rand(C, generator=g) + 0.5
+        beta = torch.randn(C, generator=g) * 0.3
+        a = bf(torch.relu(_bn_ref(x, st_in, gamma, beta, cnt, N // gi)))
+        pro = dict(stats=st_in.reshape(-1).to(DEV), gamma=gamma.to(DEV), beta=beta.to(DEV),
+                   act='relu', eps=1e-5, count=cnt, group_imgs=gi)
+    if pro is not None and H.lds_bytes(geo, bm, bn, 0) + H.persist_table_bytes(spec, pro) > \
+            H.LDS_MAX:
+        pytest.skip('BN table does not fit beside this tile')
+    ref = F.conv2d(a, w, stride=st, padding=1)
     wk, _ = ops.pack_conv_weight(w.to(DEV))
     out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
-    H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, (bm, bn, 0), stats=ostats)
+    H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, (bm, bn, 0), stats=ostats, pro=pro)
     torch.cuda.synchronize()
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
     assert not torch.isnan(got).any()

@@ -83,12 +83,17 @@ def test_train_forward_backward_matches_torch(arch, hw):
     print(arch, 'worst grad error relative to torch-bf16', worst)
 
 
-def test_scoring_ghost_bn_matches_ten_separate_forwards():
+@pytest.mark.parametrize('persist_bn', ['0', '1'])
+def test_scoring_ghost_bn_matches_ten_separate_forwards(persist_bn, monkeypatch):
+    """(persist_bn: the intra-block BN + ReLU applied inside the persistent halo conv)"""
     from mercury_amd.models import ResNet18
+    monkeypatch.setenv('MERCURY_PERSIST_BN', persist_bn)
     torch.manual_seed(1)
     net = ResNet18(10).to(DEV)
     eng = _engine(net)
     sm = eng.score_mode
+    if persist_bn == '1':
+        assert any(k[1] == 'hconv_bn' and p[2] == 0 for k, p in sm.plan.items())
     sm.stats_arena.zero_()
     from mercury_amd import ops
     ops.pool_build(eng.shard, eng.shard_labels, eng.ctrl, sm.input, sm.label, sm.index, 320, 32,
