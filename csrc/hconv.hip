@@ -440,12 +440,13 @@ constexpr int PHP = 4;              // taps of a slice carrying the next slice's
 
 // epilogue of one persistent tile: bf16 round, ghost-BN sums (DPP rows -> LDS -> one atomic
 // pair per column), LDS-staged coalesced 16-byte row stores.  VMEM instructions per wave:
-// BM*BN/(8*NT) stores + 2 atomics on the waves with 64 w < BN (STATS).
-template <int BM, int BN, int WM, bool STATS>
-MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / 64], char* es,
+// BM*BN/(8*64*NW) stores + 2 atomics on the waves with 64 w < BN (STATS).
+template <int BM, int BN, int WM, int NW, bool STATS>
+MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)], char* es,
                         const EpiParams& e, int m0, int n0) {
-  constexpr int WN = 4 / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
-  constexpr int CPR = BN / 8, ST = BM * CPR / NT;
+  constexpr int NTP = 64 * NW;
+  constexpr int WN = NW / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
+  constexpr int CPR = BN / 8, ST = BM * CPR / NTP;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
   float* red = (float*)es;                          // [WM][2][BN] per-wave-row partials
@@ -501,7 +502,7 @@ MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / 64], char* 
   const int ch = tid % CPR;
 #pragma unroll
   for (int it = 0; it < ST; ++it) {
-    const int rl = (tid + it * NT) / CPR;
+    const int rl = (tid + it * NTP) / CPR;
     const bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
     *(bf16x8*)(e.out + (size_t)(m0 + rl) * e.ldo + n0 + ch * 8) = v;
   }
@@ -564,17 +565,20 @@ MA_DEV void wait_tap(int t, bool hd, bool hn, bool epi, bool ew) {
 #undef WT
 }
 
-template <int BM, int BN, int WM, int NHB, int HRC, bool STATS, int MODE>
-__global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __restrict__ src,
+template <int BM, int BN, int WM, int NW, int NHB, int HRC, bool STATS, int MODE>
+__global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* __restrict__ src,
                                                               const bf16* __restrict__ wt,
                                                               HconvGeom g, EpiParams e,
                                                               HconvPro pro) {
-  constexpr int WN = 4 / WM;
+  constexpr int NTP = 64 * NW;                      // threads (NW waves, one block per CU)
+  constexpr int WN = NW / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  constexpr int BI = BN / 32;                       // weight DMA pieces per wave per step
+  constexpr int PPX = 8 * NW;                       // halo pixels per DMA piece (8 per wave)
+  constexpr int BI = BN / PPX;                      // weight DMA pieces per wave per step
+  static_assert(BI >= 1 && BN % PPX == 0, "whole weight pieces per wave");
   constexpr int SLOT = BN * 128;
   constexpr int R = 3, T = R * R;
-  constexpr int ST = BM * BN / (8 * NT);
+  constexpr int ST = BM * BN / (8 * NTP);
   constexpr int PHI = HRC / PHP;                    // halo pieces per wave on a carrying tap
   static_assert(PHP <= T - 3, "a slice's halo lands >= 2 steps before its first read");
   static_assert(HRC % PHP == 0 && HRC <= HRMAX, "halo piece capacity");
@@ -600,8 +604,8 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
 #endif
   const int nsl = g.C >> 6;
   const int Kt = T * g.C;
-  const int HR = (g.HPIX + 31) >> 5;
-  const int HBYTES = HR * 32 * 128;
+  const int HR = (g.HPIX + PPX - 1) / PPX;
+  const int HBYTES = HR * PPX * 128;
   const int lc = (lane & 7) ^ (lane >> 3);
   const int per_img = g.HT * g.HWP;
   const auto rs_src = buf_rsrc(src, (unsigned)((size_t)g.N * g.H * g.W * g.C * 2));
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
   for (int i = 0; i < HRC; ++i) {
     hbase[i] = 0;
     hrow[i] = HROW_NONE;
-    const int pix = (tid >> 3) + 32 * i;
+    const int pix = (tid >> 3) + PPX * i;
     if (i < HR && pix < g.HPIX) {
       const int img = pix / per_img, rem = pix - img * per_img;
       const int hr = rem / g.HWP, col = rem - hr * g.HWP;
@@ -676,7 +680,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
   }
   unsigned boff[BI];                                 // weight rows this lane fetches (bytes)
 #pragma unroll
-  for (int j = 0; j < BI; ++j) boff[j] = ((8 * (w + 4 * j) + (lane >> 3)) * Kt + lc * 8) * 2;
+  for (int j = 0; j < BI; ++j) boff[j] = ((8 * (w + NW * j) + (lane >> 3)) * Kt + lc * 8) * 2;
   // B-fragment byte offsets inside a ring slot (tap-invariant)
   int bfo[2][TN];
 #pragma unroll
@@ -688,11 +692,11 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
     }
   const unsigned s_halo = lds_addr(smem);
   const unsigned s_ring = s_halo + NHB * HBYTES;
-  const unsigned s_dump = s_ring + PSLOT * SLOT + wu * 1024;
+  const unsigned s_dump = s_ring + PSLOT * SLOT + wu * 1024;      // 1 KB per wave
   // MODE 1: per-(statistics group, 8-channel chunk) BN scale[8] | shift[8] of the input, built
   // once per block in LDS, so the halo transform reads no global memory (a compiler-visible
   // load there would make hipcc drain every in-flight DMA)
-  float* const coef = (float*)(smem + NHB * HBYTES + PSLOT * SLOT + 4096);
+  float* const coef = (float*)(smem + NHB * HBYTES + PSLOT * SLOT + NW * 1024);
   float csc[8], csh[8];                               // this thread's chunk of the slice
 
   // in-place BN + activation of this thread's own DMA'd chunks (pieces j0 <= j < j1) of a landed
@@ -705,7 +709,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
 #pragma unroll
       for (int j = 0; j < HRC; ++j) {
         if (j < j0 || j >= j1 || j >= HR || hoff[j] == OOB) continue;
-        u32x4* lp = (u32x4*)(hb + j * 4096);
+        u32x4* lp = (u32x4*)(hb + j * PPX * 128);
         const bf16x8 y = __builtin_bit_cast(bf16x8, *lp);
         bf16x8 o;
 #pragma unroll
@@ -733,14 +737,14 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
     // spilled to VGPR lanes)
     int hr = HR;
     asm volatile("" : "+s"(hr));
-    bdma16(rs_src, hoff[j] + cb * 128, j < hr ? s_halo + buf * HBYTES + (32 * j + 8 * wu) * 128
+    bdma16(rs_src, hoff[j] + cb * 128, j < hr ? s_halo + buf * HBYTES + (PPX * j + 8 * wu) * 128
                                               : s_dump);
   };
   auto issue_b = [&](int n0, int cb, int t, int slot) {
     const unsigned k = (unsigned)((n0 * Kt + t * g.C + cb * 64) * 2);
 #pragma unroll
     for (int j = 0; j < BI; ++j)
-      bdma16(rs_wt, boff[j] + k, s_ring + slot * SLOT + 8 * (wu + 4 * j) * 128);
+      bdma16(rs_wt, boff[j] + k, s_ring + slot * SLOT + 8 * (wu + NW * j) * 128);
   };
   // fragments of (halo buffer, ring slot, tap); the k = 0..31 half first (the next step's
   // first MFMAs need only that)
@@ -788,7 +792,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
   static_assert(PDW < T, "prologue weight tiles lie in slice 0");
   if constexpr (MODE == 1) {
     const int G = pro.stats ? g.N / pro.group_imgs : 1;
-    for (int i = tid; i < G * g.C; i += NT) {
+    for (int i = tid; i < G * g.C; i += NTP) {
       const int gi = i / g.C, c = i - gi * g.C;
       float mean, var;
       if (pro.stats) {
@@ -832,8 +836,8 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
             fb[kk][i % TN], fa[kk][i / TN], acc[i / TN][i % TN], 0, 0, 0);
   };
 
-  // Step s (tap t of a slice): wait for step s + 1's weight tile, barrier, issue the DMAs of
-  // step s + PDW and this slice's share of halo pieces, read step s + 1's fragments.  The 2 NM
+  // Step s (tap t of a slice): wait for step s + 1's weight tile, barrier, read step s + 1's
+  // fragments, issue the DMAs of step s + PDW and this slice's share of halo pieces.  The 2 NM
   // MFMAs of step s are spread over all of it (the wait, the barrier and every DMA issue stall
   // the wave; MFMAs issued before them keep the matrix pipe busy).  Newer than the awaited tile
   // at the wait: tap_wait() pieces and, on taps <= PDW - 2 of a tile's first slice, the
@@ -891,7 +895,8 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
       bf16x8 na[2][TM], nb[2][TN];
       // step s + 1's fragments interleaved with the k = 32..63 half of step s (unconditional,
       // so reads and MFMAs share one basic block; the block's last step reads a stale slot it
-      // never uses)
+      // never uses).  (Reading them right after the barrier instead measured slower: 1.545 vs
+      // 1.526 ms/step, layer1 40.2 vs 38.7 us.)
       read_frags(na, nb, t + 1 < T ? buf : bnext, slot_of(t + 1), t + 1 < T ? t + 1 : 0);
       mma(1, 0, NM);
       constexpr int NR = 2 * (TM + TN);
@@ -914,7 +919,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
       MA_LAP(4, tl);
       if (t == T - 1 && last_sl) {
         // staged in this slice's halo buffer: fully read, refilled only from the next slice on
-        epi_persist<BM, BN, WM, STATS>(acc, smem + buf * HBYTES, e, m0, n0);
+        epi_persist<BM, BN, WM, NW, STATS>(acc, smem + buf * HBYTES, e, m0, n0);
         MA_LAP(5, tl);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -946,48 +951,67 @@ __global__ __launch_bounds__(NT, 1) void hconv_persist_kernel(const bf16* __rest
 }
 
 // LDS of the persistent kernel: two halo buffers (each also the epilogue's staging area, so it
-// must hold Smem::RED_BYTES), the weight ring, the DMA sink, and (MODE 1) the BN table of
-// G x C scale / shift pairs
-template <int BM, int BN>
+// must hold Smem::RED_BYTES), the weight ring, the DMA sink (1 KB per wave), and (MODE 1) the
+// BN table of G x C scale / shift pairs
+template <int BM, int BN, int NW>
 int persist_lds_bytes(const HconvGeom& g, const HconvPro& pro) {
-  const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
+  const int ppx = 8 * NW;
+  const int hbytes = ((g.HPIX + ppx - 1) / ppx) * ppx * 128;
   if (hbytes < Smem<BM, BN>::RED_BYTES) return 1 << 30;
   const int groups = pro.mode == 1 ? (pro.stats ? g.N / pro.group_imgs : 1) : 0;
-  return 2 * hbytes + PSLOT * BN * 128 + 4096 + groups * g.C * 8;
+  return 2 * hbytes + PSLOT * BN * 128 + NW * 1024 + groups * g.C * 8;
 }
 
-template <int BM, int BN, int WM, int HRC, int MODE>
+template <int BM, int BN, int WM, int NW, int HRC, int MODE>
 void launch_persist_k(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                       const HconvPro& pro, int grid, int bytes, hipStream_t st) {
   static bool attr[2] = {false, false};
   const bool stats = e.stats != nullptr;
   if (!attr[stats]) {
     (void)hipFuncSetAttribute(
-        stats ? (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, true, MODE>
-              : (const void*)hconv_persist_kernel<BM, BN, WM, 2, HRC, false, MODE>,
+        stats ? (const void*)hconv_persist_kernel<BM, BN, WM, NW, 2, HRC, true, MODE>
+              : (const void*)hconv_persist_kernel<BM, BN, WM, NW, 2, HRC, false, MODE>,
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr[stats] = true;
   }
   if (stats)
-    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, true, MODE>), dim3(grid),
-                       dim3(NT), bytes, st, src, wt, g, e, pro);
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, NW, 2, HRC, true, MODE>), dim3(grid),
+                       dim3(64 * NW), bytes, st, src, wt, g, e, pro);
   else
-    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, 2, HRC, false, MODE>), dim3(grid),
-                       dim3(NT), bytes, st, src, wt, g, e, pro);
+    hipLaunchKernelGGL((hconv_persist_kernel<BM, BN, WM, NW, 2, HRC, false, MODE>), dim3(grid),
+                       dim3(64 * NW), bytes, st, src, wt, g, e, pro);
 }
 
-template <int BM, int BN, int WM, int HRC>
+template <int BM, int BN, int WM, int NW, int HRC>
 void launch_persist_m(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                       const HconvPro& pro, int grid, int bytes, hipStream_t st) {
   if (pro.mode == 1)
-    launch_persist_k<BM, BN, WM, HRC, 1>(src, wt, g, e, pro, grid, bytes, st);
+    launch_persist_k<BM, BN, WM, NW, HRC, 1>(src, wt, g, e, pro, grid, bytes, st);
   else
-    launch_persist_k<BM, BN, WM, HRC, 0>(src, wt, g, e, pro, grid, bytes, st);
+    launch_persist_k<BM, BN, WM, NW, HRC, 0>(src, wt, g, e, pro, grid, bytes, st);
 }
 
-// grid = one block per CU; the halo piece capacity (8, 12 or 16 per wave) is the smallest that
-// holds the tile's halo, so carrying taps issue few pieces into the sink
-template <int BM, int BN, int WM>
+// one block per CU of the grid; the halo piece capacity (8, 12 or 16 per wave) is the smallest
+// that holds the tile's halo, so carrying taps issue few pieces into the sink
+template <int BM, int BN, int WM, int NW>
+int launch_persist_w(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                     const HconvPro& pro, int grid, hipStream_t st) {
+  const int bytes = persist_lds_bytes<BM, BN, NW>(g, pro);
+  if (bytes > 160 * 1024) return 0;
+  const int hr = (g.HPIX + 8 * NW - 1) / (8 * NW);
+  if (hr <= 8)
+    launch_persist_m<BM, BN, WM, NW, 8>(src, wt, g, e, pro, grid, bytes, st);
+  else if (hr <= 12)
+    launch_persist_m<BM, BN, WM, NW, 12>(src, wt, g, e, pro, grid, bytes, st);
+  else if (hr <= 16)
+    launch_persist_m<BM, BN, WM, NW, 16>(src, wt, g, e, pro, grid, bytes, st);
+  else
+    return 0;
+  return 1;
+}
+
+// WM4 / WM8: wave rows of the 4- and 8-wave blocks (MERCURY_HCONV_PERSIST_WAVES picks, 0 = none)
+template <int BM, int BN, int WM4, int WM8>
 int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                    const HconvPro& pro, hipStream_t st) {
   static int cus = 0;
@@ -1002,24 +1026,23 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   // grid on every CU (143 KB of LDS each) locks the training kernels out for its whole length.
   // Measured, ResNet-18 step (bench.py, same box): 256 blocks 1.653 ms, 192 1.590, 160 1.550,
   // 128 1.525, 96 1.720, 64 2.037; per-tile kernels 1.607.  MERCURY_HCONV_PERSIST_GRID overrides.
-  static int gmax = -1;
+  static int gmax = -1, waves = -1;
   if (gmax < 0) {
     const char* ev = getenv("MERCURY_HCONV_PERSIST_GRID");
     gmax = ev ? atoi(ev) : cus / 2;
     if (gmax <= 0 || gmax > cus) gmax = cus;
+    // 8 waves (two per SIMD: one wave's waits, barriers and DMA issue overlap the other's
+    // MFMAs) where the tile has an 8-wave layout; measured 1.513 vs 1.521 and 1.534 vs 1.549
+    // ms/step (two same-box A/Bs), layer2 alone 33.4 vs 35.4 us
+    const char* wv = getenv("MERCURY_HCONV_PERSIST_WAVES");
+    waves = wv ? atoi(wv) : 8;
   }
   const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
   const int grid = ntiles < gmax ? ntiles : gmax;
-  const int bytes = persist_lds_bytes<BM, BN>(g, pro);
-  if (bytes > 160 * 1024) return 0;
-  const int hr = (g.HPIX + 31) >> 5;
-  if (hr <= 8)
-    launch_persist_m<BM, BN, WM, 8>(src, wt, g, e, pro, grid, bytes, st);
-  else if (hr <= 12)
-    launch_persist_m<BM, BN, WM, 12>(src, wt, g, e, pro, grid, bytes, st);
-  else
-    launch_persist_m<BM, BN, WM, 16>(src, wt, g, e, pro, grid, bytes, st);
-  return 1;
+  if constexpr (WM8 > 0) {
+    if (waves == 8) return launch_persist_w<BM, BN, WM8, 8>(src, wt, g, e, pro, grid, st);
+  }
+  return launch_persist_w<BM, BN, WM4, 4>(src, wt, g, e, pro, grid, st);
 }
 
 template <int BM, int BN, int WM, int MODE>
@@ -1092,12 +1115,12 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
                     e.bias == nullptr && !e.accumulate &&
                     e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
                     (e.stats == nullptr || e.group_rows % bm == 0);
-#define HP_CASE(BM_, BN_, WM_) \
-  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM_>(src, wt, g, e, pro, st)) \
+#define HP_CASE(BM_, BN_, WM4_, WM8_)                                                 \
+  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM4_, WM8_>(src, wt, g, e, pro, st)) \
     return 1;
-    HP_CASE(256, 64, 4)
-    HP_CASE(128, 64, 2)
-    HP_CASE(64, 64, 1)
+    HP_CASE(256, 64, 4, 8)
+    HP_CASE(128, 64, 2, 8)
+    HP_CASE(64, 64, 1, 0)
 #undef HP_CASE
   }
   const dim3 grid(gx, gy);

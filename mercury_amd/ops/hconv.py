@@ -60,12 +60,21 @@ def lds_bytes(g, bm, bn, splits):
     hbytes = -(-g['HPIX'] // 32) * 32 * 128
     red = 16 * bn * 4 + bm * (bn + 8) * 2
     if splits == 0:
+        nw = persist_waves()
+        ppx = 8 * nw                           # halo pixels per DMA piece
+        hbytes = -(-g['HPIX'] // ppx) * ppx * 128
         if hbytes < red:                       # a halo buffer doubles as the epilogue's staging
             return 1 << 30
-        return 2 * hbytes + PSLOT * bn * 128 + 4096
+        return 2 * hbytes + PSLOT * bn * 128 + nw * 1024
     per = -(-nch // max(1, min(splits, nch)))
     main = (2 if per > 1 else 1) * hbytes + NSLOT * bn * 128 + 4096
     return max(main, red)
+
+
+def persist_waves():
+    """Waves per persistent block (csrc/hconv.hip launch_persist reads the same variable)."""
+    w = int(os.environ.get('MERCURY_HCONV_PERSIST_WAVES', '8'))
+    return 8 if w == 8 else 4
 
 
 def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
@@ -249,15 +258,16 @@ def _persist_enabled():
     return os.environ.get('MERCURY_HCONV_PERSIST', '1') != '0'
 
 
-def engine_plan(spec: ConvSpec):
+def engine_plan(spec: ConvSpec, bias=False):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured
     persistent-kernel winners (MERCURY_HCONV_PERSIST=0 turns them off), measured per-tile
     winners, else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every
     measured shape)."""
     if not supported(spec):
         return None
-    key = (spec.N, spec.H, spec.C, spec.K)
-    if _persist_enabled():
+    # (the measured tables are keyed by the square CIFAR shapes)
+    key = (spec.N, spec.H, spec.C, spec.K) if spec.H == spec.W else None
+    if _persist_enabled() and not bias and key is not None:
         p = (MEASURED_PERSIST if spec.stride == 1 else MEASURED_PERSIST_S2).get(key)
         mode = os.environ.get('MERCURY_HCONV_PERSIST', '1')
         if p is None and (mode == 'all' or (mode == 'l4' and spec.stride == 1)):
