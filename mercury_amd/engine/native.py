@@ -664,38 +664,46 @@ class NativeEngine(object):
                    reduce=reduce, **kw)
 
     def backward_block(self, m, bi):
+        for _, f in self.backward_parts(m, bi):
+            f()
+
+    def backward_parts(self, m, bi):
+        """Block ``bi``'s backward as [(unit index, callable)] in execution order (last unit
+        first): after part i, the gradients of units i..last, of the BNs of units i-1..last
+        and of the shortcut are final -- so a gradient bucket may close between parts."""
         blk = self.lw.blocks[bi]
         x = m.buf[bi - 1, 'out'] if bi > 0 else m.input
         dx = m.buf[bi - 1, 'dout'] if (bi > 0 and blk.need_dx) else None
-        dout = m.buf[bi, 'dout']
-        out = m.buf[bi, 'out']
-        if blk.pool:
-            N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
-            ops.maxpool2d_bwd(dout, m.buf[bi, 'argmax'], m.buf[bi, 'dpre'], N, h, w, K, P_, Q_,
-                              k, st, pd)
-            dout, out = m.buf[bi, 'dpre'], m.buf[bi, 'pre']
         units = blk.units
         last = units[-1]
         sc = blk.shortcut
-        dy_last = m.buf[last.name, 'dy']
-        dz = dx if (blk.identity and dx is not None) else None
-        pre = m.prereduced.pop(bi, False) and not blk.pool
-        self._bn_bwd(m, last, dout, out, blk.final_act, dy_last, unit2=sc,
-                     dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz, reduce=not pre)
-        if sc is not None:
-            self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
-        d = dy_last
-        for i in range(len(units) - 1, -1, -1):
+
+        def top():
+            dout = m.buf[bi, 'dout']
+            out = m.buf[bi, 'out']
+            if blk.pool:
+                N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
+                ops.maxpool2d_bwd(dout, m.buf[bi, 'argmax'], m.buf[bi, 'dpre'], N, h, w, K, P_,
+                                  Q_, k, st, pd)
+                dout, out = m.buf[bi, 'dpre'], m.buf[bi, 'pre']
+            dz = dx if (blk.identity and dx is not None) else None
+            pre = m.prereduced.pop(bi, False) and not blk.pool
+            self._bn_bwd(m, last, dout, out, blk.final_act, m.buf[last.name, 'dy'], unit2=sc,
+                         dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz, reduce=not pre)
+            if sc is not None:
+                self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
+
+        def unit(i):
             u = units[i]
+            d = m.buf[u.name, 'dy']
             inp = x if i == 0 else m.buf[units[i - 1].name, 'a']
             if i > 0:
                 prev = units[i - 1]
                 da = m.buf[prev.name, 'da']
                 fused = self._conv_bwd(m, u, d, inp, da, accumulate=False,
                                        bw=self._bw(m, prev, m.buf[prev.name, 'a'], prev.act))
-                dyp = m.buf[prev.name, 'dy']
-                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act, dyp, reduce=not fused)
-                d = dyp
+                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
+                             m.buf[prev.name, 'dy'], reduce=not fused)
             else:
                 acc = blk.identity or sc is not None
                 bw = None
@@ -710,6 +718,14 @@ class NativeEngine(object):
                                        accumulate=acc, bw=bw)
                 if fused:
                     m.prereduced[bi - 1] = True
+
+        parts = []
+        for i in range(len(units) - 1, -1, -1):
+            if i == len(units) - 1:
+                parts.append((i, lambda i=i: (top(), unit(i))))
+            else:
+                parts.append((i, lambda i=i: unit(i)))
+        return parts
 
     # ------------------------------------------------------------------ data
     def _device_inputs(self, images):
@@ -879,10 +895,11 @@ class NativeEngine(object):
         cuts = self.bucket_plan()
         cur = [fwd_head]
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
-            cur.append(lambda bi=bi: self.backward_block(tm, bi))
-            if bi in cuts:
-                segs.append((cur, cuts[bi]))
-                cur = []
+            for i, f in self.backward_parts(tm, bi):
+                cur.append(f)
+                if (bi, i) in cuts:
+                    segs.append((cur, cuts[bi, i]))
+                    cur = []
         if cur:
             segs.append((cur, None))
         if self.check_order:
@@ -899,18 +916,31 @@ class NativeEngine(object):
         return starts
 
     def bucket_plan(self):
-        """{block index: (flat_start, flat_end)} -- a bucket closes after that block's backward
-        once it holds >= ``bucket_bytes`` of gradient (and always at block 0).  Parameters are
-        laid out in forward order, so backward finishes them from the end of the flat buffer."""
+        """{(block, unit index): (flat_start, flat_end)} -- a bucket closes after that unit's
+        backward part (backward_parts) once it holds >= ``bucket_bytes`` of gradient, and
+        always after block 0's first unit.  Parameters are laid out in forward order, so the
+        backward finishes them from the end of the flat buffer; cutting inside a block (not
+        only at block boundaries) lets the first all-reduce start one conv earlier.  A block
+        whose shortcut parameters precede its last unit's is cut only at its boundary."""
         if not self.dp:
             return {}
         starts = self._block_starts()
         cuts = {}
         end = self.lw.total
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
-            if bi == 0 or (end - starts[bi]) * 4 >= self.bucket_bytes:
-                cuts[bi] = (0 if bi == 0 else starts[bi], end)
-                end = starts[bi]
+            blk = self.lw.blocks[bi]
+            ustart = [min(s.off for s in (u.w_seg, u.g_seg, u.beta_seg)) for u in blk.units]
+            inner = blk.shortcut is None or min(
+                s.off for s in (blk.shortcut.w_seg, blk.shortcut.g_seg,
+                                blk.shortcut.beta_seg)) >= ustart[-1]
+            inner = inner and all(ustart[i] < ustart[i + 1] for i in range(len(ustart) - 1))
+            for i in range(len(blk.units) - 1, -1, -1):
+                if i > 0 and not inner:
+                    continue
+                start = starts[bi] if i == 0 else ustart[i]
+                if (bi == 0 and i == 0) or (end - start) * 4 >= self.bucket_bytes:
+                    cuts[bi, i] = (0 if (bi == 0 and i == 0) else start, end)
+                    end = start
         return cuts
 
     def tail(self):
@@ -1097,7 +1127,7 @@ class NativeEngine(object):
 
     @property
     def _nseg(self):
-        return len(self.bucket_plan()) + (0 if 0 in self.bucket_plan() else 1)
+        return len(self.bucket_plan()) + (0 if (0, 0) in self.bucket_plan() else 1)
 
     def _debug_sync(self, what):
         """Debug mode: drain the device after every phase so a fault names its phase."""
