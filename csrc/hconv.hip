@@ -499,12 +499,17 @@ MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
       atomicAdd(dst + e.stats_ld, b);
     }
   }
-  const int ch = tid % CPR;
+  // 16-byte buffer stores: the lane's byte offset is tile-invariant, the row step per
+  // iteration and the tile origin go into the scalar offset (no 64-bit address VALU)
+  const int ch = tid % CPR, r0 = tid / CPR;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)e.out, 0, 0x7fffffff, 0x00020000);
+  const int voff = (r0 * e.ldo + ch * 8) * 2;
 #pragma unroll
   for (int it = 0; it < ST; ++it) {
-    const int rl = (tid + it * NTP) / CPR;
+    const int rl = r0 + it * (NTP / CPR);
     const bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
-    *(bf16x8*)(e.out + (size_t)(m0 + rl) * e.ldo + n0 + ch * 8) = v;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff,
+                                           ((m0 + it * (NTP / CPR)) * e.ldo + n0) * 2, 0);
   }
 }
 
