@@ -258,6 +258,17 @@ def _persist_enabled():
     return os.environ.get('MERCURY_HCONV_PERSIST', '1') != '0'
 
 
+def _plan_override(key):
+    """MERCURY_HCONV_PLANS="N,H,C,K=bm,bn,splits;..." (A/B runs): a plan for that shape, or
+    'none' for igemm.  Returns (found, plan)."""
+    ev = os.environ.get('MERCURY_HCONV_PLANS', '')
+    for item in filter(None, ev.split(';')):
+        k, v = item.split('=')
+        if tuple(int(t) for t in k.split(',')) == key:
+            return True, (None if v == 'none' else tuple(int(t) for t in v.split(',')))
+    return False, None
+
+
 def engine_plan(spec: ConvSpec, bias=False):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured
     persistent-kernel winners (MERCURY_HCONV_PERSIST=0 turns them off), measured per-tile
@@ -265,6 +276,14 @@ def engine_plan(spec: ConvSpec, bias=False):
     measured shape)."""
     if not supported(spec):
         return None
+    found, p = _plan_override((spec.N, spec.H, spec.C, spec.K))
+    if found and spec.H == spec.W:
+        if p is None:
+            return None
+        g = geometry_cached(spec, p[0], p[1])
+        if g is not None and lds_bytes(g, *p) <= LDS_MAX and (p[2] != 0 or (
+                not bias and persistent_ok(spec, p[0], p[1]))):
+            return p
     # (the measured tables are keyed by the square CIFAR shapes)
     key = (spec.N, spec.H, spec.C, spec.K) if spec.H == spec.W else None
     if _persist_enabled() and not bias and key is not None:
