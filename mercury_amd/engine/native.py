@@ -147,12 +147,12 @@ class NativeEngine(object):
         # their CUs; the bn_apply passes it removes are cheap to co-schedule
         self.fuse_bn_halo = os.environ.get('MERCURY_FUSE_BN_HALO', '0')
         # stride-1 3x3 forward convs on the halo-tile kernel (csrc/hconv.hip) where measured faster
-        # ('1' both batch modes, 'score' / 'train' one of them, '0' off).  Default: the scoring
-        # pass only -- same-box A/B of the two-stream step (profiles/r2/ab_hconv_modes.json):
-        # off 1.614, score 1.605, train 1.615, both 1.640 ms/step.  The halo conv's one-wave-
-        # per-SIMD blocks are faster alone but crowd the concurrently running train kernels out
-        # of the CUs they share
-        self.use_hconv = os.environ.get('MERCURY_HCONV', 'score')
+        # ('1' both batch modes, 'score' / 'train' one of them, '0' off).  With the per-tile
+        # kernel only the scoring pass gained (profiles/r2/ab_hconv_modes.json: off 1.614,
+        # score 1.605, train 1.615, both 1.640 ms/step -- its one-wave-per-SIMD blocks crowd the
+        # concurrent train kernels out); with the persistent 8-wave kernel on the train shapes
+        # too, both passes win: 1.536 (score) vs 1.521 ms (both), profiles/r2/ab_train_persist.json
+        self.use_hconv = os.environ.get('MERCURY_HCONV', '1')
         # the scoring pass's intra-block BN + ReLU inside the persistent halo conv's staging.
         # Off by default: same-box A/B (profiles/r2/ab_persist_bn.json) 1.528 off vs 1.551 ms
         # on -- the in-LDS transform costs the persistent blocks more than the 8 bn_apply passes

@@ -246,6 +246,10 @@ MEASURED_S2 = {
 MEASURED_PERSIST = {
     (320, 32, 64, 64): (256, 64, 0), (320, 16, 128, 128): (256, 64, 0),
     (320, 8, 256, 256): (128, 64, 0),
+    # train batch (one or two tiles per block: the 8-wave slice pipeline, not the tile stream,
+    # is what helps here): step 1.536 -> 1.521 ms same-box (profiles/r2/ab_train_persist.json)
+    (32, 32, 64, 64): (256, 64, 0), (32, 16, 128, 128): (128, 64, 0),
+    (32, 8, 256, 256): (64, 64, 0),
 }
 MEASURED_PERSIST_S2 = {(320, 8, 256, 512): (64, 64, 0)}
 # slower than the per-tile / igemm plans in isolation, candidates beside the training stream
