@@ -231,6 +231,9 @@ MEASURED = {
     (32, 32, 64, 64): (256, 64, 1), (32, 16, 128, 128): (64, 64, 1),
     (32, 8, 256, 256): (64, 64, 2), (32, 4, 512, 512): (64, 64, 4),
 }
+# shapes that stay on igemm in the engine although a halo plan exists: the train-batch layer4
+# conv (1.5011 vs 1.5058 ms/step over 3 same-box rounds, profiles/r2/ab_train_l4.json)
+MEASURED_IGEMM = {(32, 4, 512, 512)}
 
 
 # stride-2 3x3 convs (fused-BN use only): best plain plans of the same sweeps
@@ -302,7 +305,7 @@ def engine_plan(spec: ConvSpec, bias=False):
             g = geometry_cached(spec, p[0], p[1])
             if g is not None and lds_bytes(g, *p) <= LDS_MAX:
                 return p
-    if spec.stride != 1:
+    if spec.stride != 1 or key in MEASURED_IGEMM:
         return None
     p = MEASURED.get(key)
     if p is not None:
