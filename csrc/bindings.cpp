@@ -267,7 +267,7 @@ PYBIND11_MODULE(_C, m) {
                        int score_kind) {
     HeadArgs a{P<const bf16>(act), P<const float>(w), P<const float>(b), P<const int>(label),
                P<const float>(isw), P<float>(pooled), P<float>(logits), P<float>(dlogits),
-               P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0, score_kind};
+               P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0, score_kind, 0};
     head_fwd_launch(a, S(st));
     check_launch("head_fwd");
   });
@@ -406,14 +406,19 @@ PYBIND11_MODULE(_C, m) {
     check_launch("tern_unpack");
   });
   m.def("pool2d_fwd", [](uintptr_t x, uintptr_t y, uintptr_t argmax, int N, int H, int W, int C,
-                         int Pp, int Q, int k, int stride, int pad, int is_max, uintptr_t st) {
-    PoolArgs a{P<const bf16>(x), P<bf16>(y), P<int>(argmax), N, H, W, C, Pp, Q, k, stride, pad, is_max};
+                         int Pp, int Q, int k, int stride, int pad, int is_max, uintptr_t st,
+                         uintptr_t stats, uintptr_t gamma, uintptr_t beta, uintptr_t rmean,
+                         uintptr_t rvar, int group_imgs, int act, float eps) {
+    PoolArgs a{P<const bf16>(x), P<bf16>(y), P<uint8_t>(argmax), N, H, W, C, Pp, Q, k, stride,
+               pad, is_max, P<const float>(stats), P<const float>(gamma), P<const float>(beta),
+               P<const float>(rmean), P<const float>(rvar), group_imgs, act, eps};
     pool2d_fwd_launch(a, S(st));
     check_launch("pool2d_fwd");
   });
   m.def("maxpool2d_bwd", [](uintptr_t dy, uintptr_t argmax, uintptr_t dx, int N, int H, int W, int C,
                             int Pp, int Q, int k, int stride, int pad, uintptr_t st) {
-    PoolArgs a{nullptr, nullptr, P<int>(argmax), N, H, W, C, Pp, Q, k, stride, pad, 1};
+    PoolArgs a{nullptr, nullptr, P<uint8_t>(argmax), N, H, W, C, Pp, Q, k, stride, pad, 1,
+               nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0.f};
     maxpool2d_bwd_launch(a, P<const bf16>(dy), P<bf16>(dx), S(st));
     check_launch("maxpool2d_bwd");
   });

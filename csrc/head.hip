@@ -16,30 +16,171 @@
 namespace {
 constexpr int NT = 256;
 
+// Wide heads (ImageNet: 2048 -> 1000 at B = 1280) first run the pool and the FC as their own
+// launches -- the per-sample dot products above would stream the whole fp32 weight matrix
+// once per sample (10 GB of L2 traffic, ~0.9 ms) -- and this kernel then only does the loss.
+
+// pooled[b][c] = mean over HW of act[b][hw][c], one thread per (sample, 8 channels)
+__global__ __launch_bounds__(NT) void head_pool_kernel(const bf16* act, float* pooled, int B, int HW,
+                                                       int C) {
+  const int C8 = C >> 3;
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= B * C8) return;
+  const int b = i / C8, c = (i - b * C8) * 8;
+  const bf16* x = act + (size_t)b * HW * C + c;
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll 7
+  for (int hw = 0; hw < HW; ++hw) {
+    const bf16x8 v = *(const bf16x8*)(x + (size_t)hw * C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += bf2f(v[k]);
+  }
+  const float inv = 1.f / (float)HW;
+  float* o = pooled + (size_t)b * C + c;
+  *(float4*)o = make_float4(s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv);
+  *(float4*)(o + 4) = make_float4(s[4] * inv, s[5] * inv, s[6] * inv, s[7] * inv);
+}
+
+// fp32 tiled GEMM for the wide head, C[m][n] = sum_r A(m, r) * B(n, r) (+ bias[n]), exact fp32
+// like the per-sample path: 64x64 output tile per block, 4x4 per thread, 16-deep r slices
+// through LDS with the next slice's global loads in flight during the current slice's FMAs.
+// AR / BR: the operand is contiguous along r (row-major [m][r]) -- else along m / n
+// ([r][m]).  Uses:  logits = pooled . W^T (AR, BR);  dpooled = dlogits . W (AR, !BR);
+// dW = dlogits^T . pooled (!AR, !BR).  OUT 0: fp32 C; 1: bf16 C * scale broadcast over HW
+// spatial rows (the activation gradient of the average pool).
+constexpr int LT = 64, LK = 16;
+template <bool RC>
+MA_DEV float4 tile_load(const float* p, int ld, int i0, int ni, int r0, int nr, int tid) {
+  // RC: rows i (64) x 16 r, thread -> row tid/4, r (tid%4)*4..+3;  else 16 r x 64 i, thread ->
+  // r tid/16, i (tid%16)*4..+3
+  float v[4];
+  const int i = RC ? i0 + (tid >> 2) : i0 + (tid & 15) * 4;
+  const int r = RC ? r0 + (tid & 3) * 4 : r0 + (tid >> 4);
+  if (RC) {
+    const float* q = p + (size_t)i * ld + r;
+    if (i < ni && r + 3 < nr) return *(const float4*)q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (i < ni && r + j < nr) ? q[j] : 0.f;
+  } else {
+    const float* q = p + (size_t)r * ld + i;
+    if (r < nr && i + 3 < ni) return *(const float4*)q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (r < nr && i + j < ni) ? q[j] : 0.f;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+template <bool RC>
+MA_DEV void tile_store(float (*T)[LT + 4], float4 v, int tid) {
+  if (RC) {
+    const int i = tid >> 2, r = (tid & 3) * 4;
+    T[r + 0][i] = v.x; T[r + 1][i] = v.y; T[r + 2][i] = v.z; T[r + 3][i] = v.w;
+  } else {
+    *(float4*)&T[tid >> 4][(tid & 15) * 4] = v;
+  }
+}
+
+template <bool AR, bool BR, int OUT>
+__global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, const float* Bm,
+                                                       int ldb, const float* bias, void* out,
+                                                       int M, int N, int R, int HW, float scale) {
+  __shared__ float As[LK][LT + 4], Bs[LK][LT + 4];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.x * LT, n0 = blockIdx.y * LT;
+  float4 ra = tile_load<AR>(A, lda, m0, M, 0, R, tid), rb = tile_load<BR>(Bm, ldb, n0, N, 0, R, tid);
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int r0 = 0; r0 < R; r0 += LK) {
+    tile_store<AR>(As, ra, tid);
+    tile_store<BR>(Bs, rb, tid);
+    __syncthreads();
+    if (r0 + LK < R) {
+      ra = tile_load<AR>(A, lda, m0, M, r0 + LK, R, tid);
+      rb = tile_load<BR>(Bm, ldb, n0, N, r0 + LK, R, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < LK; ++kk) {
+      const float4 x = *(const float4*)&As[kk][ty * 4];
+      const float4 y = *(const float4*)&Bs[kk][tx * 4];
+      const float xa[4] = {x.x, x.y, x.z, x.w}, yb[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += xa[i] * yb[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+    if (OUT == 0) {
+      float* o = (float*)out;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + tx * 4 + j;
+        if (n < N) o[(size_t)m * N + n] = acc[i][j] + (bias ? bias[n] : 0.f);
+      }
+    } else {
+      bf16* o = (bf16*)out + (size_t)m * HW * N;
+      const int n = n0 + tx * 4;
+      if (n + 3 < N) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = f2bf(acc[i][j] * scale);
+        for (int hw = 0; hw < HW; ++hw) *(bf16x4*)(o + (size_t)hw * N + n) = v;
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (n + j < N)
+            for (int hw = 0; hw < HW; ++hw) o[(size_t)hw * N + n + j] = f2bf(acc[i][j] * scale);
+      }
+    }
+  }
+}
+
+// db[k] = sum_b dlogits[b][k]
+__global__ __launch_bounds__(NT) void head_db_kernel(const float* dlogits, float* db, int B, int K) {
+  const int k = blockIdx.x * NT + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dlogits[(size_t)b * K + k];
+  db[k] = s;
+}
+
 __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* pooled = sh;               // [C]
   float* logit = sh + a.C;          // [classes]
   float* red = logit + a.classes;   // [16]
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const bf16* x = a.act + (size_t)b * a.HW * a.C;
-  const float invhw = 1.f / (float)a.HW;
-  for (int c = tid; c < a.C; c += NT) {
-    float s = 0.f;
+  if (a.logits_ready) {
+    if (a.score_kind == 1)
+      for (int c = tid; c < a.C; c += NT) pooled[c] = a.pooled[(size_t)b * a.C + c];
+    for (int k = tid; k < a.classes; k += NT) logit[k] = a.logits[(size_t)b * a.classes + k];
+  } else {
+    const bf16* x = a.act + (size_t)b * a.HW * a.C;
+    const float invhw = 1.f / (float)a.HW;
+    for (int c = tid; c < a.C; c += NT) {
+      float s = 0.f;
 #pragma unroll 8
-    for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
-    s *= invhw;
-    pooled[c] = s;
-    if (a.pooled) a.pooled[(size_t)b * a.C + c] = s;
-  }
-  __syncthreads();
-  for (int k = wv; k < a.classes; k += NT / 64) {
-    const float* wr = a.w + (size_t)k * a.C;
-    float d = 0.f;
+      for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
+      s *= invhw;
+      pooled[c] = s;
+      if (a.pooled) a.pooled[(size_t)b * a.C + c] = s;
+    }
+    __syncthreads();
+    for (int k = wv; k < a.classes; k += NT / 64) {
+      const float* wr = a.w + (size_t)k * a.C;
+      float d = 0.f;
 #pragma unroll 8
-    for (int c = lane; c < a.C; c += 64) d += wr[c] * pooled[c];
-    d = wave_sum(d);
-    if (lane == 0) logit[k] = d + (a.b ? a.b[k] : 0.f);
+      for (int c = lane; c < a.C; c += 64) d += wr[c] * pooled[c];
+      d = wave_sum(d);
+      if (lane == 0) logit[k] = d + (a.b ? a.b[k] : 0.f);
+    }
   }
   __syncthreads();
   // log-sum-exp and argmax, one wave
@@ -138,12 +279,37 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadBwdArgs a) {
 }
 }  // namespace
 
-void head_fwd_launch(const HeadArgs& a, hipStream_t st) {
+void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
+  HeadArgs a = a0;
+  a.logits_ready = 0;
+  // wide heads: pool + fp32 tiled FC as their own launches (needs the pooled/logits workspaces)
+  if (a.pooled && a.logits && a.classes >= 64 && a.C % 16 == 0) {
+    hipLaunchKernelGGL(head_pool_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0, st,
+                       a.act, a.pooled, a.B, a.HW, a.C);
+    hipLaunchKernelGGL((head_gemm_kernel<true, true, 0>),
+                       dim3((a.B + LT - 1) / LT, (a.classes + LT - 1) / LT), dim3(NT), 0, st,
+                       a.pooled, a.C, a.w, a.C, a.b, (void*)a.logits, a.B, a.classes, a.C, 1, 1.f);
+    a.logits_ready = 1;
+  }
   const size_t shm = (size_t)(a.C + a.classes + 16) * sizeof(float);
   hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), shm, st, a);
 }
 
 void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
+  if (a.classes >= 64 && a.classes % 4 == 0 && a.C % 4 == 0) {
+    // wide head: dact = (dlogits . W) / HW broadcast over HW, dW = dlogits^T . pooled, db
+    hipLaunchKernelGGL((head_gemm_kernel<true, false, 1>),
+                       dim3((a.B + LT - 1) / LT, (a.C + LT - 1) / LT), dim3(NT), 0, st,
+                       a.dlogits, a.classes, a.w, a.C, (const float*)nullptr, (void*)a.dact, a.B,
+                       a.C, a.classes, a.HW, 1.f / (float)a.HW);
+    hipLaunchKernelGGL((head_gemm_kernel<false, false, 0>),
+                       dim3((a.classes + LT - 1) / LT, (a.C + LT - 1) / LT), dim3(NT), 0, st,
+                       a.dlogits, a.classes, a.pooled, a.C, (const float*)nullptr, (void*)a.dw,
+                       a.classes, a.C, a.B, 1, 1.f);
+    hipLaunchKernelGGL(head_db_kernel, dim3((a.classes + NT - 1) / NT), dim3(NT), 0, st,
+                       a.dlogits, a.db, a.B, a.classes);
+    return;
+  }
   hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + NT - 1) / NT, a.B + a.classes), dim3(NT), 0, st,
                      a);
 }

@@ -79,6 +79,7 @@ struct HeadArgs {
   int B, HW, C, classes, mode;   // mode 0 score, 1 train, 2 eval
   int log_softmax_input;         // logits are already log-probs (VGG) -> NLL
   int score_kind;                // losses[] holds 0: CE loss, 1: classifier-layer grad norm
+  int logits_ready;              // (set by head_fwd_launch) pooled/logits already computed
 };
 void head_fwd_launch(const HeadArgs& a, hipStream_t st);
 
@@ -219,8 +220,18 @@ void tern_unpack_launch(const uint32_t* msgs, int W, long long n, float scale, f
 struct PoolArgs {                 // max-pool / avg-pool NHWC bf16
   const bf16* x;
   bf16* y;
-  int* argmax;                   // [N*P*Q*C] (max) for backward, or null
+  uint8_t* argmax;               // [N*P*Q*C] window tap r*k+s of the max, for backward, or null
   int N, H, W, C, P, Q, k, stride, pad, is_max;
+  // optional BN (+ activation) of x applied per tap before pooling: x is then the raw conv
+  // output, normalised from ghost-group sums ``stats`` [G][2][C] (G = N / group_imgs) or from
+  // running statistics (rmean/rvar) -- the scoring pass's ImageNet stem, no bn_apply pass
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  const float* rmean;
+  const float* rvar;
+  int group_imgs, act;
+  float eps;
 };
 void pool2d_fwd_launch(const PoolArgs& a, hipStream_t st);
 void maxpool2d_bwd_launch(const PoolArgs& geom, const bf16* dy, bf16* dx, hipStream_t st);

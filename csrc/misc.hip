@@ -1,5 +1,7 @@
 // Remaining layer kernels: pooling (VGG / ImageNet stem), stochastic quantisation (`util.py:65-70`) and
 // NCHW fp32 -> NHWC bf16 layout conversion for host-fed tensors.
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -7,38 +9,71 @@ namespace {
 constexpr int NT = 256;
 
 // --------------------------------------------------------------- pooling
+// One thread per (output pixel, 8-channel chunk): 16-byte loads and stores, 32-bit index math
+// (a 64-bit div/mod is a ~100-instruction call; the ImageNet-stem pool at B=1280 was VALU-bound
+// on it).  The max pool records the window tap r*k+s of each maximum as one byte per channel
+// (first maximum in scan order, like torch), so the backward reads 8 taps as one 8-byte word.
+MA_DEV float pool_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
 __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
-  const int C8 = a.C >> 3;
-  const long long total = (long long)a.N * a.P * a.Q * C8;
-  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+  const unsigned C8 = (unsigned)a.C >> 3;
+  const unsigned total = (unsigned)a.N * a.P * a.Q * C8;
+  const unsigned i = blockIdx.x * NT + threadIdx.x;
   if (i >= total) return;
-  const int c8 = (int)(i % C8);
-  const long long pix = i / C8;
-  const int q = (int)(pix % a.Q), p = (int)((pix / a.Q) % a.P), n = (int)(pix / ((long long)a.P * a.Q));
+  const unsigned c8 = i % C8;
+  unsigned pix = i / C8;
+  const int q = (int)(pix % (unsigned)a.Q);
+  pix /= (unsigned)a.Q;
+  const int p = (int)(pix % (unsigned)a.P), n = (int)(pix / (unsigned)a.P);
+  const int c = (int)c8 * 8;
+  // BN of the input: per-channel scale/shift of this image's ghost group
+  float sc[8], sh[8];
+  const bool bn = a.stats != nullptr || a.rmean != nullptr;
+  if (bn) {
+    const bool run = a.stats == nullptr;
+    const int g = a.group_imgs > 0 ? n / a.group_imgs : 0;
+    const float inv = 1.f / (float)((a.group_imgs > 0 ? a.group_imgs : a.N) * a.H * a.W);
+    const float* s0 = run ? a.rmean + c : a.stats + (size_t)g * 2 * a.C + c;
+    const float* s1 = run ? a.rvar + c : s0 + a.C;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float mean = s0[k], var = s1[k];
+      if (!run) {
+        mean *= inv;
+        var = fmaxf(var * inv - mean * mean, 0.f);
+      }
+      sc[k] = a.gamma[c + k] * rsqrtf(var + a.eps);
+      sh[k] = a.beta[c + k] - mean * sc[k];
+    }
+  }
   float acc[8];
   int arg[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     acc[k] = a.is_max ? -3.4e38f : 0.f;
-    arg[k] = -1;
+    arg[k] = 0;
   }
-  int cnt = 0;
+  const bf16* xn = a.x + (size_t)n * a.H * a.W * a.C + c;
   for (int r = 0; r < a.k; ++r) {
     const int h = p * a.stride - a.pad + r;
     if (h < 0 || h >= a.H) continue;
     for (int s = 0; s < a.k; ++s) {
       const int w = q * a.stride - a.pad + s;
       if (w < 0 || w >= a.W) continue;
-      const size_t base = ((size_t)(n * a.H + h) * a.W + w) * a.C + c8 * 8;
-      const bf16x8 v = *(const bf16x8*)(a.x + base);
-      ++cnt;
+      const bf16x8 v = *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
+      const int tap = r * a.k + s;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float f = bf2f(v[k]);
+        float f = bf2f(v[k]);
+        if (bn) f = bf2f(f2bf(pool_act(f * sc[k] + sh[k], a.act)));   // = bn_apply's bf16 out
         if (a.is_max) {
           if (f > acc[k]) {
             acc[k] = f;
-            arg[k] = (int)(base + k);
+            arg[k] = tap;
           }
         } else {
           acc[k] += f;
@@ -49,30 +84,50 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
   bf16x8 o;
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = f2bf(a.is_max ? acc[k] : acc[k] / (float)(a.k * a.k));
-  *(bf16x8*)(a.y + i * 8) = o;
+  *(bf16x8*)(a.y + (size_t)i * 8) = o;
   if (a.argmax) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a.argmax[i * 8 + k] = arg[k];
+    uint2 t;
+    t.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) |
+          ((uint32_t)arg[3] << 24);
+    t.y = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) |
+          ((uint32_t)arg[7] << 24);
+    *(uint2*)(a.argmax + (size_t)i * 8) = t;
   }
 }
 
-// gather form: every input element sums the output gradients whose argmax it is
+// gather form, one thread per (input pixel, 8 channels): every input element sums the output
+// gradients of the windows whose recorded maximum is this element's tap
 __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(PoolArgs a, const bf16* dy, bf16* dx) {
-  const long long total = (long long)a.N * a.H * a.W * a.C;
-  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+  const unsigned C8 = (unsigned)a.C >> 3;
+  const unsigned total = (unsigned)a.N * a.H * a.W * C8;
+  const unsigned i = blockIdx.x * NT + threadIdx.x;
   if (i >= total) return;
-  const int c = (int)(i % a.C);
-  const long long pix = i / a.C;
-  const int w = (int)(pix % a.W), h = (int)((pix / a.W) % a.H), n = (int)(pix / ((long long)a.H * a.W));
-  float s = 0.f;
+  const unsigned c8 = i % C8;
+  unsigned pix = i / C8;
+  const int w = (int)(pix % (unsigned)a.W);
+  pix /= (unsigned)a.W;
+  const int h = (int)(pix % (unsigned)a.H), n = (int)(pix / (unsigned)a.H);
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
   const int p0 = max(0, (h + a.pad - a.k + a.stride) / a.stride), p1 = min(a.P - 1, (h + a.pad) / a.stride);
   const int q0 = max(0, (w + a.pad - a.k + a.stride) / a.stride), q1 = min(a.Q - 1, (w + a.pad) / a.stride);
   for (int p = p0; p <= p1; ++p)
     for (int q = q0; q <= q1; ++q) {
-      const size_t o = ((size_t)(n * a.P + p) * a.Q + q) * a.C + c;
-      if (a.argmax[o] == (int)i) s += bf2f(dy[o]);
+      const size_t o = ((size_t)(n * a.P + p) * a.Q + q) * a.C + c8 * 8;
+      const uint32_t tap = (uint32_t)((h - (p * a.stride - a.pad)) * a.k + (w - (q * a.stride - a.pad)));
+      const uint2 t = *(const uint2*)(a.argmax + o);
+      const bf16x8 g = *(const bf16x8*)(dy + o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t b = ((k < 4 ? t.x : t.y) >> (8 * (k & 3))) & 255u;
+        if (b == tap) s[k] += bf2f(g[k]);
+      }
     }
-  dx[i] = f2bf(s);
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = f2bf(s[k]);
+  *(bf16x8*)(dx + (size_t)i * 8) = o;
 }
 
 // --------------------------------------------------------------- quantisation
@@ -167,10 +222,16 @@ __global__ __launch_bounds__(NT) void nchw_to_nhwc8_kernel(const float* x, bf16*
 
 void pool2d_fwd_launch(const PoolArgs& a, hipStream_t st) {
   const long long total = (long long)a.N * a.P * a.Q * (a.C / 8);
+  if (a.C % 8 || (long long)a.N * a.H * a.W * a.C >= (1ll << 32) || total >= (1ll << 31)) {
+    throw std::runtime_error("pool2d_fwd: C % 8 or the 32-bit index range violated");
+  }
   hipLaunchKernelGGL(pool2d_fwd_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, a);
 }
 void maxpool2d_bwd_launch(const PoolArgs& a, const bf16* dy, bf16* dx, hipStream_t st) {
-  const long long total = (long long)a.N * a.H * a.W * a.C;
+  const long long total = (long long)a.N * a.H * a.W * (a.C / 8);
+  if (a.C % 8 || total >= (1ll << 31) || a.k * a.k > 255) {
+    throw std::runtime_error("maxpool2d_bwd: C % 8, the 32-bit index range or window size violated");
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, a,
                      dy, dx);
 }

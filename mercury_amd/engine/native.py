@@ -348,7 +348,7 @@ class NativeEngine(object):
                 m.buf[bi, 'out'] = act(N * P_ * Q_, K)
                 m.buf[bi, 'pool_geom'] = (N, h, w, K, P_, Q_, k, st, pd)
                 if train:
-                    m.buf[bi, 'argmax'] = torch.empty(N * P_ * Q_ * K, dtype=torch.int32,
+                    m.buf[bi, 'argmax'] = torch.empty(N * P_ * Q_ * K, dtype=torch.uint8,
                                                       device=dev)
                     m.buf[bi, 'dpre'] = m.buf[bi, 'dout']
                     m.buf[bi, 'dout'] = act(N * P_ * Q_, K)
@@ -366,6 +366,7 @@ class NativeEngine(object):
         m.final_hw = H * W
         m.final_C = C
         m.pooled = torch.zeros(N, C, device=dev)
+        m.logits = torch.zeros(N, self.classes, device=dev)   # wide heads' FC output
         m.losses = torch.zeros(N, device=dev)
         if train:
             m.dlogits = torch.zeros(N, self.classes, device=dev)
@@ -411,6 +412,14 @@ class NativeEngine(object):
                  keep=m.buf[u.name, 'a'] if m.train else None)
         if m.train or m.group_imgs:
             d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
+        else:
+            d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+        return d
+
+    def _pool_bn(self, m, u, act):
+        d = dict(gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS)
+        if m.group_imgs:
+            d.update(stats=m.stats[u.name], group_imgs=m.group_imgs)
         else:
             d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
         return d
@@ -473,6 +482,7 @@ class NativeEngine(object):
         stats_on = m.train or m.group_imgs
         pend = None          # the previous block's output, not yet materialised in x's buffer
         nblk = len(self.lw.blocks)
+        pool_bn = None       # BN + activation the block's max pool applies (scoring/eval stem)
         for bi, blk in enumerate(self.lw.blocks):
             inp = x
             nu = len(blk.units)
@@ -523,12 +533,21 @@ class NativeEngine(object):
                         pend = self._pending(u, y, blk.final_act,
                                              res=res if ru is None else None,
                                              unit2=ru, y2=res if ru is not None else None)
+                    elif (blk.pool and not m.train and res is None and
+                          blk.final_act in ('relu', 'relu6', 'none')):
+                        # scoring / eval (nothing reads the pre-pool activation): the pool
+                        # applies this BN + activation per tap, straight from the conv output
+                        pool_bn = self._pool_bn(m, u, blk.final_act)
                     else:
                         self._bn_apply(m, u, y, out, blk.final_act, res=res, res_unit=ru)
             if blk.pool:
                 N, h, w, K, P_, Q_, k, st, pd = m.buf[bi, 'pool_geom']
-                ops.pool2d_fwd(m.buf[bi, 'pre'], m.buf[bi, 'out'], N, h, w, K, P_, Q_, k, st, pd,
-                               True, m.buf.get((bi, 'argmax')))
+                src = m.buf[bi, 'pre']
+                if pool_bn is not None:
+                    src = m.buf[blk.units[-1].name, 'y']
+                ops.pool2d_fwd(src, m.buf[bi, 'out'], N, h, w, K, P_, Q_, k, st, pd,
+                               True, m.buf.get((bi, 'argmax')), bn=pool_bn)
+                pool_bn = None
             x = m.buf[bi, 'out']
         return x
 
@@ -602,6 +621,7 @@ class NativeEngine(object):
             return self._mlp_head(m, x, mode, isw=isw, meters=meters)
         ops.head_fwd(x, self._pview(self.lw.fc_w), self._pview(self.lw.fc_b), m.label, m.N,
                      m.final_hw, m.final_C, self.classes, mode, pooled=m.pooled,
+                     logits=m.logits,
                      dlogits=getattr(m, 'dlogits', None) if mode == 'train' else None,
                      losses=m.losses, isw=isw, meters=meters,
                      score=self.score if mode == 'score' else 'loss')

@@ -34,12 +34,28 @@ def tern_unpack(msgs, W, n, out, scale=None):
     return out
 
 
-def pool2d_fwd(x, y, N, H, W, C, P, Q, k, stride, pad, is_max=True, argmax=None):
+ACT = {'none': 0, 'relu': 1, 'relu6': 2}
+
+
+def pool2d_fwd(x, y, N, H, W, C, P, Q, k, stride, pad, is_max=True, argmax=None, bn=None):
+    """NHWC bf16 max/avg pool.  ``argmax`` (uint8, N*P*Q*C) records the window tap of each
+    maximum for ``maxpool2d_bwd``.  ``bn`` = dict(gamma, beta, act, eps and either stats
+    [G][2][C] + group_imgs, or rmean + rvar): ``x`` is the raw conv output and its BatchNorm +
+    activation are applied per tap (no separate bn_apply pass)."""
+    _chk(x, torch.bfloat16, 'x', N * H * W * C)
+    _chk(y, torch.bfloat16, 'y', N * P * Q * C)
+    if argmax is not None:
+        _chk(argmax, torch.uint8, 'argmax', N * P * Q * C)
+    bn = bn or {}
     lib().pool2d_fwd(ptr(x), ptr(y), ptr(argmax), N, H, W, C, P, Q, k, stride, pad, int(is_max),
-                     stream_ptr())
+                     stream_ptr(), ptr(bn.get('stats')), ptr(bn.get('gamma')),
+                     ptr(bn.get('beta')), ptr(bn.get('rmean')), ptr(bn.get('rvar')),
+                     int(bn.get('group_imgs', 0)), ACT[bn.get('act', 'none')],
+                     float(bn.get('eps', 1e-5)))
 
 
 def maxpool2d_bwd(dy, argmax, dx, N, H, W, C, P, Q, k, stride, pad):
+    _chk(argmax, torch.uint8, 'argmax', N * P * Q * C)
     lib().maxpool2d_bwd(ptr(dy), ptr(argmax), ptr(dx), N, H, W, C, P, Q, k, stride, pad,
                         stream_ptr())
 

@@ -637,7 +637,7 @@ def test_quantize_pool_dwconv():
         ref = F.max_pool2d(xx, k, st, pd)
         P, Q = ref.shape[2:]
         y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
-        am = torch.empty(N * P * Q * C, dtype=torch.int32, device=DEV)
+        am = torch.empty(N * P * Q * C, dtype=torch.uint8, device=DEV)
         ops.pool2d_fwd(ops.to_nhwc(xx.detach()), y, N, H, W, C, P, Q, k, st, pd, True, am)
         close(ops.from_nhwc(y), ref, 1e-3, 1e-3)
         gy = bf(torch.randn_like(ref))
@@ -825,3 +825,93 @@ def _halo_case(ops, case, plan, gimgs):
         r = rb[gi * (gimgs or N):(gi + 1) * (gimgs or N)]
         close(stats[gi, 0], r.sum((0, 2, 3)), rtol=1e-2, atol=0.5)
         close(stats[gi, 1], r.pow(2).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+
+
+def test_head_wide_gemm_path_matches_torch():
+    """ImageNet-width head (2048 -> 1000): pool kernel + fp32 tiled FC + loss kernel, B not a
+    multiple of the 64-row tile; train (IS-weighted, dlogits) and gradnorm score modes."""
+    ops = _ops()
+    from mercury_amd.importance.pool import classifier_gradnorm
+    B, HW, C, K = 70, 49, 2048, 1000
+    act = bf(torch.rand(B, HW, C, device=DEV))
+    w = torch.randn(K, C, device=DEV) * 0.02
+    b = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (B,), device=DEV)
+    isw = torch.rand(B, device=DEV) + 0.5
+    pooled = torch.empty(B, C, device=DEV)
+    logits = torch.empty(B, K, device=DEV)
+    dlog = torch.empty(B, K, device=DEV)
+    losses = torch.empty(B, device=DEV)
+    meters = torch.zeros(8, device=DEV)
+    ops.head_fwd(act.to(torch.bfloat16), w, b, lab.int(), B, HW, C, K, 'train', pooled=pooled,
+                 logits=logits, dlogits=dlog, losses=losses, isw=isw, meters=meters)
+    h = act.double().mean(1)
+    ref_logits = h @ w.double().t() + b.double()
+    close(pooled, h.float(), rtol=1e-5, atol=1e-6)
+    close(logits, ref_logits.float(), rtol=1e-4, atol=1e-4)
+    l = F.cross_entropy(ref_logits, lab, reduction='none')
+    close(losses, l.float(), rtol=1e-4, atol=1e-4)
+    p = torch.softmax(ref_logits, 1) - F.one_hot(lab, K).double()
+    close(dlog, (p / (B * isw.double()[:, None])).float(), rtol=1e-3, atol=1e-7)
+    assert meters[2].item() == (ref_logits.argmax(1) == lab).sum().item()
+    # backward through the wide-head GEMMs vs autograd of the same fp32 graph
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ar = act.clone().requires_grad_(True)
+    (F.cross_entropy(ar.mean(1) @ wr.t() + br, lab, reduction='none') / isw).mean().backward()
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    dact = torch.empty(B, HW, C, dtype=torch.bfloat16, device=DEV)
+    ops.head_bwd(pooled, dlog, w, dw, db, dact, B, HW, C, K)
+    close(dw, wr.grad, rtol=1e-3, atol=1e-7)
+    close(db, br.grad, rtol=1e-3, atol=1e-7)
+    close(dact, ar.grad, rtol=1e-2, atol=1e-8)
+    g = torch.empty(B, device=DEV)
+    ops.head_fwd(act.to(torch.bfloat16), w, b, lab.int(), B, HW, C, K, 'score', pooled=pooled,
+                 logits=logits, losses=g, score='gradnorm')
+    close(g, classifier_gradnorm(ref_logits.float(), lab, h.float()), rtol=1e-4, atol=1e-5)
+
+
+def test_pool_with_fused_bn_matches_bn_apply_then_pool():
+    """Stem max pool applying ghost-group BN + ReLU per tap == bn_apply pass + plain pool,
+    bit for bit (same bf16 rounding), from batch sums and from running statistics."""
+    ops = _ops()
+    N, H, W, C, G = 8, 14, 14, 64, 4
+    k, st, pd = 3, 2, 1
+    P = Q = (H + 2 * pd - k) // st + 1
+    y = bf(torch.randn(N, H, W, C, device=DEV)).to(torch.bfloat16).contiguous()
+    yf = y.float().view(G, -1, C)
+    stats = torch.stack([yf.sum(1), (yf * yf).sum(1)], 1).contiguous()      # [G][2][C]
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.2
+    rm, rv = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    for bn in (dict(stats=stats, group_imgs=N // G), dict(rmean=rm, rvar=rv)):
+        a = torch.empty_like(y)
+        if 'stats' in bn:
+            ops.bn_apply(y, stats, gamma, beta, a, N * H * W, C, group_rows=(N // G) * H * W,
+                         act='relu', eps=1e-5)
+        else:
+            ops.bn_apply(y, None, gamma, beta, a, N * H * W, C, group_rows=N * H * W,
+                         act='relu', eps=1e-5, running=(rm, rv))
+        ref = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
+        ops.pool2d_fwd(a, ref, N, H, W, C, P, Q, k, st, pd, True)
+        out = torch.empty_like(ref)
+        ops.pool2d_fwd(y, out, N, H, W, C, P, Q, k, st, pd, True,
+                       bn=dict(bn, gamma=gamma, beta=beta, act='relu', eps=1e-5))
+        assert torch.equal(out, ref)
+
+
+def test_maxpool_stem_shape_bwd_matches_torch():
+    """3x3/s2/p1 pool at an ImageNet-stem-like shape (byte argmax, 8-channel threads)."""
+    ops = _ops()
+    N, C, H, W = 4, 64, 56, 56
+    xx = bf(torch.randn(N, C, H, W, device=DEV)).requires_grad_(True)
+    ref = F.max_pool2d(xx, 3, 2, 1)
+    P, Q = ref.shape[2:]
+    y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=DEV)
+    am = torch.empty(N * P * Q * C, dtype=torch.uint8, device=DEV)
+    ops.pool2d_fwd(ops.to_nhwc(xx.detach()), y, N, H, W, C, P, Q, 3, 2, 1, True, am)
+    assert torch.equal(ops.from_nhwc(y).float(), bf(ref.detach()))
+    gy = bf(torch.randn_like(ref))
+    ref.backward(gy)
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    ops.maxpool2d_bwd(ops.to_nhwc(gy), am, dx, N, H, W, C, P, Q, 3, 2, 1)
+    close(ops.from_nhwc(dx), xx.grad, 1e-2, 1e-2)
