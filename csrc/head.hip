@@ -50,34 +50,48 @@ __global__ __launch_bounds__(NT) void head_pool_kernel(const bf16* act, float* p
 // ([r][m]).  Uses:  logits = pooled . W^T (AR, BR);  dpooled = dlogits . W (AR, !BR);
 // dW = dlogits^T . pooled (!AR, !BR).  OUT 0: fp32 C; 1: bf16 C * scale broadcast over HW
 // spatial rows (the activation gradient of the average pool).
-constexpr int LT = 64, LK = 16;
+constexpr int LT = 64, LK = 64;
+// one 64 (rows) x 64 (r) operand slice per block, 16 floats per thread.  RC: thread -> row tid/4,
+// r (tid%4)*16..+15;  else r tid/16 + 16j (j < 4), rows (tid%16)*4..+3.  A whole 64-deep slice
+// per barrier pair: the loop is latency-bound (one block per CU), so fewer, larger slices.
 template <bool RC>
-MA_DEV float4 tile_load(const float* p, int ld, int i0, int ni, int r0, int nr, int tid) {
-  // RC: rows i (64) x 16 r, thread -> row tid/4, r (tid%4)*4..+3;  else 16 r x 64 i, thread ->
-  // r tid/16, i (tid%16)*4..+3
-  float v[4];
-  const int i = RC ? i0 + (tid >> 2) : i0 + (tid & 15) * 4;
-  const int r = RC ? r0 + (tid & 3) * 4 : r0 + (tid >> 4);
-  if (RC) {
-    const float* q = p + (size_t)i * ld + r;
-    if (i < ni && r + 3 < nr) return *(const float4*)q;
+MA_DEV void tile_load(const float* p, int ld, int i0, int ni, int r0, int nr, int tid,
+                      float4 (&v)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (i < ni && r + j < nr) ? q[j] : 0.f;
-  } else {
-    const float* q = p + (size_t)r * ld + i;
-    if (r < nr && i + 3 < ni) return *(const float4*)q;
+  for (int j = 0; j < 4; ++j) {
+    const int i = RC ? i0 + (tid >> 2) : i0 + (tid & 15) * 4;
+    const int r = RC ? r0 + (tid & 3) * 16 + j * 4 : r0 + (tid >> 4) + 16 * j;
+    float e[4];
+    if (RC) {
+      const float* q = p + (size_t)(i < ni ? i : 0) * ld + r;
+      if (i < ni && r + 3 < nr) {
+        v[j] = *(const float4*)q;
+        continue;
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (r < nr && i + j < ni) ? q[j] : 0.f;
+      for (int t = 0; t < 4; ++t) e[t] = (i < ni && r + t < nr) ? q[t] : 0.f;
+    } else {
+      const float* q = p + (size_t)(r < nr ? r : 0) * ld + i;
+      if (r < nr && i + 3 < ni) {
+        v[j] = *(const float4*)q;
+        continue;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) e[t] = (r < nr && i + t < ni) ? q[t] : 0.f;
+    }
+    v[j] = make_float4(e[0], e[1], e[2], e[3]);
   }
-  return make_float4(v[0], v[1], v[2], v[3]);
 }
 template <bool RC>
-MA_DEV void tile_store(float (*T)[LT + 4], float4 v, int tid) {
-  if (RC) {
-    const int i = tid >> 2, r = (tid & 3) * 4;
-    T[r + 0][i] = v.x; T[r + 1][i] = v.y; T[r + 2][i] = v.z; T[r + 3][i] = v.w;
-  } else {
-    *(float4*)&T[tid >> 4][(tid & 15) * 4] = v;
+MA_DEV void tile_store(float (*T)[LT + 4], const float4 (&v)[4], int tid) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (RC) {
+      const int i = tid >> 2, r = (tid & 3) * 16 + j * 4;
+      T[r + 0][i] = v[j].x; T[r + 1][i] = v[j].y; T[r + 2][i] = v[j].z; T[r + 3][i] = v[j].w;
+    } else {
+      *(float4*)&T[(tid >> 4) + 16 * j][(tid & 15) * 4] = v[j];
+    }
   }
 }
 
@@ -88,7 +102,9 @@ __global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, 
   __shared__ float As[LK][LT + 4], Bs[LK][LT + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int m0 = blockIdx.x * LT, n0 = blockIdx.y * LT;
-  float4 ra = tile_load<AR>(A, lda, m0, M, 0, R, tid), rb = tile_load<BR>(Bm, ldb, n0, N, 0, R, tid);
+  float4 ra[4], rb[4];
+  tile_load<AR>(A, lda, m0, M, 0, R, tid, ra);
+  tile_load<BR>(Bm, ldb, n0, N, 0, R, tid, rb);
   float acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -99,8 +115,8 @@ __global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, 
     tile_store<BR>(Bs, rb, tid);
     __syncthreads();
     if (r0 + LK < R) {
-      ra = tile_load<AR>(A, lda, m0, M, r0 + LK, R, tid);
-      rb = tile_load<BR>(Bm, ldb, n0, N, r0 + LK, R, tid);
+      tile_load<AR>(A, lda, m0, M, r0 + LK, R, tid, ra);
+      tile_load<BR>(Bm, ldb, n0, N, r0 + LK, R, tid, rb);
     }
 #pragma unroll
     for (int kk = 0; kk < LK; ++kk) {
@@ -142,11 +158,16 @@ __global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, 
   }
 }
 
+// FC sizes from which the GEMM path wins (ImageNet 1000 x 2048 does; the CIFAR-100 MobileNetV2
+// head, 100 x 1280, is faster on the per-sample path: too few 64x64 tiles to fill the GPU)
+constexpr long long WIDE = 1ll << 20;
+
 // db[k] = sum_b dlogits[b][k]
 __global__ __launch_bounds__(NT) void head_db_kernel(const float* dlogits, float* db, int B, int K) {
   const int k = blockIdx.x * NT + threadIdx.x;
   if (k >= K) return;
   float s = 0.f;
+#pragma unroll 16
   for (int b = 0; b < B; ++b) s += dlogits[(size_t)b * K + k];
   db[k] = s;
 }
@@ -283,7 +304,7 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
   HeadArgs a = a0;
   a.logits_ready = 0;
   // wide heads: pool + fp32 tiled FC as their own launches (needs the pooled/logits workspaces)
-  if (a.pooled && a.logits && a.classes >= 64 && a.C % 16 == 0) {
+  if (a.pooled && a.logits && (long long)a.classes * a.C >= WIDE && a.C % 16 == 0) {
     hipLaunchKernelGGL(head_pool_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0, st,
                        a.act, a.pooled, a.B, a.HW, a.C);
     hipLaunchKernelGGL((head_gemm_kernel<true, true, 0>),
@@ -296,7 +317,7 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
 }
 
 void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
-  if (a.classes >= 64 && a.classes % 4 == 0 && a.C % 4 == 0) {
+  if ((long long)a.classes * a.C >= WIDE && a.classes % 4 == 0 && a.C % 4 == 0) {
     // wide head: dact = (dlogits . W) / HW broadcast over HW, dW = dlogits^T . pooled, db
     hipLaunchKernelGGL((head_gemm_kernel<true, false, 1>),
                        dim3((a.B + LT - 1) / LT, (a.C + LT - 1) / LT), dim3(NT), 0, st,

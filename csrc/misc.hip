@@ -13,12 +13,21 @@ constexpr int NT = 256;
 // (a 64-bit div/mod is a ~100-instruction call; the ImageNet-stem pool at B=1280 was VALU-bound
 // on it).  The max pool records the window tap r*k+s of each maximum as one byte per channel
 // (first maximum in scan order, like torch), so the backward reads 8 taps as one 8-byte word.
+MA_DEV void ld8(const float* p, float (&v)[8]) {     // 8 floats as two 16-byte loads
+  const float4 x = *(const float4*)p, y = *(const float4*)(p + 4);
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
 MA_DEV float pool_act(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
   if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
   return v;
 }
 
+// KS > 0: the window size is a compile-time constant and all KS*KS tap loads are issued
+// before the first is used (out-of-image taps load a clamped in-image pixel and are masked);
+// KS == 0: runtime window, one tap at a time.
+template <int KS>
 __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
   const unsigned C8 = (unsigned)a.C >> 3;
   const unsigned total = (unsigned)a.N * a.P * a.Q * C8;
@@ -30,6 +39,19 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
   pix /= (unsigned)a.Q;
   const int p = (int)(pix % (unsigned)a.P), n = (int)(pix / (unsigned)a.P);
   const int c = (int)c8 * 8;
+  const int k = KS > 0 ? KS : a.k;
+  const int h0 = p * a.stride - a.pad, w0 = q * a.stride - a.pad;
+  const bf16* xn = a.x + (size_t)n * a.H * a.W * a.C + c;
+  constexpr int NV = KS > 0 ? KS * KS : 1;
+  bf16x8 v[NV];
+  if (KS > 0) {
+#pragma unroll
+    for (int t = 0; t < NV; ++t) {
+      const int h = min(max(h0 + t / (KS > 0 ? KS : 1), 0), a.H - 1);
+      const int w = min(max(w0 + t % (KS > 0 ? KS : 1), 0), a.W - 1);
+      v[t] = *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
+    }
+  }
   // BN of the input: per-channel scale/shift of this image's ghost group
   float sc[8], sh[8];
   const bool bn = a.stats != nullptr || a.rmean != nullptr;
@@ -39,51 +61,53 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
     const float inv = 1.f / (float)((a.group_imgs > 0 ? a.group_imgs : a.N) * a.H * a.W);
     const float* s0 = run ? a.rmean + c : a.stats + (size_t)g * 2 * a.C + c;
     const float* s1 = run ? a.rvar + c : s0 + a.C;
+    float m8[8], v8[8], g8[8], b8[8];
+    ld8(s0, m8);
+    ld8(s1, v8);
+    ld8(a.gamma + c, g8);
+    ld8(a.beta + c, b8);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float mean = s0[k], var = s1[k];
+    for (int j = 0; j < 8; ++j) {
+      float mean = m8[j], var = v8[j];
       if (!run) {
         mean *= inv;
         var = fmaxf(var * inv - mean * mean, 0.f);
       }
-      sc[k] = a.gamma[c + k] * rsqrtf(var + a.eps);
-      sh[k] = a.beta[c + k] - mean * sc[k];
+      sc[j] = g8[j] * rsqrtf(var + a.eps);
+      sh[j] = b8[j] - mean * sc[j];
     }
   }
   float acc[8];
   int arg[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    acc[k] = a.is_max ? -3.4e38f : 0.f;
-    arg[k] = 0;
+  for (int j = 0; j < 8; ++j) {
+    acc[j] = a.is_max ? -3.4e38f : 0.f;
+    arg[j] = 0;
   }
-  const bf16* xn = a.x + (size_t)n * a.H * a.W * a.C + c;
-  for (int r = 0; r < a.k; ++r) {
-    const int h = p * a.stride - a.pad + r;
-    if (h < 0 || h >= a.H) continue;
-    for (int s = 0; s < a.k; ++s) {
-      const int w = q * a.stride - a.pad + s;
-      if (w < 0 || w >= a.W) continue;
-      const bf16x8 v = *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
-      const int tap = r * a.k + s;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float f = bf2f(v[k]);
-        if (bn) f = bf2f(f2bf(pool_act(f * sc[k] + sh[k], a.act)));   // = bn_apply's bf16 out
+  for (int t = 0; t < (KS > 0 ? NV : 1); ++t) {
+    for (int tt = (KS > 0 ? t : 0); tt < (KS > 0 ? t + 1 : k * k); ++tt) {
+      const int h = h0 + tt / k, w = w0 + tt % k;
+      if (h < 0 || h >= a.H || w < 0 || w >= a.W) continue;
+      const bf16x8 x = KS > 0 ? v[t] : *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = bf2f(x[j]);
+        if (bn) f = bf2f(f2bf(pool_act(f * sc[j] + sh[j], a.act)));   // = bn_apply's bf16 out
         if (a.is_max) {
-          if (f > acc[k]) {
-            acc[k] = f;
-            arg[k] = tap;
+          if (f > acc[j]) {
+            acc[j] = f;
+            arg[j] = tt;
           }
         } else {
-          acc[k] += f;
+          acc[j] += f;
         }
       }
     }
   }
   bf16x8 o;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = f2bf(a.is_max ? acc[k] : acc[k] / (float)(a.k * a.k));
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(a.is_max ? acc[j] : acc[j] / (float)(k * k));
   *(bf16x8*)(a.y + (size_t)i * 8) = o;
   if (a.argmax) {
     uint2 t;
@@ -225,7 +249,13 @@ void pool2d_fwd_launch(const PoolArgs& a, hipStream_t st) {
   if (a.C % 8 || (long long)a.N * a.H * a.W * a.C >= (1ll << 32) || total >= (1ll << 31)) {
     throw std::runtime_error("pool2d_fwd: C % 8 or the 32-bit index range violated");
   }
-  hipLaunchKernelGGL(pool2d_fwd_kernel, dim3((unsigned)((total + NT - 1) / NT)), dim3(NT), 0, st, a);
+  const dim3 grid((unsigned)((total + NT - 1) / NT));
+  if (a.k == 3)
+    hipLaunchKernelGGL(pool2d_fwd_kernel<3>, grid, dim3(NT), 0, st, a);
+  else if (a.k == 2)
+    hipLaunchKernelGGL(pool2d_fwd_kernel<2>, grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL(pool2d_fwd_kernel<0>, grid, dim3(NT), 0, st, a);
 }
 void maxpool2d_bwd_launch(const PoolArgs& a, const bf16* dy, bf16* dx, hipStream_t st) {
   const long long total = (long long)a.N * a.H * a.W * (a.C / 8);
