@@ -318,8 +318,11 @@ void bn_apply_launch(const BnApplyArgs& a, hipStream_t st) {
 void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
   // a.sums must be zero on entry (the engine zeroes one arena per step)
   const size_t chunks = (size_t)a.M * (a.C / 8);
+  // 4 chunks per thread (one trip): measured at the MobileNetV2 train-batch shapes 4 / 8 / 16 /
+  // 32 / 64 chunks -> 179 / 186 / 218 / 295 / 453 us over the net (bench/small_bwd_bench.py):
+  // the loop is latency-bound, not bound by the blocks' final atomics
   if (a.phases & 1)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 8, 256)), dim3(NT), 0,
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 4, 256)), dim3(NT), 0,
                        st, a);
   if (a.phases & 2)
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0,

@@ -216,24 +216,29 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
   }
 }
 
+// One thread per (image, output row, 8 channels) walks the row's columns with the 3x3 input
+// window in registers, the next column's loads issued before the current column's FMAs.  The
+// block then reduces its threads' 9x8 partial sums through LDS -- each thread's partials in
+// its own padded LDS row, summed per (tap, channel) over the threads of that channel chunk --
+// and adds 9C values into dw: no LDS atomics (the per-thread LDS atomic adds serialised on
+// the ~256/C8 threads sharing a channel).
+constexpr int WG_LD = 73;   // floats per thread row (odd: conflict-free row writes)
 template <int S>
 __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
                                                       int H, int W, int C, int P, int Q, int pad) {
-  extern __shared__ float red[];  // [9][C]
+  extern __shared__ float part[];  // [DT][WG_LD]
   const int C8 = C >> 3;
   const int total = N * P * C8;
   const int gt = blockIdx.x * DT + threadIdx.x;
-  for (int i = threadIdx.x; i < 9 * C; i += DT) red[i] = 0.f;
-  __syncthreads();
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
   if (gt < total) {
     const int c8 = gt % C8;
     const int r = gt / C8;
     const int p = r % P, n = r / P;
-    float acc[9][8];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
     const bf16* rows[3];
     bool rok[3];
 #pragma unroll
@@ -252,41 +257,53 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
         win[rr][t] = ld8(rows[rr] + (size_t)ww * C, rok[rr] && ww >= 0 && ww < W);
       }
     const bf16* grow = dy + (size_t)(n * P + p) * Q * C + c8 * 8;
+    bf16x8 g = *(const bf16x8*)grow;
     for (int q = 0; q < Q; ++q) {
-      if (q > 0) {
-        const int base = q * S - pad;
+      // column q+1's loads first
+      bf16x8 n1[3], n2[3], ng = g;
+      const int base = (q + 1) * S - pad;
+      const bool more = q + 1 < Q;
 #pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-          if (S == 1) {
-            win[rr][0] = win[rr][1];
-            win[rr][1] = win[rr][2];
-          } else {
-            win[rr][0] = win[rr][2];
-            win[rr][1] = ld8(rows[rr] + (size_t)(base + 1) * C, rok[rr] && base + 1 >= 0 && base + 1 < W);
-          }
-          win[rr][2] = ld8(rows[rr] + (size_t)(base + 2) * C, rok[rr] && base + 2 >= 0 && base + 2 < W);
-        }
+      for (int rr = 0; rr < 3; ++rr) {
+        if (S == 2) n1[rr] = ld8(rows[rr] + (size_t)(base + 1) * C, more && rok[rr] && base + 1 >= 0 && base + 1 < W);
+        n2[rr] = ld8(rows[rr] + (size_t)(base + 2) * C, more && rok[rr] && base + 2 >= 0 && base + 2 < W);
       }
-      const bf16x8 g = *(const bf16x8*)(grow + (size_t)q * C);
+      if (more) ng = *(const bf16x8*)(grow + (size_t)(q + 1) * C);
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
         for (int t = 0; t < 3; ++t)
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc[rr * 3 + t][k] += bf2f(g[k]) * bf2f(win[rr][t][k]);
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        if (S == 1) {
+          win[rr][0] = win[rr][1];
+          win[rr][1] = win[rr][2];
+        } else {
+          win[rr][0] = win[rr][2];
+          win[rr][1] = n1[rr];
+        }
+        win[rr][2] = n2[rr];
+      }
+      g = ng;
     }
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(&red[t * C + c8 * 8 + k], acc[t][k]);
   }
+  float* mine = part + threadIdx.x * WG_LD;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mine[t * 8 + k] = acc[t][k];
   __syncthreads();
+  // output (tap t, channel c): the threads of chunk c/8 are j0, j0 + C8, ... (gt = base + j)
+  const int nthr = min(DT, total - (int)blockIdx.x * DT);
+  const int off = (int)(((long long)blockIdx.x * DT) % C8);
   for (int i = threadIdx.x; i < 9 * C; i += DT) {
-    const float v = red[i];
-    if (v != 0.f) {
-      const int t = i / C, c = i - t * C;
-      atomicAdd(&dw[c * 9 + t], v);
-    }
+    const int c = i % C, t = i / C;
+    const int j0 = ((c >> 3) - off + C8) % C8;
+    float v = 0.f;
+    for (int j = j0; j < nthr; j += C8) v += part[j * WG_LD + t * 8 + (c & 7)];
+    if (v != 0.f) atomicAdd(&dw[c * 9 + t], v);
   }
 }
 }  // namespace
@@ -314,7 +331,15 @@ void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H,
                          int Q, int stride, int pad, hipStream_t st) {
   const long long total = (long long)N * P * (C / 8);
   const dim3 grid((unsigned)((total + DT - 1) / DT));
-  const size_t shm = 9 * (size_t)C * sizeof(float);
+  const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // 73 KB: above the 64 KB default
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)dw_wgrad_kernel<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)dw_wgrad_kernel<2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
   if (stride == 1)
     hipLaunchKernelGGL(dw_wgrad_kernel<1>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad);
   else
