@@ -51,9 +51,10 @@ MA_DEV bf16x8 ld8(const bf16* p, bool ok) {
   return v;
 }
 
+constexpr int ST_LD = 17;   // floats per thread row of the forward's BN partials (odd stride)
 template <int S>
 __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
-  extern __shared__ float red[];  // [2][C] block partial BN sums
+  extern __shared__ float part[];  // [DT][ST_LD] per-thread BN partial sums (sum, sumsq)
   const int C8 = a.C >> 3, QS = (a.Q + DWL - 1) / DWL;
   const int per_img = a.P * QS * C8;
   const int total = a.N * per_img;
@@ -62,10 +63,9 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
   const int gfirst = (g0 / per_img) / imgs_per_group;
   const int glast = (min(total - 1, g0 + DT - 1) / per_img) / imgs_per_group;
   const bool lds_stats = a.stats && gfirst == glast;
-  if (lds_stats) {
-    for (int i = threadIdx.x; i < 2 * a.C; i += DT) red[i] = 0.f;
-    __syncthreads();
-  }
+  float s[8], ss[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = ss[k] = 0.f;
   if (gt < total) {
     const int c8 = gt % C8;
     int r = gt / C8;
@@ -100,9 +100,6 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
             for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o * S + t][k]) * wr[rr * 3 + t][k];
       }
     }
-    float s[8], ss[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s[k] = ss[k] = 0.f;
     bf16* yrow = a.y + (size_t)(n * a.P + p) * a.Q * a.C + c8 * 8;
 #pragma unroll
     for (int o = 0; o < DWL; ++o) {
@@ -118,28 +115,34 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
         *(bf16x8*)(yrow + (size_t)(q0 + o) * a.C) = v;
       }
     }
-    if (a.stats) {
-      if (lds_stats) {
+    if (a.stats && !lds_stats) {  // block straddles two BN groups (tiny images): global atomics
+      float* dst = a.stats + (size_t)(n / imgs_per_group) * 2 * a.C;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          atomicAdd(&red[c8 * 8 + k], s[k]);
-          atomicAdd(&red[a.C + c8 * 8 + k], ss[k]);
-        }
-      } else {  // block straddles two BN groups (tiny images): direct global atomics
-        float* dst = a.stats + (size_t)(n / imgs_per_group) * 2 * a.C;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          atomicAdd(dst + c8 * 8 + k, s[k]);
-          atomicAdd(dst + a.C + c8 * 8 + k, ss[k]);
-        }
+      for (int k = 0; k < 8; ++k) {
+        atomicAdd(dst + c8 * 8 + k, s[k]);
+        atomicAdd(dst + a.C + c8 * 8 + k, ss[k]);
       }
     }
   }
   if (lds_stats) {
+    // block reduction without LDS atomics: each thread's sums in its own padded LDS row, then
+    // per channel over the threads of that channel's chunk (j0, j0 + C8, ...; gt = g0 + j)
+    float* mine = part + threadIdx.x * ST_LD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mine[k] = s[k];
+      mine[8 + k] = ss[k];
+    }
     __syncthreads();
+    const int nthr = min(DT, total - g0), off = g0 % C8;
     float* dst = a.stats + (size_t)gfirst * 2 * a.C;
     for (int c = threadIdx.x; c < a.C; c += DT) {
-      const float v0 = red[c], v1 = red[a.C + c];
+      const int j0 = ((c >> 3) - off + C8) % C8;
+      float v0 = 0.f, v1 = 0.f;
+      for (int j = j0; j < nthr; j += C8) {
+        v0 += part[j * ST_LD + (c & 7)];
+        v1 += part[j * ST_LD + 8 + (c & 7)];
+      }
       if (v1 != 0.f) {  // sumsq == 0 <=> no (non-zero) output of this channel in the block
         atomicAdd(dst + c, v0);
         atomicAdd(dst + a.C + c, v1);
@@ -312,7 +315,7 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const int QS = (a.Q + DWL - 1) / DWL;
   const long long total = (long long)a.N * a.P * QS * (a.C / 8);
   const dim3 grid((unsigned)((total + DT - 1) / DT));
-  const size_t shm = a.stats ? 2 * (size_t)a.C * sizeof(float) : 0;
+  const size_t shm = a.stats ? (size_t)DT * ST_LD * sizeof(float) : 0;
   if (a.stride == 1)
     hipLaunchKernelGGL(dw_fwd_kernel<1>, grid, dim3(DT), shm, st, a);
   else
