@@ -26,8 +26,12 @@ MA_DEV float pool_act(float v, int act) {
 
 // KS > 0: the window size is a compile-time constant and all KS*KS tap loads are issued
 // before the first is used (out-of-image taps load a clamped in-image pixel and are masked);
-// KS == 0: runtime window, one tap at a time.
-template <int KS>
+// KS == 0: runtime window, one tap at a time.  MODE: 0 max, 1 max + argmax, 2 max of
+// act(BN(x)), 3 average.  MODE 2 keeps the max AND the min of the raw values and transforms
+// once: act(sc*x + sh) and its bf16 rounding are monotone in x -- non-decreasing for sc >= 0
+// (take the max), non-increasing for sc < 0 (take the min) -- so the result equals the max of
+// bn_apply's bf16 outputs, at a ninth of the transform work (the kernel was VALU-bound).
+template <int KS, int MODE>
 __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
   const unsigned C8 = (unsigned)a.C >> 3;
   const unsigned total = (unsigned)a.N * a.P * a.Q * C8;
@@ -52,10 +56,39 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
       v[t] = *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
     }
   }
-  // BN of the input: per-channel scale/shift of this image's ghost group
-  float sc[8], sh[8];
-  const bool bn = a.stats != nullptr || a.rmean != nullptr;
-  if (bn) {
+  float acc[8], mn[8];
+  int arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    acc[j] = MODE == 3 ? 0.f : -3.4e38f;
+    mn[j] = 3.4e38f;
+    arg[j] = 0;
+  }
+#pragma unroll
+  for (int t = 0; t < (KS > 0 ? NV : 1); ++t) {
+    for (int tt = (KS > 0 ? t : 0); tt < (KS > 0 ? t + 1 : k * k); ++tt) {
+      const int h = h0 + tt / k, w = w0 + tt % k;
+      if (h < 0 || h >= a.H || w < 0 || w >= a.W) continue;
+      const bf16x8 x = KS > 0 ? v[t] : *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(x[j]);
+        if (MODE == 3) {
+          acc[j] += f;
+        } else if (MODE == 1) {
+          if (f > acc[j]) {
+            acc[j] = f;
+            arg[j] = tt;
+          }
+        } else {
+          acc[j] = fmaxf(acc[j], f);
+          if (MODE == 2) mn[j] = fminf(mn[j], f);
+        }
+      }
+    }
+  }
+  if (MODE == 2) {
+    // BN of the input: per-channel scale/shift of this image's ghost group
     const bool run = a.stats == nullptr;
     const int g = a.group_imgs > 0 ? n / a.group_imgs : 0;
     const float inv = 1.f / (float)((a.group_imgs > 0 ? a.group_imgs : a.N) * a.H * a.W);
@@ -73,43 +106,16 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
         mean *= inv;
         var = fmaxf(var * inv - mean * mean, 0.f);
       }
-      sc[j] = g8[j] * rsqrtf(var + a.eps);
-      sh[j] = b8[j] - mean * sc[j];
-    }
-  }
-  float acc[8];
-  int arg[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    acc[j] = a.is_max ? -3.4e38f : 0.f;
-    arg[j] = 0;
-  }
-#pragma unroll
-  for (int t = 0; t < (KS > 0 ? NV : 1); ++t) {
-    for (int tt = (KS > 0 ? t : 0); tt < (KS > 0 ? t + 1 : k * k); ++tt) {
-      const int h = h0 + tt / k, w = w0 + tt % k;
-      if (h < 0 || h >= a.H || w < 0 || w >= a.W) continue;
-      const bf16x8 x = KS > 0 ? v[t] : *(const bf16x8*)(xn + (unsigned)(h * a.W + w) * (unsigned)a.C);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float f = bf2f(x[j]);
-        if (bn) f = bf2f(f2bf(pool_act(f * sc[j] + sh[j], a.act)));   // = bn_apply's bf16 out
-        if (a.is_max) {
-          if (f > acc[j]) {
-            acc[j] = f;
-            arg[j] = tt;
-          }
-        } else {
-          acc[j] += f;
-        }
-      }
+      const float sc = g8[j] * rsqrtf(var + a.eps);
+      const float sh = b8[j] - mean * sc;
+      acc[j] = pool_act((sc >= 0.f ? acc[j] : mn[j]) * sc + sh, a.act);
     }
   }
   bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = f2bf(a.is_max ? acc[j] : acc[j] / (float)(k * k));
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(MODE == 3 ? acc[j] / (float)(k * k) : acc[j]);
   *(bf16x8*)(a.y + (size_t)i * 8) = o;
-  if (a.argmax) {
+  if (MODE == 1) {
     uint2 t;
     t.x = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) |
           ((uint32_t)arg[3] << 24);
@@ -117,6 +123,16 @@ __global__ __launch_bounds__(NT) void pool2d_fwd_kernel(PoolArgs a) {
           ((uint32_t)arg[7] << 24);
     *(uint2*)(a.argmax + (size_t)i * 8) = t;
   }
+}
+
+template <int MODE>
+void pool2d_fwd_mode(const PoolArgs& a, dim3 grid, hipStream_t st) {
+  if (a.k == 3)
+    hipLaunchKernelGGL((pool2d_fwd_kernel<3, MODE>), grid, dim3(NT), 0, st, a);
+  else if (a.k == 2)
+    hipLaunchKernelGGL((pool2d_fwd_kernel<2, MODE>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((pool2d_fwd_kernel<0, MODE>), grid, dim3(NT), 0, st, a);
 }
 
 // gather form, one thread per (input pixel, 8 channels): every input element sums the output
@@ -250,12 +266,19 @@ void pool2d_fwd_launch(const PoolArgs& a, hipStream_t st) {
     throw std::runtime_error("pool2d_fwd: C % 8 or the 32-bit index range violated");
   }
   const dim3 grid((unsigned)((total + NT - 1) / NT));
-  if (a.k == 3)
-    hipLaunchKernelGGL(pool2d_fwd_kernel<3>, grid, dim3(NT), 0, st, a);
-  else if (a.k == 2)
-    hipLaunchKernelGGL(pool2d_fwd_kernel<2>, grid, dim3(NT), 0, st, a);
+  const bool bn = a.stats != nullptr || a.rmean != nullptr;
+  if (!a.is_max && (bn || a.argmax))
+    throw std::runtime_error("pool2d_fwd: BN / argmax only with the max pool");
+  if (bn && a.argmax)
+    throw std::runtime_error("pool2d_fwd: the BN-applying pool records no argmax");
+  if (!a.is_max)
+    pool2d_fwd_mode<3>(a, grid, st);
+  else if (bn)
+    pool2d_fwd_mode<2>(a, grid, st);
+  else if (a.argmax)
+    pool2d_fwd_mode<1>(a, grid, st);
   else
-    hipLaunchKernelGGL(pool2d_fwd_kernel<0>, grid, dim3(NT), 0, st, a);
+    pool2d_fwd_mode<0>(a, grid, st);
 }
 void maxpool2d_bwd_launch(const PoolArgs& a, const bf16* dy, bf16* dx, hipStream_t st) {
   const long long total = (long long)a.N * a.H * a.W * (a.C / 8);

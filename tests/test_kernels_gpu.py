@@ -871,8 +871,9 @@ def test_head_wide_gemm_path_matches_torch():
 
 
 def test_pool_with_fused_bn_matches_bn_apply_then_pool():
-    """Stem max pool applying ghost-group BN + ReLU per tap == bn_apply pass + plain pool,
-    bit for bit (same bf16 rounding), from batch sums and from running statistics."""
+    """Stem max pool applying ghost-group BN + ReLU == bn_apply pass + plain pool, bit for bit
+    (same bf16 rounding), from batch sums and from running statistics, negative BN scales
+    included (the kernel pools the raw max / min and transforms once)."""
     ops = _ops()
     N, H, W, C, G = 8, 14, 14, 64, 4
     k, st, pd = 3, 2, 1
@@ -880,7 +881,8 @@ def test_pool_with_fused_bn_matches_bn_apply_then_pool():
     y = bf(torch.randn(N, H, W, C, device=DEV)).to(torch.bfloat16).contiguous()
     yf = y.float().view(G, -1, C)
     stats = torch.stack([yf.sum(1), (yf * yf).sum(1)], 1).contiguous()      # [G][2][C]
-    gamma = torch.rand(C, device=DEV) + 0.5
+    gamma = torch.randn(C, device=DEV)            # negative scales take the min branch
+    gamma[:8] = -gamma[:8].abs() - 0.1
     beta = torch.randn(C, device=DEV) * 0.2
     rm, rv = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
     for bn in (dict(stats=stats, group_imgs=N // G), dict(rmean=rm, rvar=rv)):
