@@ -18,6 +18,8 @@
 // row stride is a multiple of C/8), so its per-channel constants are loaded once,
 // as 2 x float4 per array, all issued back to back -- never as conditional scalar
 // loads, which hipcc serialises behind one vmcnt(0) each (a ~15 us prologue).
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -78,7 +80,10 @@ MA_DEV void mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, flo
   }
 }
 
-// grid.x covers the rows of ONE stat group (grid.y = group), stride multiple of C/8
+// grid.x covers the rows of ONE stat group (grid.y = group), stride multiple of C/8.
+// ACT / RES are compile-time (activation 0-2, residual mode 0-2): with runtime values the
+// per-element code evaluated every activation and residual form and selected.
+template <int ACT, int RES>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
   const int C8 = a.C >> 3;
   const int T = gridDim.x * NT;
@@ -99,7 +104,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
     for (int u = 0; u < U; ++u) {
       const size_t off = (size_t)min(rb + u * rpi, row1 - 1) * a.C + c;
       y[u] = *(const bf16x8*)(a.y + off);
-      if (a.res_mode) r[u] = *(const bf16x8*)(a.res + off);
+      if (RES) r[u] = *(const bf16x8*)(a.res + off);
     }
   };
   int row = row0 + i0 / C8;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
     const float* s1 = run ? a.rvar + c : s0 + a.C;
     scale_shift8(s0, s1, run, inv, a.eps, a.gamma + c, a.beta + c, sc, sh);
   }
-  if (a.res_mode == 2) {
+  if (RES == 2) {
     const float* s0 = run ? a.rmean2 + c : a.stats2 + (size_t)g * 2 * a.C + c;
     const float* s1 = run ? a.rvar2 + c : s0 + a.C;
     scale_shift8(s0, s1, run, inv, a.eps, a.gamma2 + c, a.beta2 + c, sc2, sh2);
@@ -125,9 +130,9 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float v = bf2f(y[u][k]) * sc[k] + sh[k];
-        if (a.res_mode == 1) v += bf2f(r[u][k]);
-        else if (a.res_mode == 2) v += bf2f(r[u][k]) * sc2[k] + sh2[k];
-        o[k] = f2bf(act_fwd(v, a.act));
+        if (RES == 1) v += bf2f(r[u][k]);
+        else if (RES == 2) v += bf2f(r[u][k]) * sc2[k] + sh2[k];
+        o[k] = f2bf(act_fwd(v, ACT));
       }
       *(bf16x8*)(a.out + (size_t)(row + u * rpi) * a.C + c) = o;
     }
@@ -312,7 +317,17 @@ void bn_apply_launch(const BnApplyArgs& a, hipStream_t st) {
   const int G = (a.M + a.group_rows - 1) / a.group_rows;
   const size_t chunks = (size_t)a.group_rows * (a.C / 8);
   const int gx = grid_for(chunks, a.C / 8, 4, (2048 + G - 1) / G);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(gx, G), dim3(NT), 0, st, a);
+  const dim3 grid(gx, G);
+#define BN_APPLY_CASE(A, R)                                                   \
+  if (a.act == A && a.res_mode == R) {                                        \
+    hipLaunchKernelGGL((bn_apply_kernel<A, R>), grid, dim3(NT), 0, st, a);    \
+    return;                                                                   \
+  }
+  BN_APPLY_CASE(0, 0) BN_APPLY_CASE(0, 1) BN_APPLY_CASE(0, 2)
+  BN_APPLY_CASE(1, 0) BN_APPLY_CASE(1, 1) BN_APPLY_CASE(1, 2)
+  BN_APPLY_CASE(2, 0) BN_APPLY_CASE(2, 1) BN_APPLY_CASE(2, 2)
+#undef BN_APPLY_CASE
+  throw std::runtime_error("bn_apply: act must be 0-2 and res_mode 0-2");
 }
 
 void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
