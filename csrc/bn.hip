@@ -140,10 +140,11 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
   }
 }
 
+template <int ACT, bool TWO>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   __shared__ float red[3 * 2048];
   const int C8 = a.C >> 3;
-  const bool two = a.y2 != nullptr;
+  constexpr bool two = TWO;
   for (int i = threadIdx.x; i < 3 * a.C; i += NT) red[i] = 0.f;
   __syncthreads();
   const int T = gridDim.x * NT;
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
         if (row + u * rpi >= a.M) break;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float dz = bf2f(d[u][k]) * act_mask(bf2f(o[u][k]), a.act);
+          const float dz = bf2f(d[u][k]) * act_mask(bf2f(o[u][k]), ACT);
           sdz[k] += dz;
           sx[k] += dz * (bf2f(y[u][k]) - mean[k]) * rstd[k];
           if (two) sx2[k] += dz * (bf2f(y2[u][k]) - mean2[k]) * rstd2[k];
@@ -200,9 +201,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
+template <int ACT, bool TWO>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const int C8 = a.C >> 3;
-  const bool two = a.y2 != nullptr;
+  constexpr bool two = TWO;
   const float inv = 1.f / (float)a.M;
   if (blockIdx.x == 0) {  // parameter gradients
     for (int j = threadIdx.x; j < a.C; j += NT) {
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
     bf16x8 dy, dy2, dzo;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float dz = bf2f(dc[k]) * act_mask(bf2f(oc[k]), a.act);
+      const float dz = bf2f(dc[k]) * act_mask(bf2f(oc[k]), ACT);
       const float xh = (bf2f(yc[k]) - mean[k]) * rstd[k];
       dy[k] = f2bf(k1[k] * (dz - k2[k] - xh * q1[k]));
       if (two) {
@@ -336,12 +338,20 @@ void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
   // 4 chunks per thread (one trip): measured at the MobileNetV2 train-batch shapes 4 / 8 / 16 /
   // 32 / 64 chunks -> 179 / 186 / 218 / 295 / 453 us over the net (bench/small_bwd_bench.py):
   // the loop is latency-bound, not bound by the blocks' final atomics
-  if (a.phases & 1)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid_for(chunks, a.C / 8, 4, 256)), dim3(NT), 0,
-                       st, a);
-  if (a.phases & 2)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, a.C / 8, 4, 2048)), dim3(NT), 0,
-                       st, a);
+  // activation and shortcut-BN presence are compile-time (runtime values made the per-element
+  // code evaluate every activation form and select)
+  const bool two = a.y2 != nullptr;
+  if (a.act < 0 || a.act > 2) throw std::runtime_error("bn_bwd: act must be 0-2");
+  const dim3 g1(grid_for(chunks, a.C / 8, 4, 256)), g2(grid_for(chunks, a.C / 8, 4, 2048));
+#define BN_BWD_CASE(A, T)                                                                 \
+  if (a.act == A && two == T) {                                                           \
+    if (a.phases & 1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<A, T>), g1, dim3(NT), 0, st, a); \
+    if (a.phases & 2) hipLaunchKernelGGL((bn_bwd_apply_kernel<A, T>), g2, dim3(NT), 0, st, a);  \
+    return;                                                                               \
+  }
+  BN_BWD_CASE(0, false) BN_BWD_CASE(0, true) BN_BWD_CASE(1, false) BN_BWD_CASE(1, true)
+  BN_BWD_CASE(2, false) BN_BWD_CASE(2, true)
+#undef BN_BWD_CASE
 }
 
 void bn_running_launch(const BnRunEntry* tab, int nlayers, int maxC, float momentum,
