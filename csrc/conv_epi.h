@@ -68,10 +68,12 @@ MA_DEV float row16_sum(float v) {
 
 // ---------------------------------------------------------------- epilogue
 // BN-backward helpers (same arithmetic as bn.hip so fused and standalone reductions agree)
-MA_DEV float bn_act_mask(float out, int act) {
-  if (act == 1) return out > 0.f ? 1.f : 0.f;
-  if (act == 2) return (out > 0.f && out < 6.f) ? 1.f : 0.f;
-  return 1.f;
+// act'(out) != 0  <=>  lo < out < hi (finite outputs): bounds from the uniform act once, so the
+// per-element test is two compares and one select -- a runtime act switch inside the unrolled
+// element loop was if-converted into every activation form plus selects
+MA_DEV void bn_act_bounds(int act, float& lo, float& hi) {
+  lo = act == 0 ? -__builtin_huge_valf() : 0.f;
+  hi = act == 2 ? 6.f : __builtin_huge_valf();
 }
 MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, float (&mean)[8],
                           float (&rstd)[8]) {
@@ -219,6 +221,8 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
   const int colc = n0 + ch * 8;
   float mean[8], rstd[8], mean2[8], rstd2[8], sdz[8], sx[8], sx2[8];
   const bool two = bw && e.bw_y2 != nullptr;
+  float alo, ahi;
+  bn_act_bounds(e.bw_act, alo, ahi);
   if (bw) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = sx2[k] = mean2[k] = 0.f, rstd2[k] = 1.f;
@@ -247,7 +251,8 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       if (two) ay2 = *(const bf16x8*)(e.bw_y2 + off);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float dz = bf2f(v[k]) * bn_act_mask(bf2f(ao[k]), e.bw_act);
+        const float ok = bf2f(ao[k]);
+        const float dz = (ok > alo && ok < ahi) ? bf2f(v[k]) : 0.f;
         sdz[k] += dz;
         sx[k] += dz * (bf2f(ay[k]) - mean[k]) * rstd[k];
         if (two) sx2[k] += dz * (bf2f(ay2[k]) - mean2[k]) * rstd2[k];
