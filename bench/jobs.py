@@ -16,6 +16,8 @@ jobs
   presets                            every BASELINE config's bench (configs 2-5)
   ab        --env "A=1" "A=0" ...    same-box interleaved A/B of env settings (2 rounds)
   ab-ext    --old OLD.so             same-box A/B of another build (MERCURY_EXT_PATH)
+  ab-preset --old OLD.so --args CFG  ... on one BASELINE preset
+  ab-kernel --old OLD.so --args CMD  ... on a microbenchmark (bench/pool_bench.py, ...)
   sweep                              graph-timed conv plan sweeps (igemm and halo conv)
   learn                              learning check of the ResNet-50/224 preset
 """
@@ -157,6 +159,38 @@ def job_ab_ext(o, a):
     print(res, flush=True)
 
 
+def _last_ms(path):
+    with open(path) as f:
+        return json.loads(f.read().strip().splitlines()[-1])['ms_per_step']
+
+
+def job_ab_preset(o, a):
+    """same-box interleaved A/B of another build (--old OLD.so) on one preset (--args CONFIG)"""
+    cfg = a.args or 'resnet18-cifar10'
+    res = {'old': [], 'new': []}
+    for rnd in range(a.rounds):
+        for name, env in (('old', {'MERCURY_EXT_PATH': a.old}), ('new', {})):
+            out = os.path.join(o, '%s%d.json' % (name, rnd + 1))
+            run([PY, 'bench.py', '--config', cfg, '--steps', '100', '--warmup', '10',
+                 '--no-overhead'], out, 200, env=env)
+            res[name].append(_last_ms(out))
+    print(json.dumps(res), flush=True)
+    with open(os.path.join(o, 'ab.json'), 'w') as f:
+        json.dump(res, f)
+
+
+def job_ab_kernel(o, a):
+    """same-box interleaved A/B of another build (--old OLD.so) on a microbenchmark
+    (--args 'bench/pool_bench.py ...'); prints each run's last JSON line"""
+    cmd = [PY] + shlex.split(a.args)
+    for rnd in range(a.rounds + 1):
+        for name, env in (('old', {'MERCURY_EXT_PATH': a.old}), ('new', {})):
+            out = os.path.join(o, '%s%d.json' % (name, rnd + 1))
+            run(cmd, out, 200, env=env)
+            print(name, end=' ', flush=True)
+            tail(out, 1)
+
+
 def job_sweep(o, a):
     for b in (32, 320):
         run([PY, 'bench/kernel_sweep.py', '--batch', str(b), '--kind', 'fwd', '--pipes', '0'],
@@ -175,7 +209,8 @@ def job_learn(o, a):
 
 JOBS = {'tests': job_tests, 'bench': job_bench, 'session': job_session, 'trace': job_trace,
         'pmc': job_pmc, 'presets': job_presets, 'ab': job_ab, 'ab-ext': job_ab_ext,
-        'sweep': job_sweep, 'learn': job_learn}
+        'sweep': job_sweep, 'learn': job_learn, 'ab-preset': job_ab_preset,
+        'ab-kernel': job_ab_kernel}
 
 
 def main():
