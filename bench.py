@@ -87,6 +87,10 @@ def diagnostics(eng, steps, ws):
           'overlap_frac': med.get('overlap')}
     torch.cuda.synchronize()
     if ws > 1:
+        # every rank's communicator must span the whole job (one rank per GPU)
+        if dp['comm_ranks'] != ws:
+            raise RuntimeError('DP communicator spans %s ranks, job has %d'
+                               % (dp['comm_ranks'], ws))
         from mercury_amd.parallel.health import check_replicas
         ok, spread = check_replicas(eng.opt.p)
         dp['replicas_identical'] = bool(ok)

@@ -68,12 +68,21 @@ MA_DEV float row16_sum(float v) {
 
 // ---------------------------------------------------------------- epilogue
 // BN-backward helpers (same arithmetic as bn.hip so fused and standalone reductions agree)
-// act'(out) != 0  <=>  lo < out < hi (finite outputs): bounds from the uniform act once, so the
-// per-element test is two compares and one select -- a runtime act switch inside the unrolled
-// element loop was if-converted into every activation form plus selects
+// act'(out) != 0  <=>  act == none, or lo < out < hi: bounds from the uniform act once, so the
+// per-element test is two compares, one uniform OR and one select -- a runtime act switch inside
+// the unrolled element loop was if-converted into every activation form plus selects.  act ==
+// none passes EVERY value (NaN and +-inf included), exactly like bn.hip's act_mask, so a
+// diverging run is not hidden from the health checks by the fused reduction.
 MA_DEV void bn_act_bounds(int act, float& lo, float& hi) {
   lo = act == 0 ? -__builtin_huge_valf() : 0.f;
   hi = act == 2 ? 6.f : __builtin_huge_valf();
+}
+// Forward clamp bounds: act == none clamps against NaN, which v_max/v_min_f32 ignore (they
+// return the non-NaN operand), so the clamp is the identity and a NaN input stays NaN as in
+// bn.hip's act_fwd; relu / relu6 clamp as act_fwd does.
+MA_DEV void act_clamp_bounds(int act, float& lo, float& hi) {
+  lo = act == 0 ? __builtin_nanf("") : 0.f;
+  hi = act == 2 ? 6.f : (act == 0 ? __builtin_nanf("") : __builtin_huge_valf());
 }
 MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, float (&mean)[8],
                           float (&rstd)[8]) {
@@ -223,6 +232,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
   const bool two = bw && e.bw_y2 != nullptr;
   float alo, ahi;
   bn_act_bounds(e.bw_act, alo, ahi);
+  const bool pass = e.bw_act == 0;
   if (bw) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = sx2[k] = mean2[k] = 0.f, rstd2[k] = 1.f;
@@ -252,7 +262,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float ok = bf2f(ao[k]);
-        const float dz = (ok > alo && ok < ahi) ? bf2f(v[k]) : 0.f;
+        const float dz = (pass || (ok > alo && ok < ahi)) ? bf2f(v[k]) : 0.f;
         sdz[k] += dz;
         sx[k] += dz * (bf2f(ay[k]) - mean[k]) * rstd[k];
         if (two) sx2[k] += dz * (bf2f(ay2[k]) - mean2[k]) * rstd2[k];

@@ -42,13 +42,11 @@ namespace {
 constexpr int NSLOT = 3;     // weight ring slots (prefetch distance 2)
 constexpr int HRMAX = 16;    // halo DMA pieces per wave (32 pixels per piece over 4 waves)
 
-// Activation as one clamp [lo, hi] (none: -inf..inf, relu: 0..inf, relu6: 0..6) -- branch-free:
-// a per-element if-chain on the kernel-uniform selector compiled to two scalar branches per
-// element (255 in one halo transform, ~3x the transform's cost)
-MA_DEV void act_bounds(int act, float& lo, float& hi) {
-  lo = act == 0 ? -__builtin_huge_valf() : 0.f;
-  hi = act == 2 ? 6.f : __builtin_huge_valf();
-}
+// Activation as one clamp [lo, hi] (none: NaN bounds = identity that keeps NaN, relu: 0..inf,
+// relu6: 0..6; conv_epi.h act_clamp_bounds) -- branch-free: a per-element if-chain on the
+// kernel-uniform selector compiled to two scalar branches per element (255 in one halo
+// transform, ~3x the transform's cost)
+MA_DEV void act_bounds(int act, float& lo, float& hi) { act_clamp_bounds(act, lo, hi); }
 
 // per-channel scale / shift of one BatchNorm for 8 channels (same arithmetic as bn.hip), in two
 // halves so the 16-byte loads can be issued a whole slice before they are needed

@@ -305,8 +305,8 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       const float gv[8] = {pst[4].x, pst[4].y, pst[4].z, pst[4].w, pst[5].x, pst[5].y, pst[5].z, pst[5].w};
       const float bv[8] = {pst[6].x, pst[6].y, pst[6].z, pst[6].w, pst[7].x, pst[7].y, pst[7].z, pst[7].w};
       float sc[8], sh[8];
-      const float plo = pro.act == 0 ? -__builtin_huge_valf() : 0.f;
-      const float phi = pro.act == 2 ? 6.f : __builtin_huge_valf();
+      float plo, phi;
+      act_clamp_bounds(pro.act, plo, phi);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {   // same arithmetic as bn.hip scale_shift8
         float mean = mv[k], var = vv[k];
@@ -323,7 +323,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
         bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          // branch-free activation: clamp to the act's bounds (-inf/0, 6/+inf)
+          // branch-free activation: clamp to the act's bounds (identity for none)
           o[k] = f2bf(fminf(fmaxf(bf2f(y[k]) * sc[k] + sh[k], plo), phi));
         }
         const u32x4 t = __builtin_bit_cast(u32x4, o);

@@ -16,7 +16,8 @@
 // Each rank moves 2 (W-1)/W n elements over xGMI -- the same as a ring -- but spread over
 // W-1 links instead of one.  The passes are separated by stream-ordered barriers (a one-
 // element RCCL all-reduce on the same stream, or a host barrier in tests), so the kernels
-// themselves need no cross-GPU flags.  ``wire_bf16``: the exchange buffers hold bf16 (half the
+// themselves need no cross-GPU flags.  Exchange-buffer traffic uses system-coherent (sc0|sc1)
+// buffer loads and stores, so no reader depends on kernel-boundary cache maintenance.  ``wire_bf16``: the exchange buffers hold bf16 (half the
 // bytes over the links); sums are accumulated in fp32 and rounded once per pass.
 //
 // For testing on one GPU the "peers" are simply W local buffers (emulated ranks).
@@ -33,26 +34,38 @@ struct Peers {
   const void* p[XMAX];
 };
 
-MA_DEV f32x4 ld4(const void* base, long long i, bool bf) {
-  if (!bf) return ((const f32x4*)base)[i];
-  const bf16* b = (const bf16*)base + i * 4;
-  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-  const bf16x4_t v = *(const bf16x4_t*)b;
-  return f32x4{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+// Every access to an exchange buffer is SYSTEM-coherent (buffer ops with sc0|sc1): the buffers
+// are ordinary coarse-grained allocations mapped into the peers over IPC, and a reader's
+// non-coherent L2 could otherwise serve a line cached from the previous bucket that used the
+// same address -- a failure one GPU (where all "peers" share an L2) can never show.  Stores are
+// written through to memory for the same reason.  (Streaming, so the bypass costs nothing.)
+constexpr int SYS = 1 | 16;   // sc0 | sc1
+
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+
+MA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000);
 }
 
-MA_DEV void st4(void* base, long long i, f32x4 v, bool bf) {
+MA_DEV f32x4 ld4(__amdgpu_buffer_rsrc_t r, long long i, bool bf) {
+  if (!bf) return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, SYS));
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, SYS);
+  const bf16x2 lo = __builtin_bit_cast(bf16x2, v[0]), hi = __builtin_bit_cast(bf16x2, v[1]);
+  return f32x4{bf2f(lo[0]), bf2f(lo[1]), bf2f(hi[0]), bf2f(hi[1])};
+}
+
+MA_DEV void st4(__amdgpu_buffer_rsrc_t r, long long i, f32x4 v, bool bf) {
   if (!bf) {
-    ((f32x4*)base)[i] = v;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(i * 16), 0, SYS);
     return;
   }
-  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-  bf16x4_t o;
-  o[0] = f2bf(v[0]);
-  o[1] = f2bf(v[1]);
-  o[2] = f2bf(v[2]);
-  o[3] = f2bf(v[3]);
-  *(bf16x4_t*)((bf16*)base + i * 4) = o;
+  bf16x2 lo, hi;
+  lo[0] = f2bf(v[0]);
+  lo[1] = f2bf(v[1]);
+  hi[0] = f2bf(v[2]);
+  hi[1] = f2bf(v[3]);
+  const u32x2_t o{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
+  __builtin_amdgcn_raw_buffer_store_b64(o, r, (int)(i * 8), 0, SYS);
 }
 
 // chunk r = [off(r), off(r+1)) in float4 units
@@ -61,37 +74,41 @@ __host__ __device__ inline long long chunk_off(long long n4, int W, int r) { ret
 template <bool BF>
 __global__ __launch_bounds__(256) void xgmi_rs_kernel(Peers peers, int W, int rank, long long n4,
                                                       float scale) {
+  const long long bytes = n4 * (BF ? 8 : 16);
+  __amdgpu_buffer_rsrc_t r[XMAX];
+#pragma unroll
+  for (int q = 0; q < XMAX; ++q) r[q] = rsrc(peers.p[q < W ? q : 0], bytes);
   const long long c0 = chunk_off(n4, W, rank), c1 = chunk_off(n4, W, rank + 1);
   for (long long i = c0 + (long long)blockIdx.x * 256 + threadIdx.x; i < c1;
        i += (long long)gridDim.x * 256) {
-    f32x4 acc = ld4(peers.p[0], i, BF);
+    f32x4 acc = ld4(r[0], i, BF);
 #pragma unroll
     for (int q = 1; q < XMAX; ++q)
-      if (q < W) acc += ld4(peers.p[q], i, BF);
-    st4((void*)peers.p[rank], i, acc * scale, BF);
+      if (q < W) acc += ld4(r[q], i, BF);
+    st4(r[rank < XMAX ? rank : 0], i, acc * scale, BF);
   }
 }
 
-// dst (fp32, local) <- chunk p of peer p, for every p
+// dst (fp32, local) <- chunk p of peer p: blockIdx.y = p, one contiguous stream per peer (all
+// W-1 remote links read in parallel, no per-element owner search)
 template <bool BF>
 __global__ __launch_bounds__(256) void xgmi_ag_kernel(Peers peers, int W, long long n4,
                                                       float* __restrict__ dst) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * 256) {
-    // owner of element i: the p with off(p) <= i < off(p+1)
-    int p = (int)((i * W) / n4);
-    while (p > 0 && chunk_off(n4, W, p) > i) --p;
-    while (p + 1 < W && chunk_off(n4, W, p + 1) <= i) ++p;
-    ((f32x4*)dst)[i] = ld4(peers.p[p], i, BF);
-  }
+  const int p = blockIdx.y;
+  const auto r = rsrc(peers.p[p], n4 * (BF ? 8 : 16));
+  const long long c0 = chunk_off(n4, W, p), c1 = chunk_off(n4, W, p + 1);
+  for (long long i = c0 + (long long)blockIdx.x * 256 + threadIdx.x; i < c1;
+       i += (long long)gridDim.x * 256)
+    ((f32x4*)dst)[i] = ld4(r, i, BF);
 }
 
+template <bool BF>
 __global__ __launch_bounds__(256) void xgmi_pack_kernel(const float* __restrict__ src,
-                                                        void* __restrict__ xbuf, long long n4,
-                                                        int bf) {
+                                                        void* __restrict__ xbuf, long long n4) {
+  const auto r = rsrc(xbuf, n4 * (BF ? 8 : 16));
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4;
        i += (long long)gridDim.x * 256)
-    st4(xbuf, i, ((const f32x4*)src)[i], bf != 0);
+    st4(r, i, ((const f32x4*)src)[i], BF);
 }
 
 unsigned grid_for(long long n4) {
@@ -104,7 +121,10 @@ unsigned grid_for(long long n4) {
 // n: element count (a multiple of 4; the engine's buckets are 4-aligned flat ranges)
 void xgmi_pack(const float* src, void* xbuf, long long n, int bf, hipStream_t st) {
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(xgmi_pack_kernel, dim3(grid_for(n4)), dim3(256), 0, st, src, xbuf, n4, bf);
+  if (bf)
+    hipLaunchKernelGGL(xgmi_pack_kernel<true>, dim3(grid_for(n4)), dim3(256), 0, st, src, xbuf, n4);
+  else
+    hipLaunchKernelGGL(xgmi_pack_kernel<false>, dim3(grid_for(n4)), dim3(256), 0, st, src, xbuf, n4);
 }
 
 void xgmi_reduce_scatter(const void* const* peers, int W, int rank, long long n, int bf,
@@ -126,10 +146,11 @@ void xgmi_all_gather(const void* const* peers, int W, long long n, int bf, float
   Peers p{};
   for (int q = 0; q < W && q < XMAX; ++q) p.p[q] = peers[q];
   const long long n4 = n / 4;
+  const dim3 grid(grid_for((n4 + W - 1) / W), W);
   if (bf)
-    hipLaunchKernelGGL(xgmi_ag_kernel<true>, dim3(grid_for(n4)), dim3(256), 0, st, p, W, n4, dst);
+    hipLaunchKernelGGL(xgmi_ag_kernel<true>, grid, dim3(256), 0, st, p, W, n4, dst);
   else
-    hipLaunchKernelGGL(xgmi_ag_kernel<false>, dim3(grid_for(n4)), dim3(256), 0, st, p, W, n4, dst);
+    hipLaunchKernelGGL(xgmi_ag_kernel<false>, grid, dim3(256), 0, st, p, W, n4, dst);
 }
 
 int xgmi_max_ranks() { return XMAX; }

@@ -832,7 +832,11 @@ class NativeEngine(object):
             self.isw.fill_(1.0)
             return
         # groupwise (Groupwise_Sampler, `util.py:114-138`): the pool is the next CONTIGUOUS slice
-        # of the shard (cursor order, wrapping), which becomes this iteration's group
+        # of the shard (cursor order, wrapping), which becomes this iteration's group.
+        # Deviation (parity unpinned: no reference fixture covers it): when Ns % P != 0 the
+        # slice that reaches the end of the shard wraps to its head and stays a full P-sample
+        # group, where the reference truncates it at len(dataset) (a short group) and resets
+        # the cursor.  Group sizes stay P, so the table weights need no short-group handling.
         ops.pool_build(self.shard, self.shard_labels, self.ctrl, sm.input, sm.label, sm.index,
                        self.P, self.B, self.seed, zero=sm.stats_arena,
                        shuffle=self.sampler != 'groupwise')
@@ -944,6 +948,8 @@ class NativeEngine(object):
         whose shortcut parameters precede its last unit's is cut only at its boundary."""
         if not self.dp:
             return {}
+        if getattr(self, '_bucket_plan', None) is not None:
+            return self._bucket_plan       # static: cached once (the issue loop reads it)
         starts = self._block_starts()
         cuts = {}
         end = self.lw.total
@@ -961,6 +967,7 @@ class NativeEngine(object):
                 if (bi == 0 and i == 0) or (end - start) * 4 >= self.bucket_bytes:
                     cuts[bi, i] = (0 if (bi == 0 and i == 0) else start, end)
                     end = start
+        self._bucket_plan = cuts
         return cuts
 
     def tail(self):
@@ -1147,7 +1154,8 @@ class NativeEngine(object):
 
     @property
     def _nseg(self):
-        return len(self.bucket_plan()) + (0 if (0, 0) in self.bucket_plan() else 1)
+        plan = self.bucket_plan()
+        return len(plan) + (0 if (0, 0) in plan else 1)
 
     def _debug_sync(self, what):
         """Debug mode: drain the device after every phase so a fault names its phase."""

@@ -226,9 +226,14 @@ class Trainer(object):
         return running_train_loss, runing_train_acc, presam_ema_loss
 
     def _advance(self):
-        """Count a finished step, then checkpoint on cadence: the saved state is exactly
-        "``epoch_step`` steps of epoch ``epoch`` done, ``step`` is the next step", so a resume
-        finishes the partial epoch before the LR scheduler advances (see ``fit``)."""
+        """Count a finished step, then checkpoint on cadence.  Restored exactly on resume: the
+        step counter ("``epoch_step`` steps of epoch ``epoch`` done, ``step`` is the next
+        step"), so the resumed run finishes the partial epoch before the LR scheduler advances
+        and follows the same LR sequence (see ``fit``), plus weights and optimizer state.  NOT
+        restored by the eager Trainer: the presample-iterator position and the pending scored
+        pool -- a mid-epoch resume re-primes ``update_samples`` from a fresh iterator, so the
+        data order (and hence the losses) after the resume differ from an uninterrupted run.
+        (The native engine's checkpoint also carries its counters, EMA and importance table.)"""
         self.step += 1
         self.epoch_step += 1
         cfg = self.cfg

@@ -5,9 +5,9 @@ Host meters keep the reference field names and string formats
 syncs the device on every ``update`` (``.item()`` in ``Accuracy.update``,
 ``util.py:228``); here ``Accuracy`` and ``Average`` accept device tensors and
 keep them on device until someone reads ``.accuracy`` / ``.average`` -- the
-hot loop never forces a device->host sync.  ``DeviceMeters`` is the
-graph-capturable form used by the native engine: fixed device buffers that
-kernels accumulate into and that are read back only at log cadence.
+hot loop never forces a device->host sync.  The native engine's graph-captured
+form is its fixed ``meters`` buffer (engine/native.py): kernels accumulate into
+it and it is read back only at log cadence (``read_meters``).
 """
 from __future__ import annotations
 
@@ -95,30 +95,3 @@ class Accuracy(object):
 
     def __str__(self):
         return '{:.2f}%'.format(self.accuracy * 100)
-
-
-class DeviceMeters(object):
-    """Fixed device buffers for graph-captured steps.
-
-    Layout of ``buf`` (fp32): [0] loss*count sum, [1] sample count,
-    [2] correct count, [3] pool-mean-loss EMA value, [4] EMA initialised flag.
-    Kernels in the native engine accumulate into these addresses, so the
-    tensor must never be reallocated.
-    """
-
-    LOSS_SUM, COUNT, CORRECT, EMA, EMA_INIT = range(5)
-
-    def __init__(self, device):
-        self.buf = torch.zeros(8, dtype=torch.float32, device=device)
-
-    def reset(self, keep_ema=True):
-        if keep_ema:
-            self.buf[:3].zero_()
-        else:
-            self.buf.zero_()
-
-    def read(self):
-        b = self.buf.detach().cpu().tolist()
-        cnt = max(b[self.COUNT], 1.0)
-        return {'loss': b[self.LOSS_SUM] / cnt, 'acc': b[self.CORRECT] / cnt,
-                'ema': b[self.EMA], 'count': b[self.COUNT]}

@@ -807,6 +807,54 @@ def test_conv_fwd_bn_apply_prologue(case, mode):
         close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
 
 
+def test_fused_bn_paths_propagate_nan_like_bn_hip():
+    """act='none' (MobileNetV2's linear bottleneck): a NaN in the producer output must come out
+    of the fused prologue as NaN, exactly where the standalone bn_apply + conv produces NaN,
+    and the fused dgrad BN-backward reduction must see it (sums NaN, as bn_bwd's)."""
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes, dgrad_plan
+    N, H, W, C, K = 4, 8, 8, 64, 128
+    spec = ConvSpec(N, H, W, C, K, 1, 1, 1, 0)
+    g = torch.Generator(device='cpu').manual_seed(3)
+    y = bf(torch.randn(N * H * W, C, generator=g)).to(DEV)
+    y[5, 7] = float('nan')
+    y[77, 0] = float('nan')
+    yn = y.to(torch.bfloat16)
+    w = bf(torch.randn(K, C, 1, 1, generator=g) / 8).to(DEV)
+    wk, wt = ops.pack_conv_weight(w)
+    gamma = torch.ones(C, device=DEV)
+    beta = torch.zeros(C, device=DEV)
+    rmean, rvar = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    plan = fwd_plan(spec)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, K, *plan[:3]) // 4), device=DEV)
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    conv_pro_direct(ops, yn, wk, out, spec, slab, plan,
+                    dict(gamma=gamma, beta=beta, act='none', eps=0.0, rmean=rmean, rvar=rvar))
+    an = torch.empty_like(yn)
+    ops.bn_apply(yn, None, gamma, beta, an, N * H * W, C, act='none', eps=0.0,
+                 running=(rmean, rvar))
+    out2 = torch.empty_like(out)
+    ops.conv_fwd(an, wk, out2, spec, slab=slab, plan=plan)
+    nan1, nan2 = torch.isnan(out.float()), torch.isnan(out2.float())
+    assert nan2.any() and torch.equal(nan1, nan2)
+    fin = ~nan1
+    close(out.float()[fin], out2.float()[fin], rtol=1e-2, atol=1e-2)
+    # backward, act none: the fused reduce must pass dz = dx even where the saved activation
+    # is NaN (bn_bwd's act_mask is 1 for none), so sum(dz) is the plain column sum of dx
+    dspec = ConvSpec(N, H, W, C, K, 1, 1, 1, 0)
+    gy = bf(torch.randn(spec.M, K, device=DEV)).to(torch.bfloat16)
+    dx = torch.empty(N * H * W, C, dtype=torch.bfloat16, device=DEV)
+    yc = bf(torch.randn(N * H * W, C, device=DEV)).to(torch.bfloat16)
+    stats = torch.stack([yc.float().sum(0), yc.float().pow(2).sum(0)]).contiguous()
+    sums = torch.zeros(3, C, device=DEV)
+    dplan = dgrad_plan(dspec)
+    dslab = torch.zeros(max(1, slab_bytes(N * H * W, C, *dplan) // 4), device=DEV)
+    ops.conv_dgrad(gy, wt, dx, dspec, slab=dslab, plan=dplan,
+                   bw=dict(out=an, y=yc, stats=stats, sums=sums, act='none', eps=1e-5))
+    assert torch.isfinite(sums[:2]).all()
+    close(sums[0], dx.float().sum(0), 1e-3, 1e-2)
+
+
 def _halo_case(ops, case, plan, gimgs):
     from mercury_amd.ops.conv import ConvSpec
     N, H, W, C, K, R, S, st, pd = case
