@@ -83,6 +83,8 @@ def diagnostics(eng, steps, ws):
           (dist.get_world_size() if dist.is_initialized() else 1),
           'buckets_bytes': [4 * (e - s) for s, e in sorted(plan.values(), reverse=True)],
           'wire': 'ternary' if eng.grad_compress else ('bf16' if eng.wire_bf16 else 'fp32'),
+          # bucket all-reduces captured inside the train graph (timed diag steps: segmented)
+          'comm_in_graph': bool(eng.graphs and 'train_dp' in eng.graphs),
           'allreduce_ms_per_step': med.get('comm'), 'comm_exposed_ms': med.get('comm_exposed'),
           'overlap_frac': med.get('overlap')}
     torch.cuda.synchronize()

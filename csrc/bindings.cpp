@@ -73,6 +73,21 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
     check_launch("igemm");
   });
+  // 1x1 conv as a persistent LDS-DMA GEMM (pgemm.hip); returns 0 if unsupported
+  m.def("pgemm", [](uintptr_t a, uintptr_t b, uintptr_t out, uintptr_t stats, int M, int N, int K,
+                    int ldo, int stats_ld, int group_rows, long long a_bytes, long long b_bytes,
+                    long long out_bytes, int H, int W, int Pp, int Q, int stride, int bn, int grid,
+                    uintptr_t st) {
+    const long long lim = 0xFFFFFF00LL;
+    if (a_bytes >= lim || b_bytes >= lim || out_bytes >= lim)
+      throw std::invalid_argument("pgemm: tensors must be < 4 GB (32-bit buffer offsets)");
+    PgemmArgs g{P<const bf16>(a), P<const bf16>(b), P<bf16>(out), P<float>(stats), M, N, K, ldo,
+                stats_ld, group_rows, (unsigned)a_bytes, (unsigned)b_bytes, (unsigned)out_bytes,
+                H, W, Pp, Q, stride};
+    const int ok = pgemm_launch(g, bn, grid, S(st));
+    check_launch("pgemm");
+    return ok;
+  });
   // forward conv whose A operand is BN-applied + activated on load (ProParams, igemm.h)
   m.def("igemm_pro", [](uintptr_t src, uintptr_t wt, uintptr_t out, int ldo, uintptr_t bias,
                         uintptr_t stats, int stats_ld, int group_rows, uintptr_t slab, int SH,
@@ -396,8 +411,9 @@ PYBIND11_MODULE(_C, m) {
     check_launch("quantize");
   });
   m.def("tern_pack", [](uintptr_t x, long long n, uintptr_t ws, uint32_t seed, uint64_t counter,
-                        uintptr_t words, uintptr_t st) {
-    tern_pack_launch(P<const float>(x), n, P<float>(ws), seed, counter, P<uint32_t>(words), S(st));
+                        uintptr_t words, uintptr_t st, uintptr_t dctr) {
+    tern_pack_launch(P<const float>(x), n, P<float>(ws), seed, counter, P<const long long>(dctr),
+                     P<uint32_t>(words), S(st));
     check_launch("tern_pack");
   });
   m.def("tern_unpack", [](uintptr_t msgs, int W, long long n, float scale, uintptr_t out,

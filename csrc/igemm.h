@@ -128,6 +128,22 @@ struct HconvPro {
 };
 
 // returns 0 when (bm, bn) is not instantiated
+// ---------------------------------------------------------------------------- pointwise GEMM
+// 1x1 convolution as a persistent LDS-DMA-pipelined GEMM (pgemm.hip): OUT[M][ldo] (bf16) =
+// A[rows][K] . B[N][K]^T with optional ghost-BN statistics of OUT.  stride != 1: A row of output
+// pixel m = (n, p, q) is n*H*W + p*stride*W + q*stride (1x1 stride-2 shortcut convs).
+struct PgemmArgs {
+  const bf16* a;
+  const bf16* b;
+  bf16* out;
+  float* stats;            // [G][2][stats_ld] (sum, sumsq) or null
+  int M, N, K, ldo, stats_ld, group_rows;
+  unsigned a_bytes, b_bytes, out_bytes;   // buffer-resource ranges (< 4 GB)
+  int H, W, P, Q, stride;
+};
+// bn in {64, 128, 256}; grid <= 0: one block per CU.  Returns 0 when unsupported.
+int pgemm_launch(const PgemmArgs& g, int bn, int grid, hipStream_t st);
+
 int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                  const HconvPro& pro, int bm, int bn, int splits, hipStream_t st);
 const bf16* conv_zero_page();

@@ -214,7 +214,7 @@ void pack_weights_launch(const float* p, const OptSeg* segs, int nsegs, long lon
 void quantize_launch(const float* x, float* out, float* absmax_ws, long long n, uint32_t seed,
                      uint64_t counter, hipStream_t st);
 void tern_pack_launch(const float* x, long long n, float* absmax_ws, uint32_t seed,
-                      uint64_t counter, uint32_t* words, hipStream_t st);
+                      uint64_t counter, const long long* dctr, uint32_t* words, hipStream_t st);
 void tern_unpack_launch(const uint32_t* msgs, int W, long long n, float scale, float* out,
                         hipStream_t st);
 struct PoolArgs {                 // max-pool / avg-pool NHWC bf16

@@ -196,8 +196,12 @@ __global__ __launch_bounds__(NT) void quantize_kernel(const float* x, float* y, 
 // Unbiased per rank (E[scale * c] = x); the receiver sums scale_r * c_r over the W messages.
 __global__ __launch_bounds__(NT) void tern_pack_kernel(const float* x, long long n,
                                                        const float* amax, uint32_t seed,
-                                                       uint64_t counter, uint32_t* words) {
+                                                       uint64_t counter, const long long* dctr,
+                                                       uint32_t* words) {
   const long long j = (long long)blockIdx.x * NT + threadIdx.x;   // word index
+  // graph-replayed steps: the Philox stream comes from the device step counter (a captured
+  // host counter would replay the same stream every step), 256 buckets per step
+  if (dctr) counter = ((uint64_t)dctr[0] << 8) + counter;
   const long long nw = (n + 15) / 16;
   const float m = *amax;
   if (j == 0) words[0] = __float_as_uint(m);
@@ -298,14 +302,14 @@ void quantize_launch(const float* x, float* out, float* absmax_ws, long long n, 
                      seed, counter);
 }
 void tern_pack_launch(const float* x, long long n, float* absmax_ws, uint32_t seed,
-                      uint64_t counter, uint32_t* words, hipStream_t st) {
+                      uint64_t counter, const long long* dctr, uint32_t* words, hipStream_t st) {
   hipMemsetAsync(absmax_ws, 0, sizeof(float), st);
   const long long blocks = (n + NT - 1) / NT;
   hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks > 1024 ? 1024 : blocks)), dim3(NT), 0, st,
                      x, n, absmax_ws);
   const long long nw = (n + 15) / 16;
   hipLaunchKernelGGL(tern_pack_kernel, dim3((unsigned)((nw + NT - 1) / NT)), dim3(NT), 0, st, x, n,
-                     absmax_ws, seed, counter, words);
+                     absmax_ws, seed, counter, dctr, words);
 }
 void tern_unpack_launch(const uint32_t* msgs, int W, long long n, float scale, float* out,
                         hipStream_t st) {

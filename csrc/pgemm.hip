@@ -1,0 +1,383 @@
+// Pointwise (1x1) convolution as a persistent, LDS-DMA-pipelined MFMA GEMM (gfx950).
+//
+//   OUT[m][n] = sum_k A[m][k] * B[n][k]        A = NHWC activation rows (m = output pixel; a
+//                                              stride-2 1x1 conv gathers rows (n, 2p, 2q)),
+//                                              B = weights [Cout][Cin], k = input channel
+//
+// ResNet-50's bottleneck 1x1s (`pytorch_model.py:44-49`, 2/3 of its forward FLOPs) and
+// MobileNetV2's expand / project convs are plain GEMMs in NHWC, scored at B = 1280 / 320
+// (`pytorch_collab.py:95-103`): M = 62k..4M rows, K and N = 64..2048.  Most of these shapes sit
+// near the HBM/MFMA balance point, so the design goal is to stream A from HBM ONCE at full rate
+// while the matrix cores stay busy:
+//
+//   * persistent: one 512-thread block per CU walks a CONTIGUOUS range of 256-row output tiles
+//     (N-tiles of one M panel back to back, so the panel's re-reads are L2 hits) as one
+//     continuous stream of K-steps -- the next tile's first operand tiles are in flight while
+//     the current tile finishes and while its epilogue stores drain;
+//   * operands go HBM -> LDS by buffer LDS-DMA (`buffer_load_dwordx4 ... lds`, 1 KB per wave
+//     instruction) into an S-slot ring of (256 + BN) x 32 bf16 K-steps; waits are counted
+//     `s_waitcnt vmcnt(N)` + raw `s_barrier`, so S - 2 steps stay in flight across every
+//     barrier and nothing drains the ring (no compiler-visible global load inside the loop);
+//   * padding (rows past M, channels past N, K not a multiple of 32) costs nothing: those
+//     lanes' DMA offsets point past the buffer resource's range, which lands zeros; stores to
+//     such offsets are dropped by the same range check;
+//   * 8 waves (two per SIMD), 16x16x32 bf16 MFMA with weights as the MFMA "A" operand, so each
+//     lane's accumulator holds 4 consecutive channels of one pixel (8 contiguous NHWC bytes):
+//     the epilogue stores straight from registers and reduces the ghost-BN statistics (sum,
+//     sum of squares per channel and 32-image group) with DPP row sums;
+//   * step s + 1's fragments are read from LDS while step s's MFMAs issue
+//     (`sched_group_barrier` interleave);
+//   * LDS rows are 64 B (one K-step); chunk c of row r lives at chunk c ^ ((r >> 1) & 3), which
+//     makes every ds_read_b128 fragment read conflict-free for the four 16-lane groups of
+//     gfx950 (checked exhaustively on the host, `bench/lds_swizzle_check.py`); the DMA side
+//     applies the inverse permutation on the SOURCE address (the LDS image is lane-linear).
+#include "common.h"
+#include "igemm.h"
+
+namespace {
+
+constexpr int PG_BM = 256;        // output rows per tile
+constexpr int PG_BK = 32;         // K per step (one 16x16x32 MFMA k-block)
+constexpr int PG_NW = 8;          // waves per block
+constexpr int PG_NT = 64 * PG_NW;
+constexpr unsigned PG_OOB = 0xFFFFFF00u;   // byte offset past every tensor: zeros / dropped
+
+MA_DEV unsigned pg_lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+MA_DEV __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+}
+
+// 16 bytes per lane, buffer -> LDS; lane l lands at the wave-uniform LDS byte address + 16 l.
+// Inline asm on purpose: hipcc models LDS-DMA as an LDS event and would then answer every
+// fragment read with lgkmcnt(0) / drain the ring; completion is tracked by our own vmcnt waits.
+MA_DEV void pg_dma16(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               ::"v"(off), "s"(r), "s"(lds) : "memory");
+}
+
+template <int N>
+MA_DEV void pg_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// barrier without __syncthreads' release fence (its vmcnt(0) would drain the DMA ring)
+MA_DEV void pg_bar() { asm volatile("s_barrier" ::: "memory"); }
+
+MA_DEV float pg_row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// wait until a step's DMA pieces have landed: `newer` = whole steps (P pieces each) this wave
+// issued after it (0 .. S-2; wave-uniform, so the branches are scalar).  VMEM ops issued after
+// those (epilogue stores, stat atomics) are not counted: the wait then also covers some of
+// them -- longer, never too short.
+template <int P>
+MA_DEV void pg_wait_steps(int newer) {
+  switch (newer) {
+    case 0: pg_wait<0>(); break;
+    case 1: pg_wait<P>(); break;
+    case 2: pg_wait<2 * P>(); break;
+    case 3: pg_wait<3 * P>(); break;
+    default: pg_wait<4 * P>(); break;
+  }
+}
+
+template <int BN, int WM, int S, bool STATS, bool GATHER>
+__global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
+  constexpr int BM = PG_BM, WN = PG_NW / WM;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  constexpr int PA = BM / 16 / PG_NW;                     // A pieces per wave per step
+  constexpr int PB = BN >= 128 ? BN / 16 / PG_NW : 1;     // B pieces (BN = 64: waves 4-7 dump)
+  constexpr int P = PA + PB;
+  constexpr int SA = BM * 64, SB = BN * 64, SLOT = SA + SB;
+  static_assert(TM >= 1 && TN >= 1 && PA >= 1, "tile shape");
+  static_assert(S >= 3 && S <= 6, "ring depth (pg_wait_steps covers newer <= 4)");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int wm = w / WN, wn = w % WN;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int mtiles = (g.M + BM - 1) / BM;
+  const int ntiles = mtiles * ntn;
+  // contiguous tile range of this block (N-tiles of one M panel consecutive)
+  const int G = gridDim.x, b = blockIdx.x;
+  const int t_begin = (int)((long long)ntiles * b / G), t_end = (int)((long long)ntiles * (b + 1) / G);
+  if (t_begin >= t_end) return;
+  const int KT = (g.K + PG_BK - 1) / PG_BK;               // K-steps per tile
+  const int NS = (t_end - t_begin) * KT;                  // steps of this block
+
+  const auto rs_a = pg_rsrc(g.a, g.a_bytes);
+  const auto rs_b = pg_rsrc(g.b, g.b_bytes);
+  const auto rs_o = pg_rsrc(g.out, g.out_bytes);
+  const unsigned s_ring = pg_lds_addr(smem);
+  const unsigned s_dump = s_ring + S * SLOT + wu * 1024;
+
+  // ---- DMA lane roles: piece row (lane >> 2), physical chunk (lane & 3), logical chunk lc
+  const int prow = lane >> 2;
+  const int lc = (lane & 3) ^ ((prow >> 1) & 3);
+  const bool kfull = (g.K & 31) == 0;
+  const int K8 = g.K >> 3;                                // 16-byte chunks per row
+  unsigned aoff[PA], boff[PB];                            // per tile: row byte offset + lc
+  auto set_tile = [&](int t) {
+    const int mt = t / ntn, nt = t - mt * ntn;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int m = mt * BM + 16 * (wu + PG_NW * j) + prow;
+      int src = m;
+      if constexpr (GATHER) {
+        const int pq = g.P * g.Q;
+        const int n = m / pq, rem = m - n * pq;
+        const int p = rem / g.Q, q = rem - p * g.Q;
+        src = (n * g.H + p * g.stride) * g.W + q * g.stride;
+      }
+      aoff[j] = m < g.M ? (unsigned)(((long long)src * g.K + lc * 8) * 2) : PG_OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int nr = 16 * (wu + PG_NW * j) + prow;
+      const int n = nt * BN + nr;
+      boff[j] = (n < g.N && nr < BN) ? (unsigned)((n * g.K + lc * 8) * 2) : PG_OOB;
+    }
+  };
+  auto issue = [&](int kt, int slot) {
+    const unsigned kb = (unsigned)(kt * 64);
+    const bool kok = kfull || kt * 4 + lc < K8;
+    const unsigned sa = s_ring + slot * SLOT, sb = sa + SA;
+#pragma unroll
+    for (int j = 0; j < PA; ++j)
+      pg_dma16(rs_a, kok ? aoff[j] + kb : PG_OOB, sa + 16 * (wu + PG_NW * j) * 64);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const bool real = 16 * (wu + PG_NW * j) < BN;
+      pg_dma16(rs_b, kok ? boff[j] + kb : PG_OOB,
+               real ? sb + 16 * (wu + PG_NW * j) * 64 : s_dump);
+    }
+  };
+
+  // ---- fragment read offsets (lane part constant: row & 15 = lane & 15)
+  const int fl = (lane & 15) * 64 + 16 * ((lane >> 4) ^ ((lane >> 1) & 3));
+  auto read_frags = [&](bf16x8 (&fa)[TM], bf16x8 (&fb)[TN], int slot) {
+    const char* sa = smem + slot * SLOT;
+    const char* sb = sa + SA;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+      fa[tm] = *(const bf16x8*)(sa + (wm * (BM / WM) + tm * 16) * 64 + fl);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      fb[tn] = *(const bf16x8*)(sb + (wn * (BN / WN) + tn * 16) * 64 + fl);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- epilogue of one tile: bf16 round, ghost-BN sums, 8-byte stores from the registers
+  auto epilogue = [&](int t) {
+    const int mt = t / ntn, nt = t - mt * ntn;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int rbase = m0 + wm * (BM / WM) + (lane & 15);
+    const int cbase = n0 + wn * (BN / WN) + 4 * (lane >> 4);
+    int g0 = 0, bnd = 0x7fffffff;
+    bool straddle = false;
+    if constexpr (STATS) {
+      g0 = m0 / g.group_rows;
+      bnd = (g0 + 1) * g.group_rows;
+      straddle = bnd < m0 + BM && bnd < g.M;
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int col = cbase + tn * 16;
+      const bool cok = col < g.N;
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+      float s2[4] = {0.f, 0.f, 0.f, 0.f}, ss2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = rbase + tm * 16;
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
+        const bool ok = row < g.M && cok;
+        const unsigned voff = ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PG_OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rs_o, voff, 0, 0);
+        if constexpr (STATS) {
+          const float mk = row < g.M ? 1.f : 0.f;
+          const float m1 = row < bnd ? mk : 0.f, m2 = mk - m1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float f = bf2f(o[j]);
+            s[j] += f * m1;
+            ss[j] += f * f * m1;
+            s2[j] += f * m2;
+            ss2[j] += f * f * m2;
+          }
+        }
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[j] = pg_row16_sum(s[j]);
+          ss[j] = pg_row16_sum(ss[j]);
+        }
+        if ((lane & 15) == 0 && cok) {
+          float* dst = g.stats + (size_t)g0 * 2 * g.stats_ld + col;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            atomicAdd(dst + j, s[j]);
+            atomicAdd(dst + g.stats_ld + j, ss[j]);
+          }
+        }
+        if (straddle) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s2[j] = pg_row16_sum(s2[j]);
+            ss2[j] = pg_row16_sum(ss2[j]);
+          }
+          if ((lane & 15) == 0 && cok) {
+            float* dst = g.stats + (size_t)(g0 + 1) * 2 * g.stats_ld + col;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              atomicAdd(dst + j, s2[j]);
+              atomicAdd(dst + g.stats_ld + j, ss2[j]);
+            }
+          }
+        }
+      }
+    }
+  };
+
+  // ---- prologue: steps 0 .. S-2 in flight, step 0's fragments in registers
+  int t_issue = t_begin, kt_issue = 0;                    // next step to issue
+  set_tile(t_issue);
+  auto issue_next = [&](int slot) {                       // issue step (t_issue, kt_issue)
+    issue(kt_issue, slot);
+    if (++kt_issue == KT) {
+      kt_issue = 0;
+      if (++t_issue < t_end) set_tile(t_issue);
+    }
+  };
+  const int pro_n = NS < S - 1 ? NS : S - 1;
+  for (int i = 0; i < pro_n; ++i) issue_next(i);
+  pg_wait_steps<P>(pro_n - 1);                            // step 0 landed
+  pg_bar();
+  bf16x8 fa[TM], fb[TN];
+  read_frags(fa, fb, 0);
+
+  constexpr int NM = TM * TN;
+  auto mma = [&](int i0, int i1) {
+#pragma unroll
+    for (int i = 0; i < NM; ++i)
+      if (i >= i0 && i < i1)
+        acc[i / TN][i % TN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i % TN], fa[i / TN],
+                                                                       acc[i / TN][i % TN], 0, 0, 0);
+  };
+
+  int t = t_begin, kt = 0, slot = 0;
+  for (int s = 0; s < NS; ++s) {
+    const bool more = s + 1 < NS;
+    mma(0, NM / 2);
+    if (more) {
+      // issued so far: steps 0 .. min(s + S - 2, NS - 1); newer than s + 1:
+      const int last = s + S - 2 < NS - 1 ? s + S - 2 : NS - 1;
+      pg_wait_steps<P>(last - (s + 1));
+      pg_bar();
+    }
+    mma(NM / 2, 3 * NM / 4);
+    if (s + S - 1 < NS) issue_next(slot == 0 ? S - 1 : slot - 1);   // slot of step s - 1
+    const int nslot = slot + 1 == S ? 0 : slot + 1;
+    bf16x8 na[TM], nb[TN];
+    read_frags(na, nb, nslot);
+    mma(3 * NM / 4, NM);
+    constexpr int NR = TM + TN;
+    constexpr int RPM = (NR + NM / 4 - 1) / (NM / 4);
+#pragma unroll
+    for (int i = 0; i < NM / 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, RPM, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
+    if (++kt == KT) {
+      epilogue(t);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      kt = 0;
+      ++t;
+    }
+    slot = nslot;
+  }
+}
+
+template <int BN, int WM, int S>
+constexpr int pg_lds_bytes() {
+  return S * (PG_BM + BN) * 64 + PG_NW * 1024;
+}
+
+template <int BN, int WM, int S, bool STATS, bool GATHER>
+void pg_launch_k(const PgemmArgs& g, int grid, hipStream_t st) {
+  constexpr int bytes = pg_lds_bytes<BN, WM, S>();
+  static_assert(bytes <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)pgemm_kernel<BN, WM, S, STATS, GATHER>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    attr = true;
+  }
+  hipLaunchKernelGGL((pgemm_kernel<BN, WM, S, STATS, GATHER>), dim3(grid), dim3(PG_NT), bytes, st, g);
+}
+
+template <int BN, int WM, int S>
+void pg_launch(const PgemmArgs& g, int grid, hipStream_t st) {
+  const bool stats = g.stats != nullptr, gather = g.stride != 1;
+  if (stats) {
+    if (gather) pg_launch_k<BN, WM, S, true, true>(g, grid, st);
+    else pg_launch_k<BN, WM, S, true, false>(g, grid, st);
+  } else {
+    if (gather) pg_launch_k<BN, WM, S, false, true>(g, grid, st);
+    else pg_launch_k<BN, WM, S, false, false>(g, grid, st);
+  }
+}
+
+int pg_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+}  // namespace
+
+// returns 0 when the shape / tile is not supported (caller falls back to igemm)
+int pgemm_launch(const PgemmArgs& g_in, int bn, int grid, hipStream_t st) {
+  PgemmArgs g = g_in;
+  if (g.K % 8 || g.N % 8 || g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
+  if (g.stats && g.group_rows < PG_BM) return 0;           // a tile straddles <= 1 group boundary
+  const int ntiles = ((g.M + PG_BM - 1) / PG_BM) * ((g.N + bn - 1) / bn);
+  if (grid <= 0) grid = pg_cus();
+  if (grid > ntiles) grid = ntiles;
+  switch (bn) {
+    case 256: pg_launch<256, 2, 4>(g, grid, st); return 1;
+    case 128: pg_launch<128, 4, 5>(g, grid, st); return 1;
+    case 64: pg_launch<64, 8, 6>(g, grid, st); return 1;
+    default: return 0;
+  }
+}

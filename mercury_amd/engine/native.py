@@ -105,6 +105,13 @@ class NativeEngine(object):
             elif comm != 'pg':
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
+        # the bucket all-reduces captured INSIDE the train graph (event fork onto the comm stream
+        # after each bucket's backward segment, one join before the tail): a DP step replays the
+        # same three graphs as a one-GPU step, no per-bucket host replays or host-issued
+        # collectives.  Timed (diagnostic) steps still run the segmented form so each bucket's
+        # all-reduce can be bracketed by events.  MERCURY_CAPTURE_COMM=0: segmented always.
+        self.capture_comm = self.s_comm is not None and \
+            os.environ.get('MERCURY_CAPTURE_COMM', '1') == '1'
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         if grad_compress not in (None, 'none', 'ternary'):
             raise ValueError("grad_compress must be None, 'none' or 'ternary'")
@@ -999,6 +1006,27 @@ class NativeEngine(object):
             fn()
         return g
 
+    def _train_dp_body(self):
+        """Train fwd + bwd with every bucket's all-reduce forked onto the comm stream right
+        after the backward segment that finishes it, and ONE join at the end -- the whole DP
+        train phase as a single capturable stream program (graph capture follows the event
+        fork / join, so RCCL's kernels become nodes of the train graph)."""
+        s0 = torch.cuda.current_stream(self.device)
+        nb = 0
+        for si, (fs, bucket) in enumerate(self.train_segments()):
+            for f in fs:
+                f()
+            if bucket is not None:
+                self._reduce_bucket(s0, bucket, nb, si)
+                nb += 1
+        if nb:
+            if self.check_order:
+                with torch.cuda.stream(self.s_comm):
+                    self._order(tick=1, at=2)
+            ev = torch.cuda.Event()
+            ev.record(self.s_comm)
+            s0.wait_event(ev)
+
     def build_graphs(self):
         torch.cuda.synchronize(self.device)
         cap = torch.cuda.Stream(self.device)
@@ -1011,6 +1039,8 @@ class NativeEngine(object):
         }
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
+        if self.dp and self.capture_comm:
+            self.graphs['train_dp'] = self._capture(self._train_dp_body, cap)
         self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
@@ -1064,6 +1094,10 @@ class NativeEngine(object):
         works = []
         segs = graphs['train'] if graphs else self.train_segments()
         nb = 0
+        if graphs and 'train_dp' in graphs and not T.on:
+            # DP train phase incl. every bucket all-reduce and the comm join: one replay
+            graphs['train_dp'].replay()
+            segs = []
         for si, (g, bucket) in enumerate(segs):
             if graphs:
                 g.replay()
@@ -1116,7 +1150,7 @@ class NativeEngine(object):
         s, e = bucket
         g = self.opt.g[s:e]
         if self.tern is not None:
-            self._tern_ctr += 1          # a fresh Philox stream per (step, bucket)
+            self._tern_ctr += 1          # a fresh Philox stream per (step, bucket) (host path)
         if self.s_comm is None:          # torch ProcessGroup (gloo / CPU tests)
             if self.tern is not None:
                 self.tern.allreduce(g, self._tern_ctr)
@@ -1136,8 +1170,9 @@ class NativeEngine(object):
                 self.xgmi.allreduce(g, avg=True)
             elif self.tern is not None:
                 # 2-bit stochastic ternary codes + one scale per rank, all-gathered (1/16 of
-                # the fp32 bytes), decoded to the same mean on every rank
-                self.tern.allreduce(g, self._tern_ctr)
+                # the fp32 bytes), decoded to the same mean on every rank; Philox stream =
+                # (device optimizer-step counter, bucket): fresh every replayed step
+                self.tern.allreduce(g, i, dctr=self.ctrl[2:3])
             elif self.wire_bf16:
                 # bf16 on the wire: half the bytes over xGMI; the sum is rounded once per hop
                 if self.wire is None:

@@ -217,6 +217,50 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     return out
 
 
+PGEMM_BM = 256
+
+
+def pgemm_ok(spec: ConvSpec):
+    """Can the persistent pointwise GEMM (csrc/pgemm.hip) run this conv?  1x1, no padding,
+    stride 1 or 2, channel counts multiples of 8, ghost-BN groups of >= one 256-row tile, and
+    enough output tiles to fill the GPU (small-M layers stay on igemm's split-K)."""
+    if spec.R != 1 or spec.S != 1 or spec.pad != 0 or spec.stride not in (1, 2):
+        return False
+    if spec.C % 8 or spec.K % 8:
+        return False
+    if spec.group_rows and spec.group_rows < spec.M and spec.group_rows < PGEMM_BM:
+        return False
+    return spec.M >= 16 * PGEMM_BM
+
+
+def pgemm_plan(spec: ConvSpec):
+    """Output-tile width of the pointwise GEMM: the widest of 256 / 128 / 64 that the output
+    channels fill (a 256-wide tile reads each activation row once for N <= 256)."""
+    if spec.K >= 256:
+        return 256
+    if spec.K > 64:
+        return 128
+    return 64
+
+
+def pgemm_fwd(x, w, out, spec: ConvSpec, stats=None, bn=None, grid=0):
+    """out[M][K] = conv1x1(x NHWC, w [K][Cp]) on the persistent LDS-DMA GEMM (+ BN sums)."""
+    if not pgemm_ok(spec) and not (spec.R == 1 and spec.pad == 0 and spec.stride in (1, 2)):
+        raise ValueError('pgemm: 1x1 pad-0 stride-1/2 convs only')
+    Cp = spec.Cp
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
+    _chk(w, torch.bfloat16, 'w', spec.K * Cp)
+    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    grp = spec.group_rows if spec.group_rows else spec.M
+    ok = lib().pgemm(ptr(x), ptr(w), ptr(out), ptr(stats), spec.M, spec.K, Cp, spec.K, spec.K,
+                     grp, x.numel() * 2, w.numel() * 2, out.numel() * 2, spec.H, spec.W, spec.P,
+                     spec.Q, spec.stride, bn or pgemm_plan(spec), int(grid), stream_ptr())
+    if not ok:
+        raise ValueError('pgemm: unsupported shape/tile %s bn=%s' % (spec, bn))
+    return out
+
+
 _NO_BW = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0)
 _ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
 

@@ -21,7 +21,7 @@ def tern_pack(x, words, ws, seed=0, counter=0):
     n = x.numel()
     _chk(words, torch.int32, 'words', 1 + (n + 15) // 16)
     lib().tern_pack(ptr(x), n, ptr(ws), int(seed) & 0xffffffff, int(counter), ptr(words),
-                    stream_ptr())
+                    stream_ptr(), 0)
     return words
 
 

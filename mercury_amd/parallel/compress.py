@@ -78,7 +78,10 @@ class TernaryAllReduce(object):
         self.ws = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.gen = torch.Generator().manual_seed(self.seed)
 
-    def allreduce(self, g, counter):
+    def allreduce(self, g, counter, dctr=None):
+        """``counter``: the Philox stream of this (step, bucket).  ``dctr`` (GPU path, graph
+        capture): an int64 device step counter -- the stream is then (dctr[0], counter), read
+        at replay time, and ``counter`` is just the bucket index."""
         n = g.numel()
         nw = tern_words(n)
         if nw > self.send.numel():
@@ -87,7 +90,8 @@ class TernaryAllReduce(object):
             from ..ops import lib, ptr, stream_ptr
             L, st = lib(), stream_ptr()
             send, recv = self.send[:nw], self.recv[:self.size * nw]
-            L.tern_pack(ptr(g), n, ptr(self.ws), self.seed, int(counter), ptr(send), st)
+            L.tern_pack(ptr(g), n, ptr(self.ws), self.seed, int(counter), ptr(send), st,
+                        ptr(dctr) if dctr is not None else 0)
             self.comm.all_gather(recv, send)
             L.tern_unpack(ptr(recv), self.size, n, 1.0 / self.size, ptr(g), st)
             return g

@@ -141,9 +141,15 @@ def test_native_rccl_buckets_world1():
         runs = {'rccl': _engine(x, y, force_buckets=True, comm='rccl', check_order=True,
                                 exchange_scores=True),
                 'pg': _engine(x, y, force_buckets=True, comm='pg', check_order=True),
-                'bf16': _engine(x, y, force_buckets=True, comm='rccl', wire_bf16=True)}
+                'bf16': _engine(x, y, force_buckets=True, comm='rccl', wire_bf16=True),
+                'xgmi': _engine(x, y, force_buckets=True, comm='xgmi'),
+                'tern': _engine(x, y, force_buckets=True, comm='rccl', grad_compress='ternary')}
         e = runs['rccl']
         assert e.comm is not None and e.comm.size == 1 and len(e.bucket_plan()) > 1
+        # the untimed DP step is ONE captured train graph with the all-reduces inside it
+        for name in ('rccl', 'bf16', 'xgmi', 'tern'):
+            assert 'train_dp' in runs[name].graphs, name
+        assert 'train_dp' not in runs['pg'].graphs
         for _ in range(6):
             base.step()
             for r in runs.values():
@@ -157,8 +163,8 @@ def test_native_rccl_buckets_world1():
         assert ph['comm'] > 0 and ph['step'] > 0 and 0.0 <= ph['overlap'] <= 1.0
         assert abs(ph['critical'] - ph['step']) <= 0.1 * ph['step'] + 0.05, ph
         base.step()
-        runs['pg'].step()
-        runs['bf16'].step()
+        for name in ('pg', 'bf16', 'xgmi', 'tern'):
+            runs[name].step()
         torch.cuda.synchronize()
         for name in ('rccl', 'pg'):
             n, first = runs[name].order_violations()
@@ -166,6 +172,8 @@ def test_native_rccl_buckets_world1():
         g = e.score_exchange.wait()
         torch.cuda.synchronize()
         assert torch.equal(g[0], e.score_mode.losses.reshape(-1))
+        tern = runs.pop('tern')          # lossy wire: finite, not close
+        assert torch.isfinite(tern.opt.p).all()
         for name, r in runs.items():
             # atomics make the steps non-bitwise-reproducible; Adam moves each weight by at
             # most a few lr per step (bias-corrected early steps), so 8 steps stay well below 5e-2
