@@ -20,6 +20,9 @@ jobs
   ab-kernel --old OLD.so --args CMD  ... on a microbenchmark (bench/pool_bench.py, ...)
   sweep                              graph-timed conv plan sweeps (igemm and halo conv)
   learn                              learning check of the ResNet-50/224 preset
+  multi     --args 'CMD1 ;; CMD2 ...'  ad-hoc steps, each a child under its own limit
+                                     (--limit s); a plain test failure (rc 1) continues,
+                                     a crash / abort / fault / time limit stops the job
 """
 from __future__ import annotations
 
@@ -207,7 +210,17 @@ def job_learn(o, a):
     tail(out, 1)
 
 
-JOBS = {'tests': job_tests, 'bench': job_bench, 'session': job_session, 'trace': job_trace,
+def job_multi(o, a):
+    for i, c in enumerate([c.strip() for c in (a.args or '').split(';;') if c.strip()]):
+        out = os.path.join(o, 'step%d.log' % i)
+        argv = shlex.split(c)
+        if argv and argv[0] in ('python', 'python3'):
+            argv[0] = PY
+        run(argv, out, a.limit, ok_codes=(0, 1))
+        tail(out, 4)
+
+
+JOBS = {'multi': job_multi, 'tests': job_tests, 'bench': job_bench, 'session': job_session, 'trace': job_trace,
         'pmc': job_pmc, 'presets': job_presets, 'ab': job_ab, 'ab-ext': job_ab_ext,
         'sweep': job_sweep, 'learn': job_learn, 'ab-preset': job_ab_preset,
         'ab-kernel': job_ab_kernel}
@@ -223,6 +236,7 @@ def main():
     ap.add_argument('--env', nargs='*')
     ap.add_argument('--old', default='')
     ap.add_argument('--rounds', type=int, default=2)
+    ap.add_argument('--limit', type=int, default=400)
     a = ap.parse_args()
     o = os.path.join(ROOT, 'gpurun_out', '%s_%s' % (a.job, a.tag))
     os.makedirs(o, exist_ok=True)

@@ -148,18 +148,17 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
       boff[j] = (n < g.N && nr < BN) ? (unsigned)((n * g.K + lc * 8) * 2) : PG_OOB;
     }
   };
-  auto issue = [&](int kt, int slot) {
+  // DMA piece q (0 .. P-1) of K-step kt into ring slot `slot`: A pieces first, then B
+  auto issue_piece = [&](int q, int kt, int slot) {
     const unsigned kb = (unsigned)(kt * 64);
     const bool kok = kfull || kt * 4 + lc < K8;
     const unsigned sa = s_ring + slot * SLOT, sb = sa + SA;
-#pragma unroll
-    for (int j = 0; j < PA; ++j)
-      pg_dma16(rs_a, kok ? aoff[j] + kb : PG_OOB, sa + 16 * (wu + PG_NW * j) * 64);
-#pragma unroll
-    for (int j = 0; j < PB; ++j) {
+    if (q < PA) {
+      pg_dma16(rs_a, kok ? aoff[q] + kb : PG_OOB, sa + 16 * (wu + PG_NW * q) * 64);
+    } else {
+      const int j = q - PA;
       const bool real = 16 * (wu + PG_NW * j) < BN;
-      pg_dma16(rs_b, kok ? boff[j] + kb : PG_OOB,
-               real ? sb + 16 * (wu + PG_NW * j) * 64 : s_dump);
+      pg_dma16(rs_b, kok ? boff[j] + kb : PG_OOB, real ? sb + 16 * (wu + PG_NW * j) * 64 : s_dump);
     }
   };
 
@@ -182,7 +181,56 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- epilogue of one tile: bf16 round, ghost-BN sums, 8-byte stores from the registers
+  // ---- ghost-BN statistics.  Per-lane partial sums (over this lane's pixel rows) are reduced
+  // over the 16 pixel lanes by DPP, over the WM wave rows through LDS, and land as ONE atomic
+  // pair per (channel, flush): the stat addresses are shared by every block, so per-wave atomics
+  // serialised on them (measured: 8 wave rows x 15680 tiles on 5120 addresses dominated the
+  // K = 64 convs).  With a single N-tile the block keeps RUNNING sums across its consecutive
+  // tiles and flushes only when the statistics group changes (contiguous tile ranges: a few
+  // flushes per block).
+  float* red = (float*)(smem + S * SLOT + PG_NW * 1024);   // [WM][2][BN]
+  const bool run = STATS && ntn == 1;
+  float rs[TN][4], rss[TN][4];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rs[tn][j] = rss[tn][j] = 0.f;
+  int rgrp = -1;
+  auto flush = [&](int grp, int n0) {
+    // rs / rss: per-lane partials of group grp, columns n0 + (this wave's) -> stats, then zero
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rs[tn][j] = pg_row16_sum(rs[tn][j]);
+        rss[tn][j] = pg_row16_sum(rss[tn][j]);
+      }
+      if ((lane & 15) == 0) {
+        const int cl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+        *(f32x4*)(red + (wm * 2) * BN + cl) = f32x4{rs[tn][0], rs[tn][1], rs[tn][2], rs[tn][3]};
+        *(f32x4*)(red + (wm * 2 + 1) * BN + cl) = f32x4{rss[tn][0], rss[tn][1], rss[tn][2], rss[tn][3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rs[tn][j] = rss[tn][j] = 0.f;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (tid < BN && n0 + tid < g.N) {
+      float a = 0.f, c = 0.f;
+#pragma unroll
+      for (int q = 0; q < WM; ++q) {
+        a += red[(q * 2) * BN + tid];
+        c += red[(q * 2 + 1) * BN + tid];
+      }
+      float* dst = g.stats + (size_t)grp * 2 * g.stats_ld + n0 + tid;
+      atomicAdd(dst, a);
+      atomicAdd(dst + g.stats_ld, c);
+    }
+    // the red area is rewritten no earlier than the next flush: a second flush in the same
+    // epilogue (straddling tile) waits for these reads
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  // ---- epilogue of one tile: bf16 round, 8-byte stores from the registers, statistics
   auto epilogue = [&](int t) {
     const int mt = t / ntn, nt = t - mt * ntn;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -194,13 +242,16 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
       g0 = m0 / g.group_rows;
       bnd = (g0 + 1) * g.group_rows;
       straddle = bnd < m0 + BM && bnd < g.M;
+      if (run && rgrp != g0) {
+        if (rgrp >= 0) flush(rgrp, n0);
+        rgrp = g0;
+      }
     }
+    // rows < bnd of this tile (all rows unless it straddles a group edge)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int col = cbase + tn * 16;
       const bool cok = col < g.N;
-      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
-      float s2[4] = {0.f, 0.f, 0.f, 0.f}, ss2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int row = rbase + tm * 16;
@@ -211,47 +262,35 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
         const unsigned voff = ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PG_OOB;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rs_o, voff, 0, 0);
         if constexpr (STATS) {
-          const float mk = row < g.M ? 1.f : 0.f;
-          const float m1 = row < bnd ? mk : 0.f, m2 = mk - m1;
+          const float mk = row < g.M && row < bnd ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]);
-            s[j] += f * m1;
-            ss[j] += f * f * m1;
-            s2[j] += f * m2;
-            ss2[j] += f * f * m2;
+            const float f = bf2f(o[j]) * mk;
+            rs[tn][j] += f;
+            rss[tn][j] += f * f;
           }
         }
       }
-      if constexpr (STATS) {
+    }
+    if constexpr (STATS) {
+      if (straddle || !run) flush(g0, n0);
+      if (straddle) {
+        // rows >= bnd: the next group (a tile straddles at most one edge: groups >= BM rows)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s[j] = pg_row16_sum(s[j]);
-          ss[j] = pg_row16_sum(ss[j]);
-        }
-        if ((lane & 15) == 0 && cok) {
-          float* dst = g.stats + (size_t)g0 * 2 * g.stats_ld + col;
+        for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            atomicAdd(dst + j, s[j]);
-            atomicAdd(dst + g.stats_ld + j, ss[j]);
-          }
-        }
-        if (straddle) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s2[j] = pg_row16_sum(s2[j]);
-            ss2[j] = pg_row16_sum(ss2[j]);
-          }
-          if ((lane & 15) == 0 && cok) {
-            float* dst = g.stats + (size_t)(g0 + 1) * 2 * g.stats_ld + col;
+          for (int tm = 0; tm < TM; ++tm) {
+            const int row = rbase + tm * 16;
+            const float mk = row < g.M && row >= bnd ? 1.f : 0.f;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              atomicAdd(dst + j, s2[j]);
-              atomicAdd(dst + g.stats_ld + j, ss2[j]);
+              const float f = bf2f(f2bf(acc[tm][tn][j])) * mk;
+              rs[tn][j] += f;
+              rss[tn][j] += f * f;
             }
           }
-        }
+        if (run) rgrp = g0 + 1;
+        else flush(g0 + 1, n0);
       }
     }
   };
@@ -259,15 +298,18 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
   // ---- prologue: steps 0 .. S-2 in flight, step 0's fragments in registers
   int t_issue = t_begin, kt_issue = 0;                    // next step to issue
   set_tile(t_issue);
-  auto issue_next = [&](int slot) {                       // issue step (t_issue, kt_issue)
-    issue(kt_issue, slot);
+  auto advance_issue = [&]() {
     if (++kt_issue == KT) {
       kt_issue = 0;
       if (++t_issue < t_end) set_tile(t_issue);
     }
   };
   const int pro_n = NS < S - 1 ? NS : S - 1;
-  for (int i = 0; i < pro_n; ++i) issue_next(i);
+  for (int i = 0; i < pro_n; ++i) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) issue_piece(q, kt_issue, i);
+    advance_issue();
+  }
   pg_wait_steps<P>(pro_n - 1);                            // step 0 landed
   pg_bar();
   bf16x8 fa[TM], fb[TN];
@@ -281,27 +323,39 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
         acc[i / TN][i % TN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i % TN], fa[i / TN],
                                                                        acc[i / TN][i % TN], 0, 0, 0);
   };
+  // step s: MFMAs [0, H1) -- wait for step s + 1 + barrier -- the P DMA pieces of step
+  // s + S - 1, each behind a share of MFMAs [H1, H2) -- step s + 1's fragment reads interleaved
+  // with MFMAs [H2, NM)
+  constexpr int H1 = NM / 2, H2 = NM * 3 / 4;
+  constexpr int DQ = (H2 - H1 + P - 1) / P;
 
   int t = t_begin, kt = 0, slot = 0;
   for (int s = 0; s < NS; ++s) {
     const bool more = s + 1 < NS;
-    mma(0, NM / 2);
+    mma(0, H1);
     if (more) {
       // issued so far: steps 0 .. min(s + S - 2, NS - 1); newer than s + 1:
       const int last = s + S - 2 < NS - 1 ? s + S - 2 : NS - 1;
       pg_wait_steps<P>(last - (s + 1));
       pg_bar();
     }
-    mma(NM / 2, 3 * NM / 4);
-    if (s + S - 1 < NS) issue_next(slot == 0 ? S - 1 : slot - 1);   // slot of step s - 1
+    const bool iss = s + S - 1 < NS;
+    const int islot = slot == 0 ? S - 1 : slot - 1;      // slot of step s - 1, free now
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      if (iss) issue_piece(q, kt_issue, islot);
+      mma(H1 + q * DQ, H1 + (q + 1) * DQ < H2 ? H1 + (q + 1) * DQ : H2);
+    }
+    if (iss) advance_issue();
     const int nslot = slot + 1 == S ? 0 : slot + 1;
     bf16x8 na[TM], nb[TN];
     read_frags(na, nb, nslot);
-    mma(3 * NM / 4, NM);
+    mma(H2, NM);
     constexpr int NR = TM + TN;
-    constexpr int RPM = (NR + NM / 4 - 1) / (NM / 4);
+    constexpr int NL = NM - H2;
+    constexpr int RPM = (NR + NL - 1) / NL;
 #pragma unroll
-    for (int i = 0; i < NM / 4; ++i) {
+    for (int i = 0; i < NL; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x100, RPM, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
@@ -320,11 +374,14 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
     }
     slot = nslot;
   }
+  if constexpr (STATS) {
+    if (run && rgrp >= 0) flush(rgrp, 0);
+  }
 }
 
 template <int BN, int WM, int S>
 constexpr int pg_lds_bytes() {
-  return S * (PG_BM + BN) * 64 + PG_NW * 1024;
+  return S * (PG_BM + BN) * 64 + PG_NW * 1024 + WM * 2 * BN * 4;   // ring, DMA sink, stat rows
 }
 
 template <int BN, int WM, int S, bool STATS, bool GATHER>

@@ -49,22 +49,21 @@ MA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
 
 MA_DEV f32x4 ld4(__amdgpu_buffer_rsrc_t r, long long i, bool bf) {
   if (!bf) return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, SYS));
+  // bf16 -> f32 by integer shifts (bf16x2 bit-casts of the loaded dwords miscompiled: hipcc
+  // dropped the second dword and loaded 4 bytes)
   const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, SYS);
-  const bf16x2 lo = __builtin_bit_cast(bf16x2, v[0]), hi = __builtin_bit_cast(bf16x2, v[1]);
-  return f32x4{bf2f(lo[0]), bf2f(lo[1]), bf2f(hi[0]), bf2f(hi[1])};
+  return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
+               __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u)};
 }
+
+MA_DEV unsigned bf16_bits(float x) { return (unsigned)__builtin_bit_cast(unsigned short, f2bf(x)); }
 
 MA_DEV void st4(__amdgpu_buffer_rsrc_t r, long long i, f32x4 v, bool bf) {
   if (!bf) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(i * 16), 0, SYS);
     return;
   }
-  bf16x2 lo, hi;
-  lo[0] = f2bf(v[0]);
-  lo[1] = f2bf(v[1]);
-  hi[0] = f2bf(v[2]);
-  hi[1] = f2bf(v[3]);
-  const u32x2_t o{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
+  const u32x2_t o{bf16_bits(v[0]) | (bf16_bits(v[1]) << 16), bf16_bits(v[2]) | (bf16_bits(v[3]) << 16)};
   __builtin_amdgcn_raw_buffer_store_b64(o, r, (int)(i * 8), 0, SYS);
 }
 
