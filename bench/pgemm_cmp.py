@@ -36,6 +36,9 @@ def main():
     ap.add_argument('--batch', type=int, default=0)
     ap.add_argument('--group', type=int, default=32)
     ap.add_argument('--models', default='r50,mbv2')
+    ap.add_argument('--pro', action='store_true',
+                    help='also time the input-BN prologue (pgemm pro=, modes 1 and 2) against '
+                         'the bn_apply pass + igemm the engine runs without it')
     a = ap.parse_args()
     import torch
     from mercury_amd import ops
@@ -67,6 +70,28 @@ def main():
             for bn in (64, 128, 256):
                 put('pgemm%d' % bn, gtime(lambda: ops.pgemm_fwd(x, w, y, sp, stats=stats, bn=bn),
                                           reps=4))
+            if a.pro and st == 1:
+                rows = batch * H * H
+                gamma = torch.ones(C, device=dev)
+                beta = torch.zeros(C, device=dev)
+                pst = torch.rand(G * 2 * C, device=dev) * 100 + 1
+                coef = torch.zeros(G * 2 * C, device=dev)
+                act_buf = torch.empty_like(x)
+                res = torch.randn(rows * sp.Cp, device=dev).to(torch.bfloat16)
+                grp = a.group * H * H
+                for mode, r in ((1, None), (2, res)):
+                    pro = dict(stats=pst, gamma=gamma, beta=beta, act='relu', coef=coef,
+                               group_rows=grp, count=grp, res=r, keep=act_buf)
+
+                    def fused():
+                        ops.pgemm_fwd(x, w, y, sp, stats=stats, pro=pro)
+
+                    def unfused():
+                        ops.bn_apply(x, pst, gamma, beta, act_buf, rows, C, group_rows=grp,
+                                     act='relu', res=r)
+                        ops.conv_fwd(act_buf, w, y, sp, stats=stats, slab=slab, plan=plan)
+                    put('pro%d' % mode, gtime(fused, reps=4))
+                    put('bn%d_igemm' % mode, gtime(unfused, reps=4))
             if st == 1:
                 xa, wt, ya = x.view(sp.M, C), w.view(K, C).t(), y.view(sp.M, K)
                 put('matmul', gtime(lambda: torch.matmul(xa, wt, out=ya), reps=4))

@@ -77,14 +77,23 @@ PYBIND11_MODULE(_C, m) {
   m.def("pgemm", [](uintptr_t a, uintptr_t b, uintptr_t out, uintptr_t stats, int M, int N, int K,
                     int ldo, int stats_ld, int group_rows, long long a_bytes, long long b_bytes,
                     long long out_bytes, int H, int W, int Pp, int Q, int stride, int bn, int grid,
-                    uintptr_t st) {
+                    uintptr_t st, int p_mode, uintptr_t p_stats, uintptr_t p_rmean,
+                    uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, float p_inv_count,
+                    float p_eps, int p_act, int p_group_rows, int p_G, uintptr_t p_coef,
+                    uintptr_t p_res, uintptr_t p_keep, long long p_res_bytes,
+                    long long p_keep_bytes, long long p_coef_bytes) {
     const long long lim = 0xFFFFFF00LL;
-    if (a_bytes >= lim || b_bytes >= lim || out_bytes >= lim)
+    if (a_bytes >= lim || b_bytes >= lim || out_bytes >= lim || p_res_bytes >= lim ||
+        p_keep_bytes >= lim || p_coef_bytes >= lim)
       throw std::invalid_argument("pgemm: tensors must be < 4 GB (32-bit buffer offsets)");
     PgemmArgs g{P<const bf16>(a), P<const bf16>(b), P<bf16>(out), P<float>(stats), M, N, K, ldo,
                 stats_ld, group_rows, (unsigned)a_bytes, (unsigned)b_bytes, (unsigned)out_bytes,
                 H, W, Pp, Q, stride};
-    const int ok = pgemm_launch(g, bn, grid, S(st));
+    PgemmPro pr{p_mode, P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
+                P<const float>(p_gamma), P<const float>(p_beta), p_inv_count, p_eps, p_act,
+                p_group_rows, p_G, P<float>(p_coef), P<const bf16>(p_res), P<bf16>(p_keep),
+                (unsigned)p_res_bytes, (unsigned)p_keep_bytes, (unsigned)p_coef_bytes};
+    const int ok = pgemm_launch(g, bn, grid, S(st), &pr);
     check_launch("pgemm");
     return ok;
   });

@@ -141,8 +141,29 @@ struct PgemmArgs {
   unsigned a_bytes, b_bytes, out_bytes;   // buffer-resource ranges (< 4 GB)
   int H, W, P, Q, stride;
 };
+// Input prologue of the pointwise GEMM: A = act(bn(y) [+ res]) applied in LDS to each
+// operand tile as it lands (once per tile, by the thread whose DMA brought it), from per-group
+// scale / shift coefficients that a small kernel derives from the producer's statistics into
+// ``coef`` ([G][2][K], launched by pgemm_launch).  ``keep`` (optional) receives the activation:
+// the N-tile-0 tiles write each transformed chunk once.  Stride-1 convs only.
+struct PgemmPro {
+  int mode;                // 0 none, 1 act(bn(y)), 2 act(bn(y) + res)
+  const float* stats;      // [G][2][K] producer sums (sum, sumsq) per group, or null: running
+  const float* rmean;
+  const float* rvar;
+  const float* gamma;
+  const float* beta;
+  float inv_count, eps;
+  int act;                 // 0 none, 1 relu, 2 relu6
+  int group_rows;          // input rows per statistics group (>= 256, or the whole batch)
+  int G;                   // statistics groups (1 with running statistics)
+  float* coef;             // workspace [G][2][K]
+  const bf16* res;         // mode 2: residual [rows][K]
+  bf16* keep;              // optional activation output [rows][K]
+  unsigned res_bytes, keep_bytes, coef_bytes;
+};
 // bn in {64, 128, 256}; grid <= 0: one block per CU.  Returns 0 when unsupported.
-int pgemm_launch(const PgemmArgs& g, int bn, int grid, hipStream_t st);
+int pgemm_launch(const PgemmArgs& g, int bn, int grid, hipStream_t st, const PgemmPro* pro = nullptr);
 
 int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                  const HconvPro& pro, int bm, int bn, int splits, hipStream_t st);

@@ -90,14 +90,19 @@ MA_DEV void pg_wait_steps(int newer) {
   }
 }
 
-template <int BN, int WM, int S, bool STATS, bool GATHER>
-__global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
+template <int BN, int WM, int S, bool STATS, bool GATHER, int MODE>
+__global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro pro) {
   constexpr int BM = PG_BM, WN = PG_NW / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr int PA = BM / 16 / PG_NW;                     // A pieces per wave per step
   constexpr int PB = BN >= 128 ? BN / 16 / PG_NW : 1;     // B pieces (BN = 64: waves 4-7 dump)
-  constexpr int P = PA + PB;
-  constexpr int SA = BM * 64, SB = BN * 64, SLOT = SA + SB;
+  // MODE > 0: + one coefficient piece per wave (its own copy: read after its own vmcnt, no
+  // barrier), MODE 2: + the residual tile's pieces
+  constexpr int PC = MODE > 0 ? 1 : 0, PR = MODE == 2 ? PA : 0;
+  constexpr int P = PA + PB + PC + PR;
+  constexpr int SA = BM * 64, SB = BN * 64, SC = PC * PG_NW * 1024, SR = PR ? SA : 0;
+  constexpr int SLOT = SA + SB + SC + SR;
+  static_assert(!(GATHER && MODE), "input prologue: stride-1 convs only");
   static_assert(TM >= 1 && TN >= 1 && PA >= 1, "tile shape");
   static_assert(S >= 3 && S <= 6, "ring depth (pg_wait_steps covers newer <= 4)");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -120,6 +125,7 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
   const auto rs_o = pg_rsrc(g.out, g.out_bytes);
   const unsigned s_ring = pg_lds_addr(smem);
   const unsigned s_dump = s_ring + S * SLOT + wu * 1024;
+  (void)SR;
 
   // ---- DMA lane roles: piece row (lane >> 2), physical chunk (lane & 3), logical chunk lc
   const int prow = lane >> 2;
@@ -127,8 +133,20 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
   const bool kfull = (g.K & 31) == 0;
   const int K8 = g.K >> 3;                                // 16-byte chunks per row
   unsigned aoff[PA], boff[PB];                            // per tile: row byte offset + lc
+  unsigned coff = PG_OOB;                                 // MODE > 0: this lane's coef source
+  const auto rs_c = pg_rsrc(pro.coef, pro.coef_bytes);
+  const auto rs_r = pg_rsrc(pro.res, pro.res_bytes);
+  const auto rs_k = pg_rsrc(pro.keep, pro.keep_bytes);
   auto set_tile = [&](int t) {
     const int mt = t / ntn, nt = t - mt * ntn;
+    if constexpr (MODE > 0) {
+      // lanes 0-7 scale, 8-15 shift of the tile's first group; 16-31 the same for the next
+      // group (a tile straddles at most one group edge); channel offset added per step
+      const int gq = (mt * BM) / pro.group_rows + ((lane >> 4) & 1);
+      const int which = (lane >> 3) & 1;
+      coff = (lane < 32 && gq < pro.G) ? (unsigned)(((gq * 2 + which) * g.K + 4 * (lane & 7)) * 4)
+                                       : PG_OOB;
+    }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int m = mt * BM + 16 * (wu + PG_NW * j) + prow;
@@ -155,10 +173,63 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
     const unsigned sa = s_ring + slot * SLOT, sb = sa + SA;
     if (q < PA) {
       pg_dma16(rs_a, kok ? aoff[q] + kb : PG_OOB, sa + 16 * (wu + PG_NW * q) * 64);
-    } else {
+    } else if (q < PA + PB) {
       const int j = q - PA;
       const bool real = 16 * (wu + PG_NW * j) < BN;
       pg_dma16(rs_b, kok ? boff[j] + kb : PG_OOB, real ? sb + 16 * (wu + PG_NW * j) * 64 : s_dump);
+    } else if (q < PA + PB + PC) {
+      // 32 channels of this step: 128 B of scale / shift per group (channels past K: zeros)
+      const bool cok = kt * 32 + 4 * (lane & 7) < g.K;
+      pg_dma16(rs_c, coff != PG_OOB && cok ? coff + (unsigned)(kt * 128) : PG_OOB,
+               sa + SA + SB + wu * 1024);
+    } else {
+      const int j = q - PA - PB - PC;
+      pg_dma16(rs_r, kok ? aoff[j] + kb : PG_OOB, sa + SA + SB + SC + 16 * (wu + PG_NW * j) * 64);
+    }
+  };
+
+  // ---- MODE > 0: normalise this thread's own landed A chunks of a step in place (after its
+  // own vmcnt wait, before the barrier that publishes the step): a = act(y * scale + shift
+  // [+ res]); N-tile-0 tiles also write the activation to ``keep``
+  float clo = 0.f, chi = 0.f;
+  if constexpr (MODE > 0) {
+    clo = pro.act == 0 ? __builtin_nanf("") : 0.f;          // NaN bounds: identity, keeps NaN
+    chi = pro.act == 2 ? 6.f : (pro.act == 0 ? __builtin_nanf("") : __builtin_huge_valf());
+  }
+  auto transform = [&](int tt, int ktt, int sl) {
+    if constexpr (MODE > 0) {
+      const int mt = tt / ntn, nt = tt - mt * ntn;
+      const int m0 = mt * BM;
+      const int bnd = (m0 / pro.group_rows + 1) * pro.group_rows;
+      char* sa = smem + sl * SLOT;
+      const char* cw = sa + SA + SB + wu * 1024;
+#pragma unroll
+      for (int j = 0; j < PA; ++j) {
+        const int row = m0 + 16 * (wu + PG_NW * j) + prow;
+        const int gs = row >= bnd ? 256 : 0;
+        const f32x4 c0 = *(const f32x4*)(cw + gs + lc * 32), c1 = *(const f32x4*)(cw + gs + lc * 32 + 16);
+        const f32x4 h0 = *(const f32x4*)(cw + gs + 128 + lc * 32),
+                    h1 = *(const f32x4*)(cw + gs + 128 + lc * 32 + 16);
+        u32x4* ap = (u32x4*)(sa + 16 * (wu + PG_NW * j) * 64 + lane * 16);
+        const bf16x8 y = __builtin_bit_cast(bf16x8, *ap);
+        bf16x8 r8;
+        if constexpr (MODE == 2)
+          r8 = __builtin_bit_cast(bf16x8, *(const u32x4*)(sa + SA + SB + SC + 16 * (wu + PG_NW * j) * 64 + lane * 16));
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = bf2f(y[k]) * (k < 4 ? c0[k] : c1[k - 4]) + (k < 4 ? h0[k] : h1[k - 4]);
+          if constexpr (MODE == 2) v += bf2f(r8[k]);
+          o[k] = f2bf(fminf(fmaxf(v, clo), chi));
+        }
+        const u32x4 ov = __builtin_bit_cast(u32x4, o);
+        *ap = ov;
+        if (pro.keep != nullptr && nt == 0) {
+          const bool ok = row < g.M && (kfull || ktt * 4 + lc < K8);
+          const unsigned ko = ok ? (unsigned)(((long long)row * g.K + ktt * 32 + lc * 8) * 2) : PG_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(ov, rs_k, ko, 0, 0);
+        }
+      }
     }
   };
 
@@ -311,7 +382,14 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
     advance_issue();
   }
   pg_wait_steps<P>(pro_n - 1);                            // step 0 landed
-  pg_bar();
+  int t_x = t_begin, kt_x = 0;                            // step the next transform handles
+  transform(t_x, kt_x, 0);
+  auto advance_x = [&]() {
+    if (++kt_x == KT) kt_x = 0, ++t_x;
+  };
+  advance_x();
+  if constexpr (MODE > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else pg_bar();
   bf16x8 fa[TM], fb[TN];
   read_frags(fa, fb, 0);
 
@@ -337,7 +415,13 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
       // issued so far: steps 0 .. min(s + S - 2, NS - 1); newer than s + 1:
       const int last = s + S - 2 < NS - 1 ? s + S - 2 : NS - 1;
       pg_wait_steps<P>(last - (s + 1));
-      pg_bar();
+      if constexpr (MODE > 0) {
+        transform(t_x, kt_x, slot + 1 == S ? 0 : slot + 1);   // step s + 1, before publishing
+        advance_x();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        pg_bar();
+      }
     }
     const bool iss = s + S - 1 < NS;
     const int islot = slot == 0 ? S - 1 : slot - 1;      // slot of step s - 1, free now
@@ -379,34 +463,74 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g) {
   }
 }
 
-template <int BN, int WM, int S>
+template <int BN, int WM, int S, int MODE>
 constexpr int pg_lds_bytes() {
-  return S * (PG_BM + BN) * 64 + PG_NW * 1024 + WM * 2 * BN * 4;   // ring, DMA sink, stat rows
+  // ring (A, B, per-wave coefficient copies, residual), DMA sink, statistics rows
+  constexpr int slot = (PG_BM + BN) * 64 + (MODE > 0 ? PG_NW * 1024 : 0) + (MODE == 2 ? PG_BM * 64 : 0);
+  return S * slot + PG_NW * 1024 + WM * 2 * BN * 4;
 }
 
-template <int BN, int WM, int S, bool STATS, bool GATHER>
-void pg_launch_k(const PgemmArgs& g, int grid, hipStream_t st) {
-  constexpr int bytes = pg_lds_bytes<BN, WM, S>();
+template <int BN, int WM, int S, bool STATS, bool GATHER, int MODE>
+void pg_launch_k(const PgemmArgs& g, const PgemmPro& pro, int grid, hipStream_t st) {
+  constexpr int bytes = pg_lds_bytes<BN, WM, S, MODE>();
   static_assert(bytes <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)pgemm_kernel<BN, WM, S, STATS, GATHER>,
+    (void)hipFuncSetAttribute((const void*)pgemm_kernel<BN, WM, S, STATS, GATHER, MODE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     attr = true;
   }
-  hipLaunchKernelGGL((pgemm_kernel<BN, WM, S, STATS, GATHER>), dim3(grid), dim3(PG_NT), bytes, st, g);
+  hipLaunchKernelGGL((pgemm_kernel<BN, WM, S, STATS, GATHER, MODE>), dim3(grid), dim3(PG_NT), bytes,
+                     st, g, pro);
 }
 
-template <int BN, int WM, int S>
-void pg_launch(const PgemmArgs& g, int grid, hipStream_t st) {
+// ring depth per (tile width, prologue mode): the deepest that fits 160 KB
+template <int BN, int WM, int S0, int S1, int S2>
+int pg_launch(const PgemmArgs& g, const PgemmPro& pro, int grid, hipStream_t st) {
   const bool stats = g.stats != nullptr, gather = g.stride != 1;
-  if (stats) {
-    if (gather) pg_launch_k<BN, WM, S, true, true>(g, grid, st);
-    else pg_launch_k<BN, WM, S, true, false>(g, grid, st);
-  } else {
-    if (gather) pg_launch_k<BN, WM, S, false, true>(g, grid, st);
-    else pg_launch_k<BN, WM, S, false, false>(g, grid, st);
+  if (pro.mode == 0) {
+    if (stats) {
+      if (gather) pg_launch_k<BN, WM, S0, true, true, 0>(g, pro, grid, st);
+      else pg_launch_k<BN, WM, S0, true, false, 0>(g, pro, grid, st);
+    } else {
+      if (gather) pg_launch_k<BN, WM, S0, false, true, 0>(g, pro, grid, st);
+      else pg_launch_k<BN, WM, S0, false, false, 0>(g, pro, grid, st);
+    }
+    return 1;
   }
+  if (gather) return 0;
+  if (pro.mode == 1) {
+    if (stats) pg_launch_k<BN, WM, S1, true, false, 1>(g, pro, grid, st);
+    else pg_launch_k<BN, WM, S1, false, false, 1>(g, pro, grid, st);
+    return 1;
+  }
+  if constexpr (S2 > 0) {
+    if (pro.mode == 2) {
+      if (stats) pg_launch_k<BN, WM, S2, true, false, 2>(g, pro, grid, st);
+      else pg_launch_k<BN, WM, S2, false, false, 2>(g, pro, grid, st);
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// coef[g][0][c] = gamma * rsqrt(var + eps), coef[g][1][c] = beta - mean * scale, from the
+// producer's per-group sums (same arithmetic as bn.hip) or its running statistics
+__global__ __launch_bounds__(256) void pg_coef_kernel(PgemmPro p, int K) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.G * K) return;
+  const int gi = i / K, c = i - gi * K;
+  float mean, var;
+  if (p.stats) {
+    mean = p.stats[(size_t)gi * 2 * K + c] * p.inv_count;
+    var = fmaxf(p.stats[(size_t)gi * 2 * K + K + c] * p.inv_count - mean * mean, 0.f);
+  } else {
+    mean = p.rmean[c];
+    var = p.rvar[c];
+  }
+  const float sc = p.gamma[c] * rsqrtf(var + p.eps);
+  p.coef[(size_t)gi * 2 * K + c] = sc;
+  p.coef[(size_t)gi * 2 * K + K + c] = p.beta[c] - mean * sc;
 }
 
 int pg_cus() {
@@ -424,17 +548,27 @@ int pg_cus() {
 }  // namespace
 
 // returns 0 when the shape / tile is not supported (caller falls back to igemm)
-int pgemm_launch(const PgemmArgs& g_in, int bn, int grid, hipStream_t st) {
+int pgemm_launch(const PgemmArgs& g_in, int bn, int grid, hipStream_t st, const PgemmPro* pro_in) {
   PgemmArgs g = g_in;
+  PgemmPro pro{};
+  if (pro_in) pro = *pro_in;
   if (g.K % 8 || g.N % 8 || g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
   if (g.stats && g.group_rows < PG_BM) return 0;           // a tile straddles <= 1 group boundary
+  if (pro.mode) {
+    if (g.stride != 1 || !pro.coef || pro.G < 1 || pro.group_rows < PG_BM) return 0;
+    if (pro.mode == 2 && !pro.res) return 0;
+  }
   const int ntiles = ((g.M + PG_BM - 1) / PG_BM) * ((g.N + bn - 1) / bn);
   if (grid <= 0) grid = pg_cus();
   if (grid > ntiles) grid = ntiles;
+  if (pro.mode) {
+    const int n = pro.G * g.K;
+    hipLaunchKernelGGL(pg_coef_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pro, g.K);
+  }
   switch (bn) {
-    case 256: pg_launch<256, 2, 4>(g, grid, st); return 1;
-    case 128: pg_launch<128, 4, 5>(g, grid, st); return 1;
-    case 64: pg_launch<64, 8, 6>(g, grid, st); return 1;
+    case 256: return pg_launch<256, 2, 4, 3, 0>(g, pro, grid, st);
+    case 128: return pg_launch<128, 4, 5, 4, 3>(g, pro, grid, st);
+    case 64: return pg_launch<64, 8, 6, 5, 3>(g, pro, grid, st);
     default: return 0;
   }
 }

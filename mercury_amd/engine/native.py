@@ -106,12 +106,13 @@ class NativeEngine(object):
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
         # the bucket all-reduces captured INSIDE the train graph (event fork onto the comm stream
-        # after each bucket's backward segment, one join before the tail): a DP step replays the
-        # same three graphs as a one-GPU step, no per-bucket host replays or host-issued
-        # collectives.  Timed (diagnostic) steps still run the segmented form so each bucket's
-        # all-reduce can be bracketed by events.  MERCURY_CAPTURE_COMM=0: segmented always.
+        # after each bucket's backward segment, one join before the tail), so a DP step replays
+        # the same three graphs as a one-GPU step.  OFF by default: measured on MI355X at W = 1
+        # (forced buckets, same box, profiles/r3/dp_capture_ab.json) the captured RCCL graph ran
+        # 1.948 ms/step vs 1.598 for the segmented replays (non-DP 1.429) -- RCCL's captured
+        # collectives cost more than the host-issued ones.  MERCURY_CAPTURE_COMM=1 turns it on.
         self.capture_comm = self.s_comm is not None and \
-            os.environ.get('MERCURY_CAPTURE_COMM', '1') == '1'
+            os.environ.get('MERCURY_CAPTURE_COMM', '0') == '1'
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         if grad_compress not in (None, 'none', 'ternary'):
             raise ValueError("grad_compress must be None, 'none' or 'ternary'")

@@ -243,19 +243,55 @@ def pgemm_plan(spec: ConvSpec):
     return 64
 
 
-def pgemm_fwd(x, w, out, spec: ConvSpec, stats=None, bn=None, grid=0):
-    """out[M][K] = conv1x1(x NHWC, w [K][Cp]) on the persistent LDS-DMA GEMM (+ BN sums)."""
-    if not pgemm_ok(spec) and not (spec.R == 1 and spec.pad == 0 and spec.stride in (1, 2)):
+_PG_NO_PRO = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0, 1, 1, 0, 0, 0, 0, 0, 0)
+
+
+def _pg_pro_args(pro, spec, x):
+    """PgemmPro (csrc/igemm.h) from a dict: the PRODUCER's BN -- stats=[G][2][C] sums (or
+    rmean/rvar), gamma, beta, act, eps, count (pixels per stats group), group_rows (input rows
+    per group) -- plus res= (identity residual, mode 2), keep= (activation output), coef=
+    (fp32 workspace >= G*2*C)."""
+    for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta', 'coef'):
+        _chk(pro.get(k), torch.float32, 'pro.' + k)
+    rows = spec.N * spec.H * spec.W
+    _chk(pro.get('keep'), torch.bfloat16, 'pro.keep', rows * spec.Cp)
+    _chk(pro.get('res'), torch.bfloat16, 'pro.res', rows * spec.Cp)
+    if pro.get('stats') is None and pro.get('rmean') is None:
+        raise ValueError('pro needs stats or running statistics')
+    grp = int(pro.get('group_rows') or rows)
+    G = rows // grp if pro.get('stats') is not None else 1
+    if pro['coef'].numel() < G * 2 * spec.Cp:
+        raise ValueError('pro.coef workspace too small')
+    res, keep = pro.get('res'), pro.get('keep')
+    return (2 if res is not None else 1, ptr(pro.get('stats')), ptr(pro.get('rmean')),
+            ptr(pro.get('rvar')), ptr(pro['gamma']), ptr(pro['beta']),
+            1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)), _ACT[pro.get('act')],
+            grp if G > 1 else max(grp, rows), G, ptr(pro['coef']), ptr(res), ptr(keep),
+            0 if res is None else res.numel() * 2, 0 if keep is None else keep.numel() * 2,
+            pro['coef'].numel() * 4)
+
+
+def pgemm_fwd(x, w, out, spec: ConvSpec, stats=None, bn=None, grid=0, pro=None):
+    """out[M][K] = conv1x1(x NHWC, w [K][Cp]) on the persistent LDS-DMA GEMM (+ BN sums).
+    ``pro``: x is the producer's raw output; its BN + activation (+ identity residual) is
+    applied to each operand tile in LDS (see ``_pg_pro_args``)."""
+    if not (spec.R == 1 and spec.S == 1 and spec.pad == 0 and spec.stride in (1, 2)):
         raise ValueError('pgemm: 1x1 pad-0 stride-1/2 convs only')
+    if pro is not None and spec.stride != 1:
+        raise ValueError('pgemm: the input prologue needs a stride-1 conv')
     Cp = spec.Cp
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
     _chk(w, torch.bfloat16, 'w', spec.K * Cp)
     _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
     _chk(stats, torch.float32, 'stats')
     grp = spec.group_rows if spec.group_rows else spec.M
+    bn = bn or pgemm_plan(spec)
+    if pro is not None and bn == 256:
+        bn = 128      # the 256-wide tile has no register room for the prologue
+    pa = _PG_NO_PRO if pro is None else _pg_pro_args(pro, spec, x)
     ok = lib().pgemm(ptr(x), ptr(w), ptr(out), ptr(stats), spec.M, spec.K, Cp, spec.K, spec.K,
                      grp, x.numel() * 2, w.numel() * 2, out.numel() * 2, spec.H, spec.W, spec.P,
-                     spec.Q, spec.stride, bn or pgemm_plan(spec), int(grid), stream_ptr())
+                     spec.Q, spec.stride, bn, int(grid), stream_ptr(), *pa)
     if not ok:
         raise ValueError('pgemm: unsupported shape/tile %s bn=%s' % (spec, bn))
     return out

@@ -69,3 +69,79 @@ def test_pgemm_matches_torch(case):
     out2 = torch.empty_like(out)
     ops.pgemm_fwd(xn, wk, out2, spec, bn=bn, grid=grid)
     assert torch.equal(out2, out)
+
+
+PRO_CASES = [
+    # N, H, W, C, K, group_imgs, bn, act, residual, eval
+    (16, 14, 14, 256, 64, 4, 64, 'relu', False, False),     # R50 conv3-style input BN
+    (16, 14, 14, 128, 512, 4, 128, 'relu', True, False),    # block-final BN + identity residual
+    (8, 16, 16, 96, 24, 0, 64, 'none', True, False),        # MobileNetV2 linear bottleneck + res
+    (8, 16, 16, 24, 144, 2, 128, 'relu6', False, False),    # expand after a project BN, K < 32
+    (12, 9, 11, 40, 72, 0, 64, 'relu', False, True),        # eval: running statistics
+    (32, 7, 7, 512, 2048, 8, 256, 'relu', True, False),     # wide N: 256 -> 128 tile
+]
+
+
+@pytest.mark.parametrize('case', PRO_CASES)
+def test_pgemm_input_bn_prologue(case):
+    """pgemm(pro=...) == bn_apply (+ residual) pass followed by the plain conv, and == an fp32
+    torch reference; the kept activation == bn_apply's output."""
+    from mercury_amd import ops
+    from mercury_amd.ops.conv import ConvSpec
+    ops.lib()
+    N, H, W, C, K, gimgs, bn, act, resid, ev = case
+    g = torch.Generator(device='cpu').manual_seed(7 + C + K)
+    rows = N * H * W
+    y = bf(torch.randn(rows, C, generator=g) * 2 + 0.5).to(DEV)
+    res = bf(torch.randn(rows, C, generator=g)).to(DEV) if resid else None
+    w = bf(torch.randn(K, C, 1, 1, generator=g) / math.sqrt(C)).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    rmean = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    rvar = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    spec = ConvSpec(N, H, W, C, K, 1, 1, 1, 0)
+    G = N // gimgs if gimgs else 1
+    grp = (gimgs or N) * H * W
+    if gimgs:
+        spec.group_rows = grp
+    yg = y.view(G, grp, C)
+    stats = torch.stack([yg.sum(1), yg.pow(2).sum(1)], 1).contiguous()       # [G][2][C]
+    yb = y.to(torch.bfloat16)
+    rb = res.to(torch.bfloat16) if resid else None
+    # reference activation
+    if ev:
+        mean, var = rmean.view(1, 1, C), rvar.view(1, 1, C)
+    else:
+        mean = (stats[:, 0] / grp).view(G, 1, C)
+        var = (stats[:, 1] / grp).view(G, 1, C) - mean ** 2
+    a = (yg - mean) / torch.sqrt(var + 1e-5) * gamma + beta
+    if resid:
+        a = a + res.view(G, grp, C)
+    a = {'relu': torch.relu, 'relu6': lambda t: t.clamp(0, 6), 'none': lambda t: t}[act](a)
+    a = a.reshape(rows, C)
+    ref = bf(a) @ w.view(K, C).t()
+    wk, _ = ops.pack_conv_weight(w)
+    keep = torch.full_like(yb, float('nan'))
+    coef = torch.zeros(G * 2 * C, device=DEV)
+    pro = dict(gamma=gamma, beta=beta, act=act, eps=1e-5, keep=keep, coef=coef, group_rows=grp,
+               count=grp, res=rb)
+    if ev:
+        pro.update(rmean=rmean, rvar=rvar)
+    else:
+        pro.update(stats=stats.reshape(-1))
+    out = torch.empty(rows, K, dtype=torch.bfloat16, device=DEV)
+    ostats = torch.zeros(G, 2, K, device=DEV)
+    ops.pgemm_fwd(yb, wk, out, spec, stats=ostats, bn=bn, pro=pro)
+    close(out, ref)
+    # unfused: bn_apply (+ residual) pass, then the plain conv
+    an = torch.empty_like(yb)
+    ops.bn_apply(yb, None if ev else stats.reshape(-1), gamma, beta, an, rows, C,
+                 group_rows=grp if gimgs else 0, act=act, running=(rmean, rvar) if ev else None,
+                 res=rb)
+    out2 = torch.empty_like(out)
+    ostats2 = torch.zeros_like(ostats)
+    ops.pgemm_fwd(an, wk, out2, spec, stats=ostats2, bn=bn)
+    close(out, out2, rtol=1e-2, atol=1e-2)
+    close(ostats, ostats2, rtol=1e-2, atol=0.5)
+    assert not torch.isnan(keep.float()).any()
+    close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
