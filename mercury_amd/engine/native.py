@@ -32,7 +32,8 @@ import torch.distributed as dist
 
 from .. import ops
 from ..ops import hconv, tune
-from ..ops.conv import ConvSpec, cpad8, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
+from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plan,
+                        slab_bytes, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
@@ -166,6 +167,13 @@ class NativeEngine(object):
         # on -- the in-LDS transform costs the persistent blocks more than the 8 bn_apply passes
         # it removes cost the step
         self.persist_bn = os.environ.get('MERCURY_PERSIST_BN', '0') == '1'
+        # 1x1 convs on the persistent LDS-DMA pointwise GEMM (csrc/pgemm.hip): plain where it
+        # measured faster than igemm (>= 128 output channels, profiles/r3/pgemm_cmp_v2.jsonl),
+        # and wherever it takes its input's BN + activation (+ identity residual) in LDS --
+        # intra-block BNs and the block-final BN of the previous block, which then never make a
+        # separate bn_apply pass (the consumer's N-tile-0 tiles write the activation once where
+        # the residual / backward need it).  MERCURY_PGEMM=0: igemm + bn_apply passes.
+        self.use_pgemm = os.environ.get('MERCURY_PGEMM', '1') == '1'
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
@@ -273,6 +281,7 @@ class NativeEngine(object):
         H, W = self.H, self.W
         C = cpad8(self.lw.in_channels)
         slab = 0
+        coef = 0
         nstats = 0
         nsums = 0
         bf = torch.bfloat16
@@ -301,6 +310,9 @@ class NativeEngine(object):
                     m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(
                         sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
+                    if self.use_pgemm and pgemm_ok(sp) and u.b_seg is None:
+                        m.plan[u.name, 'pgemm'] = pgemm_plan(sp)
+                        coef = max(coef, m.G * 2 * sp.Cp)
                     # stride-1 3x3 convs on the halo-tile kernel where it measured faster
                     uh = self.use_hconv == '1' or self.use_hconv == ('train' if train else 'score')
                     hp = hconv.engine_plan(sp, bias=u.b_seg is not None) if uh else None
@@ -379,6 +391,9 @@ class NativeEngine(object):
         if train:
             m.dlogits = torch.zeros(N, self.classes, device=dev)
         m.slab = torch.zeros(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
+        # per-stream scale / shift workspace of the pointwise GEMM's input prologue (each fused
+        # conv's coefficient kernel fills it right before the conv, on the same stream)
+        m.coef = torch.zeros(max(1, coef), dtype=torch.float32, device=dev)
         m.input = torch.zeros(N, self.H, self.W, cpad8(self.lw.in_channels), dtype=bf, device=dev)
         m.label = torch.zeros(N, dtype=torch.int32, device=dev)
         m.index = torch.zeros(N, dtype=torch.int32, device=dev)
@@ -394,6 +409,11 @@ class NativeEngine(object):
 
     def _conv_fwd(self, m, u, x, y, stats, pro=None):
         sp = m.spec[u.name]
+        pg = m.plan.get((u.name, 'pgemm'))
+        if pg is not None and (pro is not None and pro.get('pg') or
+                               pro is None and sp.K >= 128):
+            ops.pgemm_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, bn=pg, pro=pro)
+            return
         if u.depthwise:
             ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
                            sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M)
@@ -412,12 +432,32 @@ class NativeEngine(object):
         activation (backward reads it) through the consumer's centre-tap write-back."""
         if not self.fuse_bn_fwd or nxt.depthwise or u.act not in ('relu', 'relu6', 'none'):
             return None
+        pg = self._pg_pro(m, u, u.act, m.buf[u.name, 'a'] if m.train else None, nxt)
+        if pg is not None:
+            return pg
         sp = m.spec[nxt.name]
         if not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=m.train):
             return None
         su = m.spec[u.name]
         d = dict(gamma=self._gamma(u), beta=self._beta(u), act=u.act, eps=BN_EPS,
                  keep=m.buf[u.name, 'a'] if m.train else None)
+        if m.train or m.group_imgs:
+            d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
+        else:
+            d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+        return d
+
+    def _pg_pro(self, m, u, act, keep, nxt, res=None):
+        """Input prologue of the pointwise GEMM running ``nxt`` on the raw output of ``u``:
+        act(bn_u(y) [+ res]), activation written to ``keep`` (or None), or None when ``nxt``
+        does not run on pgemm."""
+        if (nxt.name, 'pgemm') not in m.plan or act not in ('relu', 'relu6', 'none'):
+            return None
+        su = m.spec[u.name]
+        if m.spec[nxt.name].stride != 1:
+            return None
+        d = dict(pg=True, gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS,
+                 keep=keep, res=res, coef=m.coef, group_rows=su.group_rows or su.M)
         if m.train or m.group_imgs:
             d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
         else:
@@ -491,6 +531,8 @@ class NativeEngine(object):
         pend = None          # the previous block's output, not yet materialised in x's buffer
         nblk = len(self.lw.blocks)
         pool_bn = None       # BN + activation the block's max pool applies (scoring/eval stem)
+        pgp = None           # the previous block's final BN (+ identity residual), applied by the
+        #                      pointwise GEMM that consumes it (which writes the block output)
         for bi, blk in enumerate(self.lw.blocks):
             inp = x
             nu = len(blk.units)
@@ -498,7 +540,10 @@ class NativeEngine(object):
             for i, u in enumerate(blk.units):
                 y = m.buf[u.name, 'y']
                 st = m.stats[u.name] if stats_on else None
-                if pend is not None:
+                if pgp is not None:
+                    self._conv_fwd(m, u, pgp['y'], y, st, pro=pgp['pro'])
+                    pgp = None
+                elif pend is not None:
                     # BN (+ residual / shortcut BN) + act of the input applied while staging;
                     # ``keep`` materialises x (block input) for the residual, shortcut and
                     # backward; intra-block activations are kept only for the backward
@@ -533,7 +578,14 @@ class NativeEngine(object):
                     elif blk.identity:
                         res = x
                     nb = self.lw.blocks[bi + 1] if bi + 1 < nblk else None
-                    if (nb is not None and not blk.pool and nb.units and
+                    pgd = None
+                    if nb is not None and not blk.pool and nb.units and ru is None:
+                        pgd = self._pg_pro(m, u, blk.final_act, out, nb.units[0], res=res)
+                    if pgd is not None:
+                        # the next block's first (pointwise) conv applies this BN (+ identity
+                        # residual) + activation in its operand tiles and writes ``out``
+                        pgp = dict(y=y, pro=pgd)
+                    elif (nb is not None and not blk.pool and nb.units and
                             self._can_take(m, nb.units[0]) and
                             blk.final_act in ('relu', 'relu6', 'none')):
                         # the next block's first conv applies this BN (+ residual) and writes

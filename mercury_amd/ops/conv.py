@@ -230,7 +230,8 @@ def pgemm_ok(spec: ConvSpec):
         return False
     if spec.group_rows and spec.group_rows < spec.M and spec.group_rows < PGEMM_BM:
         return False
-    return spec.M >= 16 * PGEMM_BM
+    # one block per CU walks the tiles: fewer than ~half a GPU of tiles leaves CUs idle
+    return math.ceil(spec.M / PGEMM_BM) * math.ceil(spec.K / pgemm_plan(spec)) >= 128
 
 
 def pgemm_plan(spec: ConvSpec):
