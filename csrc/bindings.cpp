@@ -295,6 +295,28 @@ PYBIND11_MODULE(_C, m) {
     head_fwd_launch(a, S(st));
     check_launch("head_fwd");
   });
+  // speech-VGG head (flatten -> fc1 -> fc2 -> log-softmax CE), head.hip
+  m.def("mlp_head_fwd", [](uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,
+                           uintptr_t h1, uintptr_t logits, uintptr_t label, uintptr_t isw,
+                           uintptr_t dlogits, uintptr_t losses, uintptr_t meters, int B, int F,
+                           int H1, int K, int mode, int score_kind, int splits, uintptr_t st) {
+    mlp_head_fwd_launch(P<const bf16>(x), P<const bf16>(w1), P<const float>(b1),
+                        P<const float>(w2), P<const float>(b2), P<float>(h1), P<float>(logits), B,
+                        F, H1, K, splits, S(st));
+    HeadArgs a{nullptr, P<const float>(w2), P<const float>(b2), P<const int>(label),
+               P<const float>(isw), P<float>(h1), P<float>(logits), P<float>(dlogits),
+               P<float>(losses), P<float>(meters), B, 1, H1, K, mode, 0, score_kind, 1};
+    head_loss_launch(a, S(st));
+    check_launch("mlp_head_fwd");
+  });
+  m.def("mlp_head_bwd", [](uintptr_t dlogits, uintptr_t h1, uintptr_t x, uintptr_t w1, uintptr_t w2,
+                           uintptr_t dh1, uintptr_t dw1, uintptr_t db1, uintptr_t dw2, uintptr_t db2,
+                           uintptr_t dx, int B, int F, int H1, int K, uintptr_t st) {
+    mlp_head_bwd_launch(P<const float>(dlogits), P<const float>(h1), P<const bf16>(x),
+                        P<const bf16>(w1), P<const float>(w2), P<float>(dh1), P<float>(dw1),
+                        P<float>(db1), P<float>(dw2), P<float>(db2), P<bf16>(dx), B, F, H1, K, S(st));
+    check_launch("mlp_head_bwd");
+  });
   m.def("head_bwd", [](uintptr_t pooled, uintptr_t dlogits, uintptr_t w, uintptr_t dw, uintptr_t db,
                        uintptr_t dact, int B, int HW, int C, int classes, uintptr_t st) {
     HeadBwdArgs a{P<const float>(pooled), P<const float>(dlogits), P<const float>(w), P<float>(dw),

@@ -54,8 +54,18 @@ constexpr int LT = 64, LK = 64;
 // one 64 (rows) x 64 (r) operand slice per block, 16 floats per thread.  RC: thread -> row tid/4,
 // r (tid%4)*16..+15;  else r tid/16 + 16j (j < 4), rows (tid%16)*4..+3.  A whole 64-deep slice
 // per barrier pair: the loop is latency-bound (one block per CU), so fewer, larger slices.
-template <bool RC>
-MA_DEV void tile_load(const float* p, int ld, int i0, int ni, int r0, int nr, int tid,
+// element type of a head operand: fp32, or bf16 (activations / packed weights, read 8 bytes at
+// a time and widened)
+MA_DEV float4 ld4x(const float* q) { return *(const float4*)q; }
+MA_DEV float4 ld4x(const bf16* q) {
+  const bf16x4 v = *(const bf16x4*)q;
+  return make_float4(bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3]));
+}
+MA_DEV float ld1x(const float* q) { return *q; }
+MA_DEV float ld1x(const bf16* q) { return bf2f(*q); }
+
+template <bool RC, typename T>
+MA_DEV void tile_load(const T* p, int ld, int i0, int ni, int r0, int nr, int tid,
                       float4 (&v)[4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -63,21 +73,21 @@ MA_DEV void tile_load(const float* p, int ld, int i0, int ni, int r0, int nr, in
     const int r = RC ? r0 + (tid & 3) * 16 + j * 4 : r0 + (tid >> 4) + 16 * j;
     float e[4];
     if (RC) {
-      const float* q = p + (size_t)(i < ni ? i : 0) * ld + r;
+      const T* q = p + (size_t)(i < ni ? i : 0) * ld + r;
       if (i < ni && r + 3 < nr) {
-        v[j] = *(const float4*)q;
+        v[j] = ld4x(q);
         continue;
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) e[t] = (i < ni && r + t < nr) ? q[t] : 0.f;
+      for (int t = 0; t < 4; ++t) e[t] = (i < ni && r + t < nr) ? ld1x(q + t) : 0.f;
     } else {
-      const float* q = p + (size_t)(r < nr ? r : 0) * ld + i;
+      const T* q = p + (size_t)(r < nr ? r : 0) * ld + i;
       if (r < nr && i + 3 < ni) {
-        v[j] = *(const float4*)q;
+        v[j] = ld4x(q);
         continue;
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) e[t] = (r < nr && i + t < ni) ? q[t] : 0.f;
+      for (int t = 0; t < 4; ++t) e[t] = (r < nr && i + t < ni) ? ld1x(q + t) : 0.f;
     }
     v[j] = make_float4(e[0], e[1], e[2], e[3]);
   }
@@ -95,28 +105,34 @@ MA_DEV void tile_store(float (*T)[LT + 4], const float4 (&v)[4], int tid) {
   }
 }
 
-template <bool AR, bool BR, int OUT>
-__global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, const float* Bm,
+// OUT 2: bf16 C (plain row-major [M][N], * scale).  TA / TB: operand element types.  Split-R
+// (gridDim.z > 1, OUT 0 only): each z-slice adds its partial product into C atomically (C must
+// be zeroed; slice 0 adds the bias).
+template <bool AR, bool BR, int OUT, typename TA = float, typename TB = float>
+__global__ __launch_bounds__(NT) void head_gemm_kernel(const TA* A, int lda, const TB* Bm,
                                                        int ldb, const float* bias, void* out,
                                                        int M, int N, int R, int HW, float scale) {
   __shared__ float As[LK][LT + 4], Bs[LK][LT + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int m0 = blockIdx.x * LT, n0 = blockIdx.y * LT;
+  // split-R: this block's slice [rb0, rb1) of the reduction (whole LK steps)
+  const int nz = gridDim.z, per = ((R + LK - 1) / LK + nz - 1) / nz * LK;
+  const int rb0 = blockIdx.z * per, rb1 = min(R, rb0 + per);
   float4 ra[4], rb[4];
-  tile_load<AR>(A, lda, m0, M, 0, R, tid, ra);
-  tile_load<BR>(Bm, ldb, n0, N, 0, R, tid, rb);
+  tile_load<AR>(A, lda, m0, M, rb0, rb1, tid, ra);
+  tile_load<BR>(Bm, ldb, n0, N, rb0, rb1, tid, rb);
   float acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  for (int r0 = 0; r0 < R; r0 += LK) {
+  for (int r0 = rb0; r0 < rb1; r0 += LK) {
     tile_store<AR>(As, ra, tid);
     tile_store<BR>(Bs, rb, tid);
     __syncthreads();
-    if (r0 + LK < R) {
-      tile_load<AR>(A, lda, m0, M, r0 + LK, R, tid, ra);
-      tile_load<BR>(Bm, ldb, n0, N, r0 + LK, R, tid, rb);
+    if (r0 + LK < rb1) {
+      tile_load<AR>(A, lda, m0, M, r0 + LK, rb1, tid, ra);
+      tile_load<BR>(Bm, ldb, n0, N, r0 + LK, rb1, tid, rb);
     }
 #pragma unroll
     for (int kk = 0; kk < LK; ++kk) {
@@ -139,7 +155,17 @@ __global__ __launch_bounds__(NT) void head_gemm_kernel(const float* A, int lda, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + tx * 4 + j;
-        if (n < N) o[(size_t)m * N + n] = acc[i][j] + (bias ? bias[n] : 0.f);
+        if (n >= N) continue;
+        const float v = acc[i][j] + (bias && blockIdx.z == 0 ? bias[n] : 0.f);
+        if (nz > 1) atomicAdd(o + (size_t)m * N + n, v);
+        else o[(size_t)m * N + n] = v;
+      }
+    } else if (OUT == 2) {
+      bf16* o = (bf16*)out + (size_t)m * N;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + tx * 4 + j;
+        if (n < N) o[n] = f2bf(acc[i][j] * scale);
       }
     } else {
       bf16* o = (bf16*)out + (size_t)m * HW * N;
@@ -312,6 +338,52 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
                        a.pooled, a.C, a.w, a.C, a.b, (void*)a.logits, a.B, a.classes, a.C, 1, 1.f);
     a.logits_ready = 1;
   }
+  const size_t shm = (size_t)(a.C + a.classes + 16) * sizeof(float);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), shm, st, a);
+}
+
+// ---------------------------------------------------------------- speech-VGG head
+// flatten -> fc1 -> fc2 -> log_softmax (`pytorch_model.py:145-153`).  fc1's weights are kept
+// in the engine's [f1][H][W][C] layout (the flatten order of an NHWC activation; torch's
+// [f1][C][H][W] at the state-dict boundary), so fc1 is a plain GEMM on the activation rows.
+// Forward: h1 = x . W1^T + b1 (split-R, atomics into a zeroed h1), logits = h1 . W2^T + b2, then
+// the loss / dlogits / meters kernel.  Backward: dW2, db2, dh1 = dlogits . W2, db1, dW1 =
+// dh1^T . x (straight into the flat gradient, engine layout), dx = dh1 . W1 (bf16 NHWC).
+void mlp_head_fwd_launch(const bf16* x, const bf16* w1, const float* b1, const float* w2,
+                         const float* b2, float* h1, float* logits, int B, int F, int H1, int K,
+                         int splits, hipStream_t st) {
+  (void)hipMemsetAsync(h1, 0, sizeof(float) * B * H1, st);
+  hipLaunchKernelGGL((head_gemm_kernel<true, true, 0, bf16, bf16>),
+                     dim3((B + LT - 1) / LT, (H1 + LT - 1) / LT, splits), dim3(NT), 0, st, x, F,
+                     w1, F, b1, (void*)h1, B, H1, F, 1, 1.f);
+  hipLaunchKernelGGL((head_gemm_kernel<true, true, 0>), dim3((B + LT - 1) / LT, (K + LT - 1) / LT),
+                     dim3(NT), 0, st, h1, H1, w2, H1, b2, (void*)logits, B, K, H1, 1, 1.f);
+}
+
+void mlp_head_bwd_launch(const float* dlogits, const float* h1, const bf16* x, const bf16* w1,
+                         const float* w2, float* dh1, float* dw1, float* db1, float* dw2,
+                         float* db2, bf16* dx, int B, int F, int H1, int K, hipStream_t st) {
+  hipLaunchKernelGGL((head_gemm_kernel<false, false, 0>), dim3((K + LT - 1) / LT, (H1 + LT - 1) / LT),
+                     dim3(NT), 0, st, dlogits, K, h1, H1, (const float*)nullptr, (void*)dw2, K,
+                     H1, B, 1, 1.f);
+  hipLaunchKernelGGL(head_db_kernel, dim3((K + NT - 1) / NT), dim3(NT), 0, st, dlogits, db2, B, K);
+  hipLaunchKernelGGL((head_gemm_kernel<true, false, 0>), dim3((B + LT - 1) / LT, (H1 + LT - 1) / LT),
+                     dim3(NT), 0, st, dlogits, K, w2, H1, (const float*)nullptr, (void*)dh1, B, H1,
+                     K, 1, 1.f);
+  hipLaunchKernelGGL(head_db_kernel, dim3((H1 + NT - 1) / NT), dim3(NT), 0, st, dh1, db1, B, H1);
+  hipLaunchKernelGGL((head_gemm_kernel<false, false, 0, float, bf16>),
+                     dim3((H1 + LT - 1) / LT, (F + LT - 1) / LT), dim3(NT), 0, st, dh1, H1, x, F,
+                     (const float*)nullptr, (void*)dw1, H1, F, B, 1, 1.f);
+  hipLaunchKernelGGL((head_gemm_kernel<true, false, 2, float, bf16>),
+                     dim3((B + LT - 1) / LT, (F + LT - 1) / LT), dim3(NT), 0, st, dh1, H1, w1, F,
+                     (const float*)nullptr, (void*)dx, B, F, H1, 1, 1.f);
+}
+
+// loss / dlogits / meters / score from precomputed logits (a.pooled: the classifier input, for
+// the gradient-norm score)
+void head_loss_launch(const HeadArgs& a0, hipStream_t st) {
+  HeadArgs a = a0;
+  a.logits_ready = 1;
   const size_t shm = (size_t)(a.C + a.classes + 16) * sizeof(float);
   hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), shm, st, a);
 }

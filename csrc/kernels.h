@@ -82,6 +82,7 @@ struct HeadArgs {
   int logits_ready;              // (set by head_fwd_launch) pooled/logits already computed
 };
 void head_fwd_launch(const HeadArgs& a, hipStream_t st);
+void head_loss_launch(const HeadArgs& a, hipStream_t st);
 
 struct HeadBwdArgs {
   const float* pooled;           // [B][C]
@@ -92,6 +93,12 @@ struct HeadBwdArgs {
   bf16* dact;                    // [B][HW][C] grad of final activation
   int B, HW, C, classes;
 };
+void mlp_head_fwd_launch(const bf16* x, const bf16* w1, const float* b1, const float* w2,
+                         const float* b2, float* h1, float* logits, int B, int F, int H1, int K,
+                         int splits, hipStream_t st);
+void mlp_head_bwd_launch(const float* dlogits, const float* h1, const bf16* x, const bf16* w1,
+                         const float* w2, float* dh1, float* dw1, float* db1, float* dw2,
+                         float* db2, bf16* dx, int B, int F, int H1, int K, hipStream_t st);
 void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st);
 
 // ------------------------------------------------------------------ importance sampling

@@ -32,8 +32,8 @@ import torch.distributed as dist
 
 from .. import ops
 from ..ops import hconv, tune
-from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plan,
-                        slab_bytes, wgrad_plan)
+from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plain_wins,
+                        pgemm_plan, pgemm_pro_wins, slab_bytes, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
@@ -210,9 +210,35 @@ class NativeEngine(object):
             self.tern = TernaryAllReduce(cap, self.device, comm=self.comm, seed=seed)
 
     # ------------------------------------------------------------------ parameters
+    def _final_chw(self):
+        """(C, H, W) of the last block's output (speech VGG: 512 x 3 x 5 for 1x101x161)."""
+        h, w = self.H, self.W
+        for blk in self.lw.blocks:
+            for u in blk.units:
+                h = (h + 2 * u.pad - u.R) // u.stride + 1
+                w = (w + 2 * u.pad - u.R) // u.stride + 1
+            if blk.pool is not None:
+                k, st, pd = blk.pool
+                h = (h + 2 * pd - k) // st + 1
+                w = (w + 2 * pd - k) // st + 1
+        return self.lw.blocks[-1].units[-1].K, h, w
+
     def _make_params(self, optimizer, lr, betas, eps, wd, momentum):
         segs = []
         self.w_krsc, self.w_crsk = {}, {}
+        # speech VGG: fc1's master weights live in [f1][H][W][C] order (the flatten order of the
+        # NHWC activation), so fc1 is a plain GEMM on the activation rows; the optimizer writes
+        # its bf16 copy like a conv weight's (torch's [f1][C][H][W] at the state-dict boundary)
+        self.mlp_chw = None
+        self.w1p = None
+        if self.lw.head_pool == 'mlp2':
+            c, h, w = self._final_chw()
+            f1 = self.lw.fc1.out_features
+            if c * h * w != self.lw.fc1.in_features:
+                raise ValueError('fc1 expects %d inputs, the features give %d x %d x %d'
+                                 % (self.lw.fc1.in_features, c, h, w))
+            self.mlp_chw = (c, h, w)
+            self.w1p = torch.zeros(f1, h, w, c, dtype=torch.bfloat16, device=self.device)
         for u in self.units:
             if u.depthwise:
                 continue
@@ -229,6 +255,10 @@ class NativeEngine(object):
             if u is not None and not u.depthwise:
                 d.update(kind=1, K=u.K, R=u.R, S=u.R, C=u.C, Cpad=cpad8(u.C),
                          w_krsc=self.w_krsc[u.name], w_crsk=self.w_crsk.get(u.name))
+            elif self.mlp_chw is not None and s is self.lw.fc1_w:
+                c, h, w = self.mlp_chw
+                d.update(kind=1, K=self.lw.fc1.out_features, R=h, S=w, C=c, Cpad=c,
+                         w_krsc=self.w1p, w_crsk=None)
             segs.append(d)
         self.opt = ops.FlatOptimizer(segs, self.lw.total, self.device, optimizer, lr, betas, eps,
                                      wd, momentum)
@@ -238,38 +268,41 @@ class NativeEngine(object):
         buf = self.opt.g if grad else self.opt.p
         return buf[seg.off:seg.off + seg.numel]
 
+    def _krsc_shape(self, seg):
+        """[K][C][R][S] torch shape of a segment stored KRSC in the master, else None."""
+        if seg.kind == 'conv':
+            return tuple(seg.param.shape)
+        if self.mlp_chw is not None and seg is self.lw.fc1_w:
+            c, h, w = self.mlp_chw
+            return (self.lw.fc1.out_features, c, h, w)
+        return None
+
     @torch.no_grad()
     def load_from_module(self):
         """Module parameters (torch layout) -> flat master (engine layout) + bf16 copies."""
         for s in self.lw.segs:
-            p = s.param.detach().to(self.device, torch.float32)
-            if s.kind == 'conv':
-                p = p.permute(0, 2, 3, 1)
-            self.opt.p[s.off:s.off + s.numel].copy_(p.reshape(-1))
+            self._from_torch_layout(s, self.opt.p, s.param.detach())
         self.opt.pack_weights()
-        self._mlp_refresh()
 
     @torch.no_grad()
     def sync_to_module(self):
         """Flat master -> module parameters (torch layout).  BN buffers are shared already."""
         for s in self.lw.segs:
-            v = self.opt.p[s.off:s.off + s.numel]
-            if s.kind == 'conv':
-                k, c, r, ss = s.param.shape
-                v = v.view(k, r, ss, c).permute(0, 3, 1, 2)
-            s.param.data.copy_(v.reshape(s.param.shape))
+            s.param.data.copy_(self._to_torch_layout(s, self.opt.p).reshape(s.param.shape))
 
     def _to_torch_layout(self, seg, flat):
         v = flat[seg.off:seg.off + seg.numel]
-        if seg.kind == 'conv':
-            k, c, r, s = seg.param.shape
-            return v.view(k, r, s, c).permute(0, 3, 1, 2).contiguous()
+        sh = self._krsc_shape(seg)
+        if sh is not None:
+            k, c, r, s = sh
+            return v.view(k, r, s, c).permute(0, 3, 1, 2).reshape(seg.param.shape).contiguous()
         return v.view(seg.param.shape).clone()
 
     def _from_torch_layout(self, seg, flat, t):
         t = t.to(self.device, torch.float32)
-        if seg.kind == 'conv':
-            t = t.permute(0, 2, 3, 1)
+        sh = self._krsc_shape(seg)
+        if sh is not None:
+            t = t.reshape(sh).permute(0, 2, 3, 1)
         flat[seg.off:seg.off + seg.numel].copy_(t.reshape(-1))
 
     # ------------------------------------------------------------------ buffers
@@ -411,7 +444,7 @@ class NativeEngine(object):
         sp = m.spec[u.name]
         pg = m.plan.get((u.name, 'pgemm'))
         if pg is not None and (pro is not None and pro.get('pg') or
-                               pro is None and sp.K >= 128):
+                               pro is None and pgemm_plain_wins(sp)):
             ops.pgemm_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, bn=pg, pro=pro)
             return
         if u.depthwise:
@@ -454,7 +487,7 @@ class NativeEngine(object):
         if (nxt.name, 'pgemm') not in m.plan or act not in ('relu', 'relu6', 'none'):
             return None
         su = m.spec[u.name]
-        if m.spec[nxt.name].stride != 1:
+        if m.spec[nxt.name].stride != 1 or not pgemm_pro_wins(m.spec[nxt.name]):
             return None
         d = dict(pg=True, gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS,
                  keep=keep, res=res, coef=m.coef, group_rows=su.group_rows or su.M)
@@ -612,69 +645,34 @@ class NativeEngine(object):
         return x
 
     # ------------------------------------------------------------------ speech-VGG head
-    # flatten -> fc1 -> fc2 (-> log_softmax; CE on log-probs == CE on logits).  Plain GEMMs
-    # at M = batch, so they go to hipBLASLt through torch.matmul (captured in the step graphs).
-    # fc1's columns are stored in torch's (C,H,W) flatten order; activations are NHWC, so a
-    # bf16 copy with (H,W,C) column order is refreshed after every optimizer step.
-    def _mlp_refresh(self):
-        if self.lw.head_pool != 'mlp2' or getattr(self, 'mlp_hwc', None) is None:
-            return
-        h, w, c = self.mlp_hwc
-        W1 = self._pview(self.lw.fc1_w).view(-1, c, h, w)
-        self.w1p.copy_(W1.permute(0, 2, 3, 1).reshape(W1.shape[0], -1))
-
+    # flatten -> fc1 -> fc2 -> log_softmax (CE on log-probs == CE on logits), all HIP kernels
+    # (csrc/head.hip mlp_head_*): fc1 runs on the NHWC activation rows against the [f1][H][W][C]
+    # bf16 copy the optimizer writes, its weight gradient lands in the flat buffer in that order
     def _mlp_setup(self, m):
-        last = len(self.lw.blocks) - 1
-        h, w = m.buf[last, 'hw']
-        self.mlp_hwc = (h, w, m.final_C)
         f1 = self.lw.fc1.out_features
-        if getattr(self, 'w1p', None) is None:
-            self.w1p = torch.zeros(f1, h * w * m.final_C, dtype=torch.bfloat16, device=self.device)
-            self._mlp_refresh()
+        m.h1 = torch.zeros(m.N, f1, device=self.device)
+        if m.train:
+            m.dh1 = torch.zeros(m.N, f1, device=self.device)
 
     def _mlp_head(self, m, x, mode, isw=None, meters=None):
-        N, f1 = m.N, self.lw.fc1.out_features
-        xf = x.view(N, -1)
-        h1 = (xf @ self.w1p.t()).float() + self._pview(self.lw.fc1_b)
-        W2 = self._pview(self.lw.fc_w).view(self.classes, f1)
-        logits = torch.addmm(self._pview(self.lw.fc_b), h1, W2.t())
-        lab = m.label.long()
-        lse = torch.logsumexp(logits, 1)
-        loss = lse - logits.gather(1, lab[:, None])[:, 0]
-        p = torch.exp(logits - lse[:, None])
-        d = p.clone()
-        d[torch.arange(N, device=d.device), lab] -= 1.0
-        if mode == 'score':
-            if self.score == 'gradnorm':
-                m.losses.copy_(d.norm(dim=1) * torch.sqrt(h1.pow(2).sum(1) + 1.0))
-            else:
-                m.losses.copy_(loss)
-            return
-        if meters is not None:
-            wl = loss / isw if (mode == 'train' and isw is not None) else loss
-            meters[0:1].add_(wl.sum())
-            meters[1:2].add_(float(N))
-            meters[2:3].add_((logits.argmax(1) == lab).float().sum())
-        if mode == 'train':
-            m.losses.copy_(loss)
-            m.mlp_h1 = h1
-            m.dlogits.copy_(d / (float(N) * isw[:, None]))
+        if getattr(m, 'h1', None) is None:
+            self._mlp_setup(m)
+        c, h, w = self.mlp_chw
+        ops.mlp_head_fwd(x, self.w1p, self._pview(self.lw.fc1_b), self._pview(self.lw.fc_w),
+                         self._pview(self.lw.fc_b), m.h1, m.logits, m.label, m.N, c * h * w,
+                         self.lw.fc1.out_features, self.classes, mode, isw=isw,
+                         dlogits=m.dlogits if mode == 'train' else None, losses=m.losses,
+                         meters=meters if mode != 'score' else None,
+                         score=self.score if mode == 'score' else 'loss')
 
     def _mlp_head_bwd(self, m, dout):
         """Grads of fc2 / fc1 into the flat buffer and d(activation) (NHWC bf16) into dout."""
-        N, f1 = m.N, self.lw.fc1.out_features
-        h, w, c = self.mlp_hwc
-        g = m.dlogits
-        W2 = self._pview(self.lw.fc_w).view(self.classes, f1)
-        self._pview(self.lw.fc_w, True).view(self.classes, f1).copy_(g.t() @ m.mlp_h1)
-        self._pview(self.lw.fc_b, True).copy_(g.sum(0))
-        dh1 = g @ W2
-        self._pview(self.lw.fc1_b, True).copy_(dh1.sum(0))
-        xf = m.buf[len(self.lw.blocks) - 1, 'out'].view(N, -1)
-        dW1p = dh1.t() @ xf.float()                                 # (H,W,C) column order
-        self._pview(self.lw.fc1_w, True).view(f1, c, h, w).copy_(
-            dW1p.view(f1, h, w, c).permute(0, 3, 1, 2))
-        dout.view(N, -1).copy_(dh1.to(torch.bfloat16) @ self.w1p)
+        c, h, w = self.mlp_chw
+        x = m.buf[len(self.lw.blocks) - 1, 'out']
+        ops.mlp_head_bwd(m.dlogits, m.h1, x, self.w1p, self._pview(self.lw.fc_w), m.dh1,
+                         self._pview(self.lw.fc1_w, True), self._pview(self.lw.fc1_b, True),
+                         self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True), dout,
+                         m.N, c * h * w, self.lw.fc1.out_features, self.classes)
 
     def head(self, m, x, mode, isw=None, meters=None):
         if self.lw.head_pool == 'mlp2':
@@ -843,6 +841,7 @@ class NativeEngine(object):
         self.score_mode = self.mode('score', self.P, self.B, False)
         if self.lw.head_pool == 'mlp2':
             self._mlp_setup(self.train_mode)
+            self._mlp_setup(self.score_mode)
         self.idx = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._arange_b = torch.arange(self.B, dtype=torch.int32, device=self.device)
         self.isw = torch.ones(self.B, dtype=torch.float32, device=self.device)
@@ -1040,7 +1039,6 @@ class NativeEngine(object):
             self._order(tick=3, at=5)
         (self.bn_table if self.scoring else self.bn_table_uniform).launch(0.1)
         self.opt.step(self.ctrl[2:3])
-        self._mlp_refresh()
         self.gather_batch()
 
     def _order(self, slot=-1, ref=0, mult=0, add=0, ge=False, tick=-1, at=0):

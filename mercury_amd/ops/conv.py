@@ -244,6 +244,22 @@ def pgemm_plan(spec: ConvSpec):
     return 64
 
 
+def pgemm_plain_wins(spec: ConvSpec):
+    """Plain (no input prologue) pointwise GEMM faster than igemm: measured at the ResNet-50
+    scoring batch (profiles/r3/pgemm_cmp_v2.jsonl) on every shape with >= 256 input and
+    >= 256 output channels (10-16 %), within noise or slower elsewhere."""
+    return spec.C >= 256 and spec.K >= 256
+
+
+def pgemm_pro_wins(spec: ConvSpec):
+    """The input-BN prologue beats a bn_apply pass + igemm when the transformed operand tile is
+    used by ONE output tile (N <= 128: each activation element normalised once) and the input is
+    wide enough to be memory-bound on the pass it saves (profiles/r3/pgemm_pro_cmp.jsonl:
+    ResNet-50 256->64 @56 1105 vs 1323 us, 256->128 1184 vs 1461; it loses where every element
+    is re-normalised for 2-4 output tiles, e.g. 1024->512 @14 741 vs 592)."""
+    return spec.K <= 128 and spec.C >= 128
+
+
 _PG_NO_PRO = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0, 1, 1, 0, 0, 0, 0, 0, 0)
 
 

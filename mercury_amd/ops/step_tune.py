@@ -50,8 +50,8 @@ def coordinates(eng):
     out = {}
     for m in eng.modes.values():
         for (name, kind), _ in m.plan.items():
-            if kind in ('wgrad', 'hconv', 'hconv_bn'):   # (halo-conv plans: measured, not tuned)
-                continue
+            if kind in ('wgrad', 'hconv', 'hconv_bn', 'pgemm'):   # (halo-conv / pointwise-GEMM
+                continue                                          # plans: measured, not tuned)
             if kind == 'fwd' and (name, 'hconv') in m.plan:
                 continue                                  # (its igemm plan is never launched)
             sp = m.spec[name]
