@@ -470,9 +470,16 @@ PYBIND11_MODULE(_C, m) {
     check_launch("maxpool2d_bwd");
   });
   m.def("dwconv_fwd", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W,
-                         int C, int Pp, int Q, int stride, int pad, int group_rows, uintptr_t st) {
+                         int C, int Pp, int Q, int stride, int pad, int group_rows, uintptr_t st,
+                         uintptr_t p_stats, uintptr_t p_rmean, uintptr_t p_rvar, uintptr_t p_gamma,
+                         uintptr_t p_beta, uintptr_t keep, float p_inv_count, float p_eps,
+                         int p_act, int p_group_imgs) {
+    if (p_gamma && (pad != 1 || (stride != 1 && stride != 2) || H != Pp * stride || W != Q * stride))
+      throw std::invalid_argument("dwconv_fwd: input prologue needs a pad-1 'same' 3x3 conv");
     DwArgs a{P<const bf16>(x), P<const float>(w), P<bf16>(y), P<float>(stats), N, H, W, C, Pp, Q,
-             stride, pad, group_rows};
+             stride, pad, group_rows, P<const float>(p_stats), P<const float>(p_rmean),
+             P<const float>(p_rvar), P<const float>(p_gamma), P<const float>(p_beta), P<bf16>(keep),
+             p_inv_count, p_eps, p_act, p_group_imgs > 0 ? p_group_imgs : N};
     dwconv_fwd_launch(a, S(st));
     check_launch("dwconv_fwd");
   });

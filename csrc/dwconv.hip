@@ -52,7 +52,7 @@ MA_DEV bf16x8 ld8(const bf16* p, bool ok) {
 }
 
 constexpr int ST_LD = 17;   // floats per thread row of the forward's BN partials (odd stride)
-template <int S>
+template <int S, bool PRO>
 __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
   extern __shared__ float part[];  // [DT][ST_LD] per-thread BN partial sums (sum, sumsq)
   const int C8 = a.C >> 3, QS = (a.Q + DWL - 1) / DWL;
@@ -76,6 +76,27 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
     load_w72(a.w, c8, wr);
     constexpr int NCOL = (DWL - 1) * S + 3;
     const int q0 = qs * DWL, w0 = q0 * S - a.pad;
+    // input prologue: this thread's 8 channels of its image's statistics group (same arithmetic
+    // as bn.hip); NaN clamp bounds for act none keep NaN (conv_epi.h act_clamp_bounds)
+    float psc[8], psh[8], plo = 0.f, phi = 0.f;
+    if constexpr (PRO) {
+      const int ch = c8 * 8;
+      const float* m0p = a.pro_stats ? a.pro_stats + (size_t)(n / a.pro_group_imgs) * 2 * a.C + ch
+                                     : a.pro_rmean + ch;
+      const float* v0p = a.pro_stats ? m0p + a.C : a.pro_rvar + ch;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float mean = m0p[k], var = v0p[k];
+        if (a.pro_stats) {
+          mean *= a.pro_inv_count;
+          var = fmaxf(var * a.pro_inv_count - mean * mean, 0.f);
+        }
+        psc[k] = a.pro_gamma[ch + k] * rsqrtf(var + a.pro_eps);
+        psh[k] = a.pro_beta[ch + k] - mean * psc[k];
+      }
+      plo = a.pro_act == 0 ? __builtin_nanf("") : 0.f;
+      phi = a.pro_act == 2 ? 6.f : (a.pro_act == 0 ? __builtin_nanf("") : __builtin_huge_valf());
+    }
     float acc[DWL][8];
 #pragma unroll
     for (int o = 0; o < DWL; ++o)
@@ -90,7 +111,19 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
         for (int j = 0; j < NCOL; ++j) {
           const int ww = w0 + j;
-          col[j] = ld8(row + (size_t)ww * a.C, ww >= 0 && ww < a.W);
+          const bool in = ww >= 0 && ww < a.W;
+          col[j] = ld8(row + (size_t)ww * a.C, in);
+          if constexpr (PRO) {
+            if (in) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k)
+                col[j][k] = f2bf(fminf(fmaxf(bf2f(col[j][k]) * psc[k] + psh[k], plo), phi));
+              // the strip owning input (h, ww) writes the activation once: rows p*S .. p*S+S-1
+              // (rr >= pad), columns of its own output strip
+              if (a.keep && rr >= a.pad && rr < a.pad + S && j >= a.pad && j < a.pad + DWL * S)
+                *(bf16x8*)(a.keep + (size_t)(n * a.H + h) * a.W * a.C + (size_t)ww * a.C + c8 * 8) = col[j];
+            }
+          }
         }
 #pragma unroll
         for (int o = 0; o < DWL; ++o)
@@ -316,10 +349,14 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long long total = (long long)a.N * a.P * QS * (a.C / 8);
   const dim3 grid((unsigned)((total + DT - 1) / DT));
   const size_t shm = a.stats ? (size_t)DT * ST_LD * sizeof(float) : 0;
-  if (a.stride == 1)
-    hipLaunchKernelGGL(dw_fwd_kernel<1>, grid, dim3(DT), shm, st, a);
-  else
-    hipLaunchKernelGGL(dw_fwd_kernel<2>, grid, dim3(DT), shm, st, a);
+  const bool pro = a.pro_gamma != nullptr;
+  if (a.stride == 1) {
+    if (pro) hipLaunchKernelGGL((dw_fwd_kernel<1, true>), grid, dim3(DT), shm, st, a);
+    else hipLaunchKernelGGL((dw_fwd_kernel<1, false>), grid, dim3(DT), shm, st, a);
+  } else {
+    if (pro) hipLaunchKernelGGL((dw_fwd_kernel<2, true>), grid, dim3(DT), shm, st, a);
+    else hipLaunchKernelGGL((dw_fwd_kernel<2, false>), grid, dim3(DT), shm, st, a);
+  }
 }
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int P,
                          int Q, int stride, int pad, hipStream_t st) {

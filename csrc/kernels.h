@@ -248,6 +248,17 @@ struct DwArgs {                   // depthwise 3x3 conv NHWC bf16
   bf16* y;
   float* stats;                  // BN sums [G][2][C] or null
   int N, H, W, C, P, Q, stride, pad, group_rows;
+  // input prologue (pro_gamma != null): x is the producer's raw output, act(bn(x)) is applied
+  // to every loaded input chunk (padding stays zero); keep (optional) receives the activation,
+  // each element written once by the thread whose strip owns it
+  const float* pro_stats;        // [G][2][C] producer sums, or null -> running statistics
+  const float* pro_rmean;
+  const float* pro_rvar;
+  const float* pro_gamma;
+  const float* pro_beta;
+  bf16* keep;
+  float pro_inv_count, pro_eps;
+  int pro_act, pro_group_imgs;
 };
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,

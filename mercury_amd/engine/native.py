@@ -174,6 +174,8 @@ class NativeEngine(object):
         # separate bn_apply pass (the consumer's N-tile-0 tiles write the activation once where
         # the residual / backward need it).  MERCURY_PGEMM=0: igemm + bn_apply passes.
         self.use_pgemm = os.environ.get('MERCURY_PGEMM', '1') == '1'
+        # depthwise convs take their input's BN + activation in their chunk loads
+        self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
@@ -449,7 +451,8 @@ class NativeEngine(object):
             return
         if u.depthwise:
             ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
-                           sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M)
+                           sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M,
+                           pro=pro if pro is not None and pro.get('dw') else None)
         elif pro is None and (u.name, 'hconv') in m.plan:
             hconv.hconv_fwd(x, self.w_krsc[u.name], y, sp, m.plan[u.name, 'hconv'], stats=stats,
                             slab=m.slab,
@@ -463,8 +466,21 @@ class NativeEngine(object):
         """BN-apply of ``u`` folded into the load of its consumer ``nxt`` (csrc/igemm.h
         ProParams), or None when that conv/plan cannot take it.  Train mode also keeps the
         activation (backward reads it) through the consumer's centre-tap write-back."""
-        if not self.fuse_bn_fwd or nxt.depthwise or u.act not in ('relu', 'relu6', 'none'):
+        if not self.fuse_bn_fwd or u.act not in ('relu', 'relu6', 'none'):
             return None
+        if nxt.depthwise:
+            # MobileNetV2's expand BN + ReLU6 applied to each chunk the depthwise conv loads
+            if not self.dw_pro:
+                return None
+            su = m.spec[u.name]
+            d = dict(dw=True, gamma=self._gamma(u), beta=self._beta(u), act=u.act, eps=BN_EPS,
+                     keep=m.buf[u.name, 'a'] if m.train else None,
+                     group_imgs=m.group_imgs or m.N)
+            if m.train or m.group_imgs:
+                d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
+            else:
+                d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+            return d
         pg = self._pg_pro(m, u, u.act, m.buf[u.name, 'a'] if m.train else None, nxt)
         if pg is not None:
             return pg

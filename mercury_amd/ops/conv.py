@@ -257,7 +257,11 @@ def pgemm_pro_wins(spec: ConvSpec):
     wide enough to be memory-bound on the pass it saves (profiles/r3/pgemm_pro_cmp.jsonl:
     ResNet-50 256->64 @56 1105 vs 1323 us, 256->128 1184 vs 1461; it loses where every element
     is re-normalised for 2-4 output tiles, e.g. 1024->512 @14 741 vs 592)."""
-    return spec.K <= 128 and spec.C >= 128
+    if spec.K <= 128 and spec.C >= 128:
+        return True
+    # MobileNetV2 at 32x32 (profiles/r3/pgemm_pro_cmp.jsonl, M = 327680): every expand /
+    # project shape gained (e.g. 24->144 53 vs 73 us); at 16x16 and below it lost
+    return spec.M >= 131072 and spec.K <= 192
 
 
 _PG_NO_PRO = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0, 1, 1, 0, 0, 0, 0, 0, 0)

@@ -60,9 +60,26 @@ def maxpool2d_bwd(dy, argmax, dx, N, H, W, C, P, Q, k, stride, pad):
                         stream_ptr())
 
 
-def dwconv_fwd(x, w, y, N, H, W, C, P, Q, stride, pad, stats=None, group_rows=0):
+_ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
+
+
+def dwconv_fwd(x, w, y, N, H, W, C, P, Q, stride, pad, stats=None, group_rows=0, pro=None):
+    """Depthwise 3x3 forward (+ BN sums).  ``pro``: x is the producer's raw output and
+    act(bn(x)) is applied to each loaded chunk -- dict(stats=[G][2][C] | rmean/rvar, gamma,
+    beta, act, eps, count, group_imgs, keep=optional activation output)."""
+    pa = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0, 0)
+    if pro is not None:
+        for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta'):
+            _chk(pro.get(k), torch.float32, 'pro.' + k)
+        _chk(pro.get('keep'), torch.bfloat16, 'pro.keep', N * H * W * C)
+        if pro.get('stats') is None and pro.get('rmean') is None:
+            raise ValueError('pro needs stats or running statistics')
+        pa = (ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')),
+              ptr(pro['gamma']), ptr(pro['beta']), ptr(pro.get('keep')),
+              1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)),
+              _ACT[pro.get('act')], int(pro.get('group_imgs') or N))
     lib().dwconv_fwd(ptr(x), ptr(w), ptr(y), ptr(stats), N, H, W, C, P, Q, stride, pad,
-                     group_rows or N * P * Q, stream_ptr())
+                     group_rows or N * P * Q, stream_ptr(), *pa)
 
 
 def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad):

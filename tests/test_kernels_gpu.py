@@ -965,3 +965,36 @@ def test_maxpool_stem_shape_bwd_matches_torch():
     dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
     ops.maxpool2d_bwd(ops.to_nhwc(gy), am, dx, N, H, W, C, P, Q, 3, 2, 1)
     close(ops.from_nhwc(dx), xx.grad, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize('stride', [1, 2])
+@pytest.mark.parametrize('ghost', [False, True])
+def test_dwconv_input_bn_prologue_matches_bn_apply_then_dw(stride, ghost):
+    """Depthwise 3x3 with its input's BN + ReLU6 applied to every loaded chunk (MobileNetV2
+    expand -> dw) == bn_apply pass + plain depthwise conv; the kept activation == bn_apply's."""
+    ops = _ops()
+    N, H, W, C = 8, 16, 16, 96
+    P, Q = H // stride, W // stride
+    g = torch.Generator(device='cpu').manual_seed(11 + stride)
+    y = bf(torch.randn(N * H * W, C, generator=g) * 2 + 0.3).to(DEV).to(torch.bfloat16)
+    w = (torch.randn(C, 9, generator=g) * 0.3).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    gi = 4 if ghost else N
+    G = N // gi
+    yg = y.float().view(G, gi * H * W, C)
+    stats = torch.stack([yg.sum(1), yg.pow(2).sum(1)], 1).contiguous().reshape(-1)
+    cnt = gi * H * W
+    a = torch.empty_like(y)
+    ops.bn_apply(y, stats, gamma, beta, a, N * H * W, C, group_rows=cnt if ghost else 0,
+                 act='relu6')
+    ref = torch.empty(N * P * Q, C, dtype=torch.bfloat16, device=DEV)
+    ops.dwconv_fwd(a, w, ref, N, H, W, C, P, Q, stride, 1)
+    out = torch.empty_like(ref)
+    keep = torch.full_like(y, float('nan'))
+    ops.dwconv_fwd(y, w, out, N, H, W, C, P, Q, stride, 1,
+                   pro=dict(stats=stats, gamma=gamma, beta=beta, act='relu6', eps=1e-5,
+                            count=cnt, group_imgs=gi, keep=keep))
+    close(out, ref, rtol=1e-2, atol=1e-2)
+    assert not torch.isnan(keep.float()).any()
+    close(keep, a, rtol=1e-2, atol=1e-2)
