@@ -62,16 +62,13 @@ def main():
             stats = torch.zeros(2, K, device=dev)
             pf = fwd_plan(sp)
             slab = torch.zeros(max(1, slab_bytes(sp.M, K, *pf) // 4), device=dev)
-            ours_f = timeit(lambda: ops.conv_fwd(xn, wk, y, sp, stats=stats, slab=slab, plan=pf,
-                                                 pipe=0), args.iters)
-            pipe_f = {pp: timeit(lambda: ops.conv_fwd(xn, wk, y, sp, stats=stats, slab=slab,
-                                                      plan=pf, pipe=pp), args.iters)
-                      for pp in (3, 4)}
+            ours_f = timeit(lambda: ops.conv_fwd(xn, wk, y, sp, stats=stats, slab=slab, plan=pf),
+                            args.iters)
             ref_f = timeit(lambda: F.conv2d(x, w, stride=st, padding=pd), args.iters)
             flops = sp.flops()
             r = dict(N=N, C=C, K=K, H=H, R=R, stride=st, gflop=flops / 1e9,
                      fwd_us=ours_f, fwd_miopen_us=ref_f, fwd_tflops=flops / ours_f / 1e6,
-                     fwd_plan=list(pf), fwd_pipe3_us=pipe_f[3], fwd_pipe4_us=pipe_f[4])
+                     fwd_plan=list(pf))
             dw = torch.zeros(K, R, R, C, device=dev)
             r['wgrad_us'] = timeit(lambda: ops.conv_wgrad(gyn, xn, dw, sp), args.iters)
             if C % 8 == 0:
@@ -79,9 +76,7 @@ def main():
                 pd_ = dgrad_plan(sp)
                 slab2 = torch.zeros(max(1, slab_bytes(N * H * H, C, *pd_) // 4), device=dev)
                 r['dgrad_us'] = timeit(lambda: ops.conv_dgrad(gyn, wt, dx, sp, slab=slab2,
-                                                              plan=pd_, pipe=0), args.iters)
-                r['dgrad_pipe4_us'] = timeit(lambda: ops.conv_dgrad(gyn, wt, dx, sp, slab=slab2,
-                                                                    plan=pd_, pipe=4), args.iters)
+                                                              plan=pd_), args.iters)
                 xr = x.clone().requires_grad_(False)
 
                 def ref_bwd():
@@ -93,8 +88,7 @@ def main():
             print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v)
                               for k, v in r.items()}), flush=True)
     tot = {k: sum(r.get(k, 0) for r in rows) for k in
-           ('fwd_us', 'fwd_pipe3_us', 'fwd_pipe4_us', 'fwd_miopen_us', 'wgrad_us', 'dgrad_us',
-            'dgrad_pipe4_us', 'bwd_miopen_us')}
+           ('fwd_us', 'fwd_miopen_us', 'wgrad_us', 'dgrad_us', 'bwd_miopen_us')}
     print(json.dumps({'totals_us': {k: round(v, 1) for k, v in tot.items()}}))
     if args.json:
         with open(args.json, 'w') as f:

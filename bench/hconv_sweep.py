@@ -25,6 +25,10 @@ from gtime import gtime  # noqa: E402
 SHAPES = [  # C, K, H, R, stride
     (64, 64, 32, 3, 1), (64, 128, 32, 3, 2), (128, 128, 16, 3, 1), (128, 256, 16, 3, 2),
     (256, 256, 8, 3, 1), (256, 512, 8, 3, 2), (512, 512, 4, 3, 1)]
+# ResNet-50/224 bottleneck 3x3 convs (conv2 of each stage; the stride-2 ones open a stage)
+R50_SHAPES = [(64, 64, 56, 3, 1), (128, 128, 56, 3, 2), (128, 128, 28, 3, 1),
+              (256, 256, 28, 3, 2), (256, 256, 14, 3, 1), (512, 512, 14, 3, 2),
+              (512, 512, 7, 3, 1)]
 
 
 def main():
@@ -32,6 +36,7 @@ def main():
     ap.add_argument('--batch', type=int, default=320)
     ap.add_argument('--no-bn', action='store_true')
     ap.add_argument('--reps', type=int, default=12)
+    ap.add_argument('--r50', action='store_true', help='ResNet-50/224 3x3 shapes')
     args = ap.parse_args()
     import torch
     from mercury_amd import ops
@@ -42,7 +47,7 @@ def main():
     gimgs = 32 if N > 32 else 0
     G = N // gimgs if gimgs else 1
     tot = dict(igemm=0.0, bn_apply=0.0, hconv=0.0, hconv_bn=0.0)
-    for (C, K, Hh, R, st) in SHAPES:
+    for (C, K, Hh, R, st) in (R50_SHAPES if args.r50 else SHAPES):
         sp = ConvSpec(N, Hh, Hh, C, K, R, R, st, R // 2)
         if gimgs:
             sp.group_rows = gimgs * sp.P * sp.Q
@@ -78,6 +83,10 @@ def main():
         for c in cands:
             res[c] = gtime(lambda: H.hconv_fwd(y, wk, out, sp, c, stats=stats, slab=slab),
                            reps=args.reps)
+        if not res:
+            print(json.dumps(dict(shape=[N, C, K, Hh, R, st], igemm_us=round(ti, 2),
+                                  bn_apply_us=round(tb, 2), hconv=None)), flush=True)
+            continue
         best = min(res, key=res.get)
         pro = dict(stats=ystats, gamma=gamma, beta=beta, act='relu', count=(gimgs or N) * Hh * Hh,
                    group_imgs=gimgs or N, keep=a if H.keep_ok(sp) else None)

@@ -196,7 +196,7 @@ def job_ab_kernel(o, a):
 
 def job_sweep(o, a):
     for b in (32, 320):
-        run([PY, 'bench/kernel_sweep.py', '--batch', str(b), '--kind', 'fwd', '--pipes', '0'],
+        run([PY, 'bench/kernel_sweep.py', '--batch', str(b), '--kind', 'fwd'],
             os.path.join(o, 'igemm%d.jsonl' % b), 400)
         run([PY, 'bench/hconv_sweep.py', '--batch', str(b)], os.path.join(o, 'hconv%d.jsonl' % b),
             400)

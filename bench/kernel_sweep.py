@@ -30,7 +30,7 @@ SHAPES = [  # C, K, H, R, stride, pad
     (256, 512, 8, 1, 2, 0)]
 
 
-def fwd_cands(sp, pipes):
+def fwd_cands(sp):
     kt = math.ceil(sp.R * sp.S * sp.Cp / 64)
     out = []
     for bm, bn in ((256, 128), (256, 64), (128, 128), (128, 64), (64, 128), (64, 64)):
@@ -40,8 +40,7 @@ def fwd_cands(sp, pipes):
             continue
         for s in (1, 2, 4, 8):
             if s <= max(1, kt // 2):
-                for p in pipes:
-                    out.append((bm, bn, s, p))
+                out.append((bm, bn, s))
     return out
 
 
@@ -49,7 +48,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--kind', default='both', choices=('fwd', 'bwd', 'both'))
-    ap.add_argument('--pipes', default='0,3,4')
     ap.add_argument('--reps', type=int, default=12)
     ap.add_argument('--write-cache', default='')
     args = ap.parse_args()
@@ -58,7 +56,6 @@ def main():
     from mercury_amd.ops import tune
     from mercury_amd.ops.conv import ConvSpec, dgrad_plan, fwd_plan, slab_bytes, wgrad_plan
     dev = 'cuda'
-    pipes = tuple(int(p) for p in args.pipes.split(','))
     N = args.batch
     gimgs = 32 if N > 32 else 0
     cache = {}
@@ -75,14 +72,14 @@ def main():
         if args.kind in ('fwd', 'both'):
             y = torch.empty(sp.M * K, dtype=torch.bfloat16, device=dev)
             stats = torch.zeros(G * 2 * K, device=dev)
-            cands = fwd_cands(sp, pipes)
+            cands = fwd_cands(sp)
             heur = tuple(fwd_plan(sp)) + (0,)
             slab = torch.zeros(max([slab_bytes(sp.M, K, *c[:3]) for c in cands + [heur]] + [4])
                                // 4 + 1, device=dev)
 
             def run(p):
                 return gtime(lambda: ops.conv_fwd(x, wk, y, sp, stats=stats, slab=slab,
-                                                  plan=p[:3], pipe=p[3]), reps=args.reps)
+                                                  plan=p[:3]), reps=args.reps)
             th = run(heur)
             best = (th, heur)
             for c in cands:

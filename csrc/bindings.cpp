@@ -60,7 +60,7 @@ PYBIND11_MODULE(_C, m) {
                     uintptr_t stats, int stats_ld, int group_rows, int accumulate, uintptr_t slab,
                     int SH, int SW, int SC, int RP, int RQ, int R, int Sk, int stride, int pad, int Kc,
                     int Ncols, int M, int bm, int bn, int splits, bool trans, uintptr_t st,
-                    int pipe, uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
+                    uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
                     uintptr_t bw_stats2, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
                     int bw_act) {
     if (stats && bw_sums)   // the epilogue reduces both through one LDS scratch
@@ -70,7 +70,7 @@ PYBIND11_MODULE(_C, m) {
                 accumulate, P<float>(slab), P<const bf16>(bw_out), P<const bf16>(bw_y),
                 P<const float>(bw_stats), P<const bf16>(bw_y2), P<const float>(bw_stats2),
                 P<float>(bw_sums), bw_inv_count, bw_eps, bw_act};
-    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st), pipe);
+    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
     check_launch("igemm");
   });
   // 1x1 conv as a persistent LDS-DMA GEMM (pgemm.hip); returns 0 if unsupported
@@ -111,7 +111,7 @@ PYBIND11_MODULE(_C, m) {
     ProParams pr{P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
                  P<const float>(p_gamma), P<const float>(p_beta), P<bf16>(p_keep), p_group_rows,
                  p_inv_count, p_eps, p_act, p_keep_tap};
-    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, false, S(st), 0, &pr);
+    igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, false, S(st), &pr);
     check_launch("igemm_pro");
   });
   // halo-tile forward conv (hconv.hip) with the producer's BN (+ residual / shortcut BN) +

@@ -65,11 +65,9 @@ struct ProParams {
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);
-// pipe = 0: register-staged double buffer; 3/4: LDS-DMA ring of that many stages.
-// pro != null: BN-apply prologue (forward, pipe 0 only).
+// pro != null: BN-apply prologue (forward only).
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
-                  int bn, int splits, bool trans, hipStream_t st, int pipe = 0,
-                  const ProParams* pro = nullptr);
+                  int bn, int splits, bool trans, hipStream_t st, const ProParams* pro = nullptr);
 
 struct WgradGeom {
   int N, H, W, C;     // input x (C padded), NHWC

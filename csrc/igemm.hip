@@ -23,13 +23,10 @@
 // DPP row operations (cdna_hip_programming.md §3: choose the product orientation
 // so later consumers see the layout they want).
 //
-// Main loop (two variants, same LDS image and fragment reads):
-//   pipe 0 : 256 threads = 4 waves (2x2), BK = 64 per stage, register-staged double
-//            buffer (stage t+1 loads issued before stage t's MFMAs, one barrier/stage)
-//   pipe 3/4: LDS-DMA ring (`global_load_lds_dwordx4`) of that many stages, counted
-//            `s_waitcnt vmcnt(N)` + raw `s_barrier` so tiles stay in flight across
-//            barriers; the XOR swizzle moves to the source address (lane l fetches
-//            logical chunk (l&7)^(l>>3) of its row, landing at physical chunk l&7).
+// Main loop: 256 threads = 4 waves (2x2), BK = 64 per stage, register-staged double buffer
+// (stage t+1 loads issued before stage t's MFMAs, one barrier per stage).  (An LDS-DMA ring
+// variant was A/B'd slower on every conv shape of the step and removed in round 3; the 1x1
+// convs that gain from an LDS-DMA pipeline run on the persistent pointwise GEMM, pgemm.hip.)
 // LDS rows are XOR-swizzled (chunk c of row r lives at c ^ (r&7)).  All address math
 // is 32-bit (per-row base offsets + one uniform per-tap offset), padding chunks read
 // a zero page.  Split-K writes fp32 partial tiles in fragment order (16 B per lane,
@@ -410,112 +407,10 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_pro_kernel(const
                                      blockIdx.y, gridDim.x, gridDim.y, pro);
 }
 
-// ---------------------------------------------------------------- LDS-DMA ring loop
-template <int N>
-MA_DEV void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-MA_DEV void glds16(const void* src, void* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
-}
-
-template <int BM, int BN, int STAGES, bool TRANS>
-__global__ __launch_bounds__(NT, 1) void igemm_pipe_kernel(const bf16* __restrict__ src,
-                                                            const bf16* __restrict__ wt,
-                                                            ConvGeom g, EpiParams e,
-                                                            int ktiles_per_split) {
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int AI = BM / 32, BI = BN / 32;  // LDS-DMA instructions per wave per stage
-  constexpr int G = AI + BI;
-  constexpr int STAGE = Smem<BM, BN>::STAGE;
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(STAGES)];
-  bf16* sbase = (bf16*)smem;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int ntn = (g.Ncols + BN - 1) / BN;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int ktiles = (g.Kc + 7) / 8;
-  const int kt0 = blockIdx.y * ktiles_per_split;
-  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
-  const int Kelems = g.Kc * 8;
-  const int lrow = lane >> 3;                  // row inside an 8-row DMA instruction
-  const int lc = (lane & 7) ^ lrow;            // logical chunk this lane fetches
-
-  int aoff[AI], ah[AI], aw[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i)
-    row_init<TRANS>(g, m0 + w * (BM / 4) + i * 8 + lrow, aoff[i], ah[i], aw[i]);
-  int boff[BI];
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int n = n0 + w * (BN / 4) + i * 8 + lrow;
-    boff[i] = n < g.Ncols ? n * Kelems : -1;
-  }
-  KCursor kc;
-  kc.init(g, kt0);
-  const bf16* zp = g.zero;
-
-  auto issue = [&](int kt, int slot) {
-    bf16* a_st = sbase + slot * STAGE;
-    bf16* b_st = a_st + BM * BK;
-    int r, s, c8;
-    bool kval;
-    kc.decode(g, kt, lc, r, s, c8, kval);
-    kc.advance(g);
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      int o = row_at<TRANS>(g, aoff[i], ah[i], aw[i], r, s, c8);
-      o = kval ? o : -1;                       // select, not a branch around the gather
-      glds16(o >= 0 ? (const void*)(src + o) : (const void*)zp, a_st + (w * (BM / 4) + i * 8) * BK);
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const bool ok = kval && boff[i] >= 0;
-      glds16(ok ? (const void*)(wt + boff[i] + (kt * 8 + lc) * 8) : (const void*)zp,
-             b_st + (w * (BN / 4) + i * 8) * BK);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = kt1 - kt0;
-#pragma unroll
-  for (int j = 0; j < STAGES - 1; ++j)
-    if (j < nk) issue(kt0 + j, j);
-  for (int it = 0; it < nk; ++it) {
-    const int ahead = min(STAGES - 2, nk - 1 - it);  // tiles issued after this one
-    if (ahead >= 2) wait_vmcnt<2 * G>();
-    else if (ahead == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (it + STAGES - 1 < nk) issue(kt0 + it + STAGES - 1, (it + STAGES - 1) % STAGES);
-    const bf16* a = sbase + (it % STAGES) * STAGE;
-    mma_stage<BM, BN>(a, a + BM * BK, acc, lane, wm, wn);
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  finish<BM, BN>(acc, smem, e, g.M, g.Ncols, m0, n0, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
-}
-
 template <int BM, int BN, bool TRANS>
 void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int per,
-                 dim3 grid, int pipe, hipStream_t st) {
-  if (pipe >= 4)
-    hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, (BM + BN > 256 ? 3 : 4), TRANS>), grid, dim3(NT),
-                       0, st, src, wt, g, e, per);
-  else if (pipe == 3)
-    hipLaunchKernelGGL((igemm_pipe_kernel<BM, BN, 3, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e,
-                       per);
-  else
-    hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
+                 dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
 }
 
 // split-K decomposition (clamped; no split when the tile counters would not fit)
@@ -531,7 +426,7 @@ inline void ig_grid(const ConvGeom& g, int BM, int BN, int splits, int& gx, int&
 
 template <int BM, int BN, bool TRANS>
 void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
-                int pipe, hipStream_t st, const ProParams* pro) {
+                hipStream_t st, const ProParams* pro) {
   int gx, per, gy;
   ig_grid(g, BM, BN, splits, gx, per, gy);
   if (gy == 1) e.slab = nullptr;
@@ -540,7 +435,7 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
                        per, *pro);
     return;
   }
-  launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), pipe, st);
+  launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), st);
 }
 
 // ---------------------------------------------------------------- dgrad + wgrad pair launch
@@ -614,14 +509,13 @@ const bf16* conv_zero_page() {
 }
 
 void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const EpiParams& e,
-                  int bm, int bn, int splits, bool trans, hipStream_t st, int pipe,
-                  const ProParams* pro) {
+                  int bm, int bn, int splits, bool trans, hipStream_t st, const ProParams* pro) {
   ConvGeom g = g_in;
   g.zero = zero_page();
 #define MA_CASE(BM_, BN_)                                                           \
   if (bm == BM_ && bn == BN_) {                                                     \
-    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, pipe, st, nullptr); \
-    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, pipe, st, pro);          \
+    if (trans) launch_cfg<BM_, BN_, true>(src, wt, g, e, splits, st, nullptr);       \
+    else launch_cfg<BM_, BN_, false>(src, wt, g, e, splits, st, pro);                \
     return;                                                                         \
   }
   MA_CASE(128, 128)

@@ -14,13 +14,9 @@ from dataclasses import dataclass
 
 import torch
 
-import os
-
 from . import _chk, lib, ptr, stream_ptr
 
 CU = 256
-# NT implicit-GEMM main loop: 0 = register-staged double buffer, 3/4 = LDS-DMA ring
-PIPE = int(os.environ.get('MERCURY_IGEMM_PIPE', '0'))
 
 
 def cpad8(c):
@@ -147,8 +143,7 @@ def pro_ok(spec: ConvSpec, plan, keep=False):
     register-staged loop, real channels a multiple of 8, ghost-BN groups that are whole tiles,
     and -- to keep the activation -- a stride-1 'same' conv (its centre tap is a bijection)."""
     bm = plan[0]
-    pipe = plan[3] if len(plan) > 3 and plan[3] is not None else PIPE
-    if pipe != 0 or spec.C % 8:
+    if spec.C % 8:
         return False
     # pointwise convs only: a 3x3 conv re-loads every input chunk once per tap, and redoing the
     # normalisation 9x in VALU made the conv 2-2.5x slower than a separate bn_apply pass
@@ -185,7 +180,7 @@ def _pro_args(pro, spec):
 
 
 def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=None,
-             accumulate=False, pipe=None, pro=None):
+             accumulate=False, pro=None):
     """out[M][K] = conv(x NHWC, w [K][R][S][Cp]); optional BN-sum epilogue.  ``pro``: x is the
     producer's raw conv output and its BN + activation are applied while loading (see
     ``pro_ok`` / ``_pro_args``)."""
@@ -196,13 +191,11 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     _chk(stats, torch.float32, 'stats')
     plan = plan or fwd_plan(spec)
     bm, bn, splits = plan[:3]
-    if pipe is None and len(plan) > 3 and plan[3] is not None:
-        pipe = plan[3]                       # tuned pipeline variant (ops/tune.py)
     if splits > 1:
         slab = _slab(slab, slab_bytes(spec.M, spec.K, bm, bn, splits), x.device)
     grp = spec.group_rows if spec.group_rows else spec.M
     if pro is not None:
-        if accumulate or not pro_ok(spec, (bm, bn, splits, pipe), keep=pro.get('keep') is not None):
+        if accumulate or not pro_ok(spec, (bm, bn, splits), keep=pro.get('keep') is not None):
             raise ValueError('BN-apply prologue not supported for this conv/plan')
         lib().igemm_pro(ptr(x), ptr(w), ptr(out), spec.K, ptr(bias), ptr(stats), spec.K, grp,
                         ptr(slab) if splits > 1 else 0, spec.H, spec.W, Cp, spec.P, spec.Q,
@@ -213,7 +206,7 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
                 int(accumulate), ptr(slab) if splits > 1 else 0,
                 spec.H, spec.W, Cp, spec.P, spec.Q, spec.R, spec.S, spec.stride, spec.pad,
                 spec.R * spec.S * Cp // 8, spec.K, spec.M, bm, bn, splits, False, stream_ptr(),
-                PIPE if pipe is None else pipe, *_NO_BW)
+                *_NO_BW)
     return out
 
 
@@ -339,8 +332,7 @@ def _bw_args(bw, Mx, Cp):
             _ACT[bw.get('act')])
 
 
-def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, pipe=None,
-               bw=None):
+def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, bw=None):
     """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2.  ``bw``: also reduce
     the BN-backward sums of the (final, post-accumulate) dx in the epilogue."""
     if spec.stride not in (1, 2):
@@ -359,7 +351,7 @@ def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=Fals
                 ptr(slab) if splits > 1 else 0,
                 spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
                 spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, True, stream_ptr(),
-                PIPE if pipe is None else pipe, *_bw_args(bw, Mx, Cp))
+                *_bw_args(bw, Mx, Cp))
     return dx
 
 

@@ -1,7 +1,7 @@
 """Per-shape kernel-plan autotuner with a persistent cache (the MIOpen "find" idea, for our
 own kernels).
 
-The implicit-GEMM conv kernels take a plan -- (tile M, tile N, K-splits[, pipe]) for the
+The implicit-GEMM conv kernels take a plan -- (tile M, tile N, K-splits[, 0]) for the
 forward / data-gradient GEMM and (tile, pixel-splits) for the weight gradient.  The best plan
 depends on the shape and batch in ways heuristics only approximate (bench/fwd_sweep.py,
 bench/bwd_pair_sweep.py: 10-35 % per layer between the heuristic and the best candidate at
@@ -43,7 +43,6 @@ _DIRTY = False
 # pipeline variants tried for the forward GEMM.  The LDS-DMA ring (pipe 3) wins several shapes
 # in isolation but holds a whole CU per block; in the two-stream step it slowed the step
 # (ResNet-18 1.67 -> 1.71 ms), so only the register-staged loop is tuned by default.
-PIPES = tuple(int(p) for p in os.environ.get('MERCURY_TUNE_PIPES', '0').split(','))
 
 
 def enable(flag=True):
@@ -127,8 +126,7 @@ def _fwd_candidates(sp):
             continue
         for s in (1, 2, 4, 8):
             if s <= max(1, kt // 2):
-                for pipe in PIPES:
-                    out.append((bm, bn, s, pipe))
+                out.append((bm, bn, s, 0))
     return out
 
 
@@ -143,7 +141,7 @@ def _bwd_candidates(sp):
 
 
 def fwd_plan_for(sp, heuristic):
-    """(bm, bn, splits, pipe) for the forward conv of ``sp``."""
+    """(bm, bn, splits, 0) for the forward conv of ``sp``."""
     c = _load()
     k = _key('fwd', sp)
     if k in c:

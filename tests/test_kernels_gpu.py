@@ -699,36 +699,6 @@ def test_depthwise_strips_ghost_stats(case):
     close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize('pipe', [1, 3, 4])
-@pytest.mark.parametrize('case', CONV_CASES)
-def test_conv_pipelined_lds_dma(case, pipe):
-    """Main-loop variants of the NT implicit GEMM -- direct-A registers (1), LDS-DMA ring (3, 4):
-    forward, stats, split-K, dgrad, all tile shapes."""
-    ops = _ops()
-    from mercury_amd.ops.conv import ConvSpec, slab_bytes
-    N, H, W, C, K, R, S, st, pd = case
-    x, w = _mk(case, 11)
-    spec = ConvSpec(N, H, W, C, K, R, S, st, pd)
-    xn = ops.to_nhwc(x)
-    wk, wt = ops.pack_conv_weight(w)
-    ref = F.conv2d(x, w, stride=st, padding=pd)
-    for plan in [(128, 128, 1), (64, 128, 2), (128, 64, 1), (64, 64, 3), (256, 64, 1),
-                 (256, 128, 2)]:
-        out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
-        stats = torch.zeros(2, K, device=DEV)
-        ops.conv_fwd(xn, wk, out, spec, stats=stats, plan=plan, pipe=pipe)
-        close(out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2), ref)
-        close(stats[0], bf(ref).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
-    if C % 8 == 0:
-        gy = bf(torch.randn(N, K, spec.P, spec.Q, device=DEV))
-        xr = x.clone().requires_grad_(True)
-        F.conv2d(xr, w, stride=st, padding=pd).backward(gy)
-        for plan in [(128, 128, 1), (64, 128, 3)]:
-            dx = torch.empty(N * H * W, spec.Cp, dtype=torch.bfloat16, device=DEV)
-            ops.conv_dgrad(ops.to_nhwc(gy), wt, dx, spec, plan=plan, pipe=pipe)
-            close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
-
-
 def conv_pro_direct(ops, x, wk, out, spec, slab, plan, pro):
     """conv_fwd(pro=...) without the engine's pointwise-only policy (the kernel takes any
     R x S; the policy is a speed choice)."""
