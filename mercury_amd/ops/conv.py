@@ -223,8 +223,10 @@ def pgemm_ok(spec: ConvSpec):
         return False
     if spec.group_rows and spec.group_rows < spec.M and spec.group_rows < PGEMM_BM:
         return False
-    # one block per CU walks the tiles: fewer than ~half a GPU of tiles leaves CUs idle
-    return math.ceil(spec.M / PGEMM_BM) * math.ceil(spec.K / pgemm_plan(spec)) >= 128
+    # one block per CU walks the tiles: a persistent kernel pays off when every block has
+    # several tiles (>= 64k rows); the latency-bound train-batch convs stay on igemm (measured:
+    # MobileNetV2 at B = 32, 128 tiles, was slower on pgemm)
+    return spec.M >= 65536
 
 
 def pgemm_plan(spec: ConvSpec):
