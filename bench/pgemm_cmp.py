@@ -70,6 +70,9 @@ def main():
             for bn in (64, 128, 256):
                 put('pgemm%d' % bn, gtime(lambda: ops.pgemm_fwd(x, w, y, sp, stats=stats, bn=bn),
                                           reps=4))
+            pw = st == 1 and sp.Cp <= 128
+            if pw:
+                put('pwconv', gtime(lambda: ops.pwconv_fwd(x, w, y, sp, stats=stats), reps=4))
             if a.pro and st == 1:
                 rows = batch * H * H
                 gamma = torch.ones(C, device=dev)
@@ -91,6 +94,9 @@ def main():
                                      act='relu', res=r)
                         ops.conv_fwd(act_buf, w, y, sp, stats=stats, slab=slab, plan=plan)
                     put('pro%d' % mode, gtime(fused, reps=4))
+                    if pw and r is None:
+                        put('pwpro', gtime(lambda: ops.pwconv_fwd(x, w, y, sp, stats=stats,
+                                                                  pro=pro), reps=4))
                     put('bn%d_igemm' % mode, gtime(unfused, reps=4))
             if st == 1:
                 xa, wt, ya = x.view(sp.M, C), w.view(K, C).t(), y.view(sp.M, K)

@@ -93,8 +93,9 @@ PYBIND11_MODULE(_C, m) {
                 P<const float>(p_gamma), P<const float>(p_beta), p_inv_count, p_eps, p_act,
                 p_group_rows, p_G, P<float>(p_coef), P<const bf16>(p_res), P<bf16>(p_keep),
                 (unsigned)p_res_bytes, (unsigned)p_keep_bytes, (unsigned)p_coef_bytes};
-    const int ok = pgemm_launch(g, bn, grid, S(st), &pr);
-    check_launch("pgemm");
+    // bn == 0: the panel-resident narrow-input kernel (pwconv.hip) instead
+    const int ok = bn == 0 ? pwconv_launch(g, S(st), &pr) : pgemm_launch(g, bn, grid, S(st), &pr);
+    check_launch(bn == 0 ? "pwconv" : "pgemm");
     return ok;
   });
   // forward conv whose A operand is BN-applied + activated on load (ProParams, igemm.h)

@@ -162,6 +162,9 @@ struct PgemmPro {
 };
 // bn in {64, 128, 256}; grid <= 0: one block per CU.  Returns 0 when unsupported.
 int pgemm_launch(const PgemmArgs& g, int bn, int grid, hipStream_t st, const PgemmPro* pro = nullptr);
+// Narrow-input (K <= 128) stride-1 1x1 conv with the whole A panel (128 rows x K) resident in
+// LDS and normalised once for all N-tiles (pwconv.hip); mode-1 prologue only.  0: unsupported.
+int pwconv_launch(const PgemmArgs& g, hipStream_t st, const PgemmPro* pro = nullptr);
 
 int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                  const HconvPro& pro, int bm, int bn, int splits, hipStream_t st);

@@ -33,7 +33,8 @@ import torch.distributed as dist
 from .. import ops
 from ..ops import hconv, tune
 from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plain_wins,
-                        pgemm_plan, pgemm_pro_wins, slab_bytes, wgrad_plan)
+                        pgemm_plan, pgemm_pro_wins, pwconv_ok, pwconv_pro_wins, slab_bytes,
+                        wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
@@ -174,6 +175,8 @@ class NativeEngine(object):
         # separate bn_apply pass (the consumer's N-tile-0 tiles write the activation once where
         # the residual / backward need it).  MERCURY_PGEMM=0: igemm + bn_apply passes.
         self.use_pgemm = os.environ.get('MERCURY_PGEMM', '1') == '1'
+        # narrow-input 1x1 convs with the input BN on the panel-resident kernel (pwconv.hip)
+        self.use_pwconv = os.environ.get('MERCURY_PWCONV', '1') == '1'
         # depthwise convs take their input's BN + activation in their chunk loads
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
 
@@ -348,6 +351,9 @@ class NativeEngine(object):
                     if self.use_pgemm and pgemm_ok(sp) and u.b_seg is None:
                         m.plan[u.name, 'pgemm'] = pgemm_plan(sp)
                         coef = max(coef, m.G * 2 * sp.Cp)
+                    if self.use_pwconv and pwconv_ok(sp) and u.b_seg is None:
+                        m.plan[u.name, 'pwconv'] = True
+                        coef = max(coef, m.G * 2 * sp.Cp)
                     # stride-1 3x3 convs on the halo-tile kernel where it measured faster
                     uh = self.use_hconv == '1' or self.use_hconv == ('train' if train else 'score')
                     hp = hconv.engine_plan(sp, bias=u.b_seg is not None) if uh else None
@@ -444,6 +450,9 @@ class NativeEngine(object):
 
     def _conv_fwd(self, m, u, x, y, stats, pro=None):
         sp = m.spec[u.name]
+        if pro is not None and pro.get('pw'):
+            ops.pwconv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, pro=pro)
+            return
         pg = m.plan.get((u.name, 'pgemm'))
         if pg is not None and (pro is not None and pro.get('pg') or
                                pro is None and pgemm_plain_wins(sp)):
@@ -499,14 +508,20 @@ class NativeEngine(object):
     def _pg_pro(self, m, u, act, keep, nxt, res=None):
         """Input prologue of the pointwise GEMM running ``nxt`` on the raw output of ``u``:
         act(bn_u(y) [+ res]), activation written to ``keep`` (or None), or None when ``nxt``
-        does not run on pgemm."""
-        if (nxt.name, 'pgemm') not in m.plan or act not in ('relu', 'relu6', 'none'):
+        does not run on pgemm.  Narrow-input convs whose output spans several N-tiles take the
+        panel-resident kernel instead (pwconv.hip: each element normalised once, not per tile)."""
+        if act not in ('relu', 'relu6', 'none'):
             return None
-        su = m.spec[u.name]
-        if m.spec[nxt.name].stride != 1 or not pgemm_pro_wins(m.spec[nxt.name]):
+        su, sn = m.spec[u.name], m.spec[nxt.name]
+        if res is None and (nxt.name, 'pwconv') in m.plan and pwconv_pro_wins(sn):
+            kind = 'pw'
+        elif (nxt.name, 'pgemm') in m.plan and sn.stride == 1 and pgemm_pro_wins(sn):
+            kind = 'pg'
+        else:
             return None
-        d = dict(pg=True, gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS,
+        d = dict(gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS,
                  keep=keep, res=res, coef=m.coef, group_rows=su.group_rows or su.M)
+        d[kind] = True
         if m.train or m.group_imgs:
             d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
         else:

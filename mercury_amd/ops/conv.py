@@ -252,11 +252,10 @@ def pgemm_pro_wins(spec: ConvSpec):
     wide enough to be memory-bound on the pass it saves (profiles/r3/pgemm_pro_cmp.jsonl:
     ResNet-50 256->64 @56 1105 vs 1323 us, 256->128 1184 vs 1461; it loses where every element
     is re-normalised for 2-4 output tiles, e.g. 1024->512 @14 741 vs 592)."""
-    if spec.K <= 128 and spec.C >= 128:
-        return True
-    # MobileNetV2 at 32x32 (profiles/r3/pgemm_pro_cmp.jsonl, M = 327680): every expand /
-    # project shape gained (e.g. 24->144 53 vs 73 us); at 16x16 and below it lost
-    return spec.M >= 131072 and spec.K <= 192
+    # MobileNetV2's 32x32 expand / project shapes also gained in isolation (24->144 53 vs 73 us)
+    # but the persistent kernel beside the latency-bound train stream lost 0.09 ms/step in the
+    # engine (profiles/r3/mbv2_pgemm_ab.json): the narrow ones go to pwconv instead
+    return spec.K <= 128 and spec.C >= 128
 
 
 _PG_NO_PRO = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0, 1, 1, 0, 0, 0, 0, 0, 0)
@@ -310,6 +309,51 @@ def pgemm_fwd(x, w, out, spec: ConvSpec, stats=None, bn=None, grid=0, pro=None):
                      spec.Q, spec.stride, bn, int(grid), stream_ptr(), *pa)
     if not ok:
         raise ValueError('pgemm: unsupported shape/tile %s bn=%s' % (spec, bn))
+    return out
+
+
+PWCONV_KMAX = 128
+
+
+def pwconv_ok(spec: ConvSpec):
+    """Narrow-input pointwise conv for the panel-resident kernel (csrc/pwconv.hip): 1x1 stride 1,
+    <= 128 input channels (the whole 128-row A panel stays in LDS across every N-tile), ghost-BN
+    groups of >= 128 rows."""
+    if spec.R != 1 or spec.S != 1 or spec.pad != 0 or spec.stride != 1:
+        return False
+    if spec.C % 8 or spec.K % 8 or spec.Cp > PWCONV_KMAX:
+        return False
+    return not (spec.group_rows and spec.group_rows < spec.M and spec.group_rows < 128)
+
+
+def pwconv_pro_wins(spec: ConvSpec):
+    """Panel-resident input-BN prologue (pwconv) over a bn_apply pass + igemm / pgemm's
+    per-tile prologue: the expansion convs -- narrow input (<= 128 channels) read and normalised
+    once, >= 2x wider output -- at >= 64k rows (profiles/r3/pwconv_cmp_*.jsonl: ResNet-50 64->256
+    @56 857 vs 993 us, 128->512 @28 472 vs 610; MobileNetV2 24->144 @32 46 vs 74; the project
+    convs 96->24 lost, 54 vs 48)."""
+    return pwconv_ok(spec) and spec.K >= 2 * spec.C and spec.M >= 65536
+
+
+def pwconv_fwd(x, w, out, spec: ConvSpec, stats=None, pro=None):
+    """out[M][K] = conv1x1(x, w) with the input panel normalised ONCE in LDS (``pro`` as in
+    ``pgemm_fwd``, identity residual excluded) and reused by all output-channel tiles."""
+    if not pwconv_ok(spec):
+        raise ValueError('pwconv: unsupported conv %s' % (spec,))
+    if pro is not None and pro.get('res') is not None:
+        raise ValueError('pwconv: no residual prologue')
+    Cp = spec.Cp
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
+    _chk(w, torch.bfloat16, 'w', spec.K * Cp)
+    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    grp = spec.group_rows if spec.group_rows else spec.M
+    pa = _PG_NO_PRO if pro is None else _pg_pro_args(pro, spec, x)
+    ok = lib().pgemm(ptr(x), ptr(w), ptr(out), ptr(stats), spec.M, spec.K, Cp, spec.K, spec.K,
+                     grp, x.numel() * 2, w.numel() * 2, out.numel() * 2, spec.H, spec.W, spec.P,
+                     spec.Q, 1, 0, 0, stream_ptr(), *pa)
+    if not ok:
+        raise ValueError('pwconv: unsupported shape %s' % (spec,))
     return out
 
 

@@ -2,7 +2,8 @@
 bottlenecks and MobileNetV2's expand / project layers (`pytorch_model.py:44-49`).  Covers every
 tile width, odd channel counts (K, N not multiples of 32 / 64), M not a tile multiple, stride-2
 row gathers, ghost-BN statistics with groups that straddle tiles, and more tiles than blocks
-(the persistent step stream crossing tile boundaries)."""
+(the persistent step stream crossing tile boundaries).  The panel-resident narrow-input kernel
+(csrc/pwconv.hip, K <= 128) runs the same checks on its stride-1 shapes."""
 import math
 
 import pytest
@@ -34,15 +35,33 @@ CASES = [
     (20, 8, 8, 24, 144, 1, 5, 128, 0),         # expand: K = 24 (< one 32-deep step)
     (12, 9, 11, 40, 72, 1, 0, 64, 7),          # M = 1188 (not a tile multiple), 7 blocks
     (64, 7, 7, 2048, 512, 1, 32, 256, 5),      # deep K, few blocks: long step streams
+    # pwconv-only shapes: every panel depth (32 / 64 / 96 / 128 channels), N not a 64 multiple
+    (16, 14, 14, 64, 256, 1, 4, 0, 0),
+    (10, 10, 10, 96, 200, 1, 2, 0, 0),         # 200-row groups: blocks straddle group edges
+    (9, 7, 13, 128, 512, 1, 3, 0, 0),
 ]
 
 
+def _pw_ok(C, st, resid=False):
+    return st == 1 and C <= 128 and not resid
+
+
+@pytest.mark.parametrize('kern', ['pgemm', 'pwconv'])
 @pytest.mark.parametrize('case', CASES)
-def test_pgemm_matches_torch(case):
+def test_pgemm_matches_torch(case, kern):
     from mercury_amd import ops
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, st, gimgs, bn, grid = case
+    if kern == 'pwconv' and not _pw_ok(C, st):
+        pytest.skip('not a pwconv shape')
+    if kern == 'pgemm' and bn == 0:
+        pytest.skip('pwconv-only case')
+
+    def run(xn, wk, out, spec, stats=None):
+        if kern == 'pwconv':
+            return ops.pwconv_fwd(xn, wk, out, spec, stats=stats)
+        return ops.pgemm_fwd(xn, wk, out, spec, stats=stats, bn=bn, grid=grid)
     g = torch.Generator(device='cpu').manual_seed(hash(case) % 1000)
     x = bf(torch.randn(N, C, H, W, generator=g)).to(DEV)
     w = bf(torch.randn(K, C, 1, 1, generator=g) / math.sqrt(C)).to(DEV)
@@ -54,7 +73,7 @@ def test_pgemm_matches_torch(case):
     wk, _ = ops.pack_conv_weight(w)
     out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
     stats = torch.zeros(G, 2, K, device=DEV)
-    ops.pgemm_fwd(xn, wk, out, spec, stats=stats, bn=bn, grid=grid)
+    run(xn, wk, out, spec, stats=stats)
     ref = F.conv2d(x, w, stride=st)
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2)
     assert not torch.isnan(got.float()).any()
@@ -67,7 +86,7 @@ def test_pgemm_matches_torch(case):
         close(stats[gi, 1], r.pow(2).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
     # no stats: plain GEMM path, bitwise equal output
     out2 = torch.empty_like(out)
-    ops.pgemm_fwd(xn, wk, out2, spec, bn=bn, grid=grid)
+    run(xn, wk, out2, spec)
     assert torch.equal(out2, out)
 
 
@@ -79,17 +98,23 @@ PRO_CASES = [
     (8, 16, 16, 24, 144, 2, 128, 'relu6', False, False),    # expand after a project BN, K < 32
     (12, 9, 11, 40, 72, 0, 64, 'relu', False, True),        # eval: running statistics
     (32, 7, 7, 512, 2048, 8, 256, 'relu', True, False),     # wide N: 256 -> 128 tile
+    (16, 14, 14, 64, 256, 4, 64, 'relu', False, False),     # R50 conv3: 64 -> 256, 4 N-tiles
+    (9, 10, 10, 128, 520, 3, 64, 'relu', False, False),     # 300-row groups, N % 64 != 0
+    (6, 12, 12, 96, 576, 0, 64, 'relu6', False, True),      # MobileNetV2 expand, eval
 ]
 
 
+@pytest.mark.parametrize('kern', ['pgemm', 'pwconv'])
 @pytest.mark.parametrize('case', PRO_CASES)
-def test_pgemm_input_bn_prologue(case):
+def test_pgemm_input_bn_prologue(case, kern):
     """pgemm(pro=...) == bn_apply (+ residual) pass followed by the plain conv, and == an fp32
     torch reference; the kept activation == bn_apply's output."""
     from mercury_amd import ops
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, gimgs, bn, act, resid, ev = case
+    if kern == 'pwconv' and not _pw_ok(C, 1, resid):
+        pytest.skip('not a pwconv shape')
     g = torch.Generator(device='cpu').manual_seed(7 + C + K)
     rows = N * H * W
     y = bf(torch.randn(rows, C, generator=g) * 2 + 0.5).to(DEV)
@@ -131,7 +156,10 @@ def test_pgemm_input_bn_prologue(case):
         pro.update(stats=stats.reshape(-1))
     out = torch.empty(rows, K, dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV)
-    ops.pgemm_fwd(yb, wk, out, spec, stats=ostats, bn=bn, pro=pro)
+    if kern == 'pwconv':
+        ops.pwconv_fwd(yb, wk, out, spec, stats=ostats, pro=pro)
+    else:
+        ops.pgemm_fwd(yb, wk, out, spec, stats=ostats, bn=bn, pro=pro)
     close(out, ref)
     # unfused: bn_apply (+ residual) pass, then the plain conv
     an = torch.empty_like(yb)
