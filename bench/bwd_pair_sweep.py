@@ -41,12 +41,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=30)
     ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--default-only', action='store_true',
+                    help='graph-timed default plans only (for same-box A/B of two builds)')
     args = ap.parse_args()
     import torch
     from mercury_amd import ops
     from mercury_amd.ops.conv import ConvSpec, dgrad_plan, slab_bytes, wgrad_plan
     dev = 'cuda'
     N = args.batch
+    tot = 0.0
     for (C, K, H, R, st, pd) in SHAPES:
         sp = ConvSpec(N, H, H, C, K, R, R, st, pd)
         Mx = N * H * H
@@ -70,6 +73,15 @@ def main():
         slab = torch.zeros(max(slab_bytes(Mx, sp.Cp, bm, bn, s) for bm, bn, s in dcands) // 4 + 1,
                            device=dev)
         dp0, wp0 = dgrad_plan(sp), wgrad_plan(sp)
+        if args.default_only:
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            from gtime import gtime
+            us = gtime(lambda: ops.conv_bwd(gy, wt, dx, x, dw, sp, dplan=dp0, wplan=wp0,
+                                            slab=slab), reps=8)
+            tot += us
+            print(json.dumps({'shape': [N, C, K, H, R, st], 'us': round(us, 1),
+                              'plan': [list(dp0), list(wp0)]}), flush=True)
+            continue
         base = timeit(lambda: ops.conv_bwd(gy, wt, dx, x, dw, sp, dplan=dp0, wplan=wp0,
                                            slab=slab), args.iters)
         best = (base, dp0, wp0)
@@ -81,6 +93,8 @@ def main():
         print(json.dumps({'shape': [N, C, K, H, R, st], 'default_us': round(base, 1),
                           'default': [list(dp0), list(wp0)], 'best_us': round(best[0], 1),
                           'best': [list(best[1]), list(best[2])]}), flush=True)
+    if args.default_only:
+        print(json.dumps({'total_us': round(tot, 1)}), flush=True)
 
 
 if __name__ == '__main__':

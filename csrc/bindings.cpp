@@ -484,6 +484,16 @@ PYBIND11_MODULE(_C, m) {
     dwconv_fwd_launch(a, S(st));
     check_launch("dwconv_fwd");
   });
+  // stem conv (<= 4 input channels, taps x channels packed into k); returns 0 if unsupported
+  m.def("stem_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stats,
+                       int N, int H, int W, int K, int R, int stride, int pad, int Pp, int Q,
+                       int group_imgs, uintptr_t st) {
+    StemArgs a{P<const bf16>(x), P<const bf16>(w), P<const float>(bias), P<bf16>(y), P<float>(stats),
+               N, H, W, K, R, stride, pad, Pp, Q, group_imgs, 0, 0};
+    const int ok = stem_fwd_launch(a, S(st));
+    check_launch("stem_fwd");
+    return ok;
+  });
   m.def("dwconv_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int H, int W, int C,
                            int Pp, int Q, int stride, int pad, uintptr_t st) {
     dwconv_dgrad_launch(P<const bf16>(dy), P<const float>(w), P<bf16>(dx), N, H, W, C, Pp, Q, stride,

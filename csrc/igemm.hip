@@ -203,7 +203,7 @@ MA_DEV void mma_stage(const bf16* a, const bf16* b, f32x4 (&acc)[BM / 32][BN / 3
 // (ProParams in igemm.h).  Everything it needs for the chunk staged next -- the 8 channels'
 // statistics / gamma / beta, which rows are padding, where the activation is kept -- is loaded
 // or computed in load_stage, so it is in flight under the MFMA phase like the tile itself.
-template <int BM, int BN, bool TRANS, bool PRO = false>
+template <int BM, int BN, bool TRANS, bool PRO = false, int PF = 1>
 MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                           const ConvGeom& g, const EpiParams& e, int ktiles_per_split, char* smem,
                           int bx, int by, int gx, int gy, const ProParams& pro) {
@@ -245,7 +245,6 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   kc.init(g, kt0);
   const bf16* zp = g.zero;
 
-  u32x4 ra[AR], rb[BR];
   // prologue state for the chunk in flight (PRO only; dead code otherwise)
   float4 pst[8];
   int pz = 0;
@@ -255,11 +254,12 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     const int grp = m0 / pro.group_rows;
     pbase = pro.stats ? pro.stats + (size_t)grp * 2 * g.SC : nullptr;
   }
-  auto load_stage = [&](int kt) {
+  auto load_stage = [&](int kt, u32x4 (&ra)[AR], u32x4 (&rb)[BR]) {
     int r, s, c8;
     bool kval;
     kc.decode(g, kt, cc, r, s, c8, kval);
     kc.advance(g);
+    kval = kval && kt < kt1;       // a prefetch past this split's range loads zeros
     bool keep = false;
     if constexpr (PRO) {
       const int ch = kval ? c8 * 8 : 0;
@@ -293,7 +293,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       rb[i] = *(const u32x4*)(ok ? wt + boff[i] + (kt * 8 + cc) * 8 : zp);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, u32x4 (&ra)[AR], const u32x4 (&rb)[BR]) {
     bf16* a = sA + buf * Smem<BM, BN>::STAGE;
     bf16* b = a + BM * BK;
     if constexpr (PRO) {
@@ -346,9 +346,33 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
-    load_stage(kt0);
-    store_stage(0);
+  if (kt0 < kt1 && PF == 2) {
+    // two stages in flight in registers (the train-batch dgrad is latency-bound: a 64-deep
+    // stage is a few MFMAs per wave against a memory round trip); unrolled by two so each
+    // register set is named statically, every trip issues the same loads (counted vmcnt exact)
+    u32x4 ra0[AR], rb0[BR], ra1[AR], rb1[BR];
+    load_stage(kt0, ra0, rb0);
+    store_stage(0, ra0, rb0);
+    load_stage(kt0 + 1, ra1, rb1);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      load_stage(kt + 2, ra0, rb0);      // LDS 0 holds stage kt, ra1 stage kt + 1
+      mma_stage<BM, BN>(sA, sA + BM * BK, acc, lane, wm, wn);
+      if (kt + 1 >= kt1) break;
+      store_stage(1, ra1, rb1);
+      __syncthreads();
+      load_stage(kt + 3, ra1, rb1);      // LDS 1 holds stage kt + 1, ra0 stage kt + 2
+      const bf16* a1 = sA + Smem<BM, BN>::STAGE;
+      mma_stage<BM, BN>(a1, a1 + BM * BK, acc, lane, wm, wn);
+      if (kt + 2 >= kt1) break;
+      store_stage(0, ra0, rb0);
+      __syncthreads();
+    }
+    __syncthreads();                     // the epilogue may reuse the stage LDS
+  } else if (kt0 < kt1) {
+    u32x4 ra[AR], rb[BR];
+    load_stage(kt0, ra, rb);
+    store_stage(0, ra, rb);
     __syncthreads();
     MA_STAMP(1);
 #ifdef MERCURY_STAMPS
@@ -358,12 +382,12 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     int buf = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
-      if (more) load_stage(kt + 1);
+      if (more) load_stage(kt + 1, ra, rb);
       MA_LAP(0, tl);
       const bf16* a = sA + buf * Smem<BM, BN>::STAGE;
       mma_stage<BM, BN>(a, a + BM * BK, acc, lane, wm, wn);
       MA_LAP(1, tl);
-      if (more) store_stage(buf ^ 1);
+      if (more) store_stage(buf ^ 1, ra, rb);
       MA_LAP(2, tl);
       __syncthreads();
       MA_LAP(3, tl);
@@ -383,7 +407,11 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
 }
 
 
-template <int BM, int BN, bool TRANS>
+// two register-staged stages in flight where the second register set fits (64-wide tiles)
+template <int BM, int BN>
+constexpr int PAIR_PF() { return BM * BN <= 64 * 128 ? 2 : 1; }
+
+template <int BM, int BN, bool TRANS, int PF = 1>
 __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const bf16* __restrict__ src,
                                                           const bf16* __restrict__ wt,
                                                           ConvGeom g, EpiParams e,
@@ -391,8 +419,8 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_nt_kernel(const 
   __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
   const ProParams none{};
   const int bx = gridDim.y == 1 ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
-  igemm_nt_body<BM, BN, TRANS>(src, wt, g, e, ktiles_per_split, smem, bx, blockIdx.y,
-                               gridDim.x, gridDim.y, none);
+  igemm_nt_body<BM, BN, TRANS, false, PF>(src, wt, g, e, ktiles_per_split, smem, bx, blockIdx.y,
+                                          gridDim.x, gridDim.y, none);
 }
 
 // forward conv with the BN-apply prologue on its input (ProParams)
@@ -410,6 +438,17 @@ __global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_pro_kernel(const
 template <int BM, int BN, bool TRANS>
 void launch_main(const bf16* src, const bf16* wt, const ConvGeom& g, const EpiParams& e, int per,
                  dim3 grid, hipStream_t st) {
+  // a grid that does not fill the chip twice over is latency-bound (the train batch): two
+  // stages in flight per block where the second register set fits
+  if constexpr (PAIR_PF<BM, BN>() == 2) {
+#ifndef MERCURY_FWD_PF1   // (A/B builds: bench/build_variant.py with this flag)
+    if (grid.x * grid.y <= 512) {
+      hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS, 2>), grid, dim3(NT), 0, st, src, wt, g, e,
+                         per);
+      return;
+    }
+#endif
+  }
   hipLaunchKernelGGL((igemm_nt_kernel<BM, BN, TRANS>), grid, dim3(NT), 0, st, src, wt, g, e, per);
 }
 
@@ -461,7 +500,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict_
     const ProParams none{};
     // (no XCD renumbering here: measured +1 % step time -- the pair's wgrad blocks come first,
     // so the dgrad tiles' XCD placement is already rotated and interleaved with them)
-    igemm_nt_body<DBM, DBN, true>(dy, wt, g, e, dper, smem, d % dgx, d / dgx, dgx, dgy, none);
+    igemm_nt_body<DBM, DBN, true, false, PAIR_PF<DBM, DBN>()>(dy, wt, g, e, dper, smem, d % dgx,
+                                                               d / dgx, dgx, dgy, none);
   }
 }
 

@@ -261,6 +261,16 @@ struct DwArgs {                   // depthwise 3x3 conv NHWC bf16
   int pro_act, pro_group_imgs;
 };
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
+struct StemArgs {                 // first conv: <= 4 input channels packed densely into k (stem.hip)
+  const bf16* x;                  // [N][H][W][8] (channels >= C zero)
+  const bf16* w;                  // [K][R][R][8] bf16 weights (channels >= C zero)
+  const float* bias;              // [K] or null
+  bf16* y;                        // [N][P][Q][K]
+  float* stats;                   // BN sums [G][2][K] or null
+  int N, H, W, K, R, stride, pad, P, Q, group_imgs;
+  int tpb, blocks_per_img;        // set by the launcher
+};
+int stem_fwd_launch(StemArgs a, hipStream_t st);
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
                          int P, int Q, int stride, int pad, hipStream_t st);
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,

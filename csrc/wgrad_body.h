@@ -23,7 +23,9 @@ struct WgSmem {
 };
 
 // One (column tile bx, pixel split by) of the weight-gradient GEMM; gy = number of splits.
-template <int BM, int BN>
+// PF: stages in flight in registers -- 2 where the extra register set fits (64-wide tiles),
+// 1 for 128 x 128 (the second set spilled)
+template <int BM, int BN, int PF = (BM * BN <= 64 * 128 ? 2 : 1)>
 MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, const WgradGeom& g,
                        float* __restrict__ dw, int ptiles_per_split, bf16* smem, int bx, int by,
                        int gy) {
@@ -61,14 +63,16 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
   const int acc_ = tid % ACH;
 
   const float rpq = 1.f / (float)(g.P * g.Q), rq = 1.f / (float)g.Q;
-  u32x4 ra[AR], rb[BR];
-  auto load_stage = [&](int pt) {
+  // stage loads into a register set; a stage past this split's range loads the zero page, so
+  // every trip issues the same number of loads and hipcc's counted vmcnt stays exact
+  auto load_stage = [&](int pt, u32x4 (&ra)[AR], u32x4 (&rb)[BR]) {
+    const bool live = pt < pt1;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = tid / ACH + i * (NT / ACH);
       const int pix = pt * BKP + row;
       const int k = m0 + acc_ * 8;
-      const bool ok = pix < npix && k < g.K;
+      const bool ok = live && pix < npix && k < g.K;
       // select the address, load unconditionally (no exec-masked branch per row)
       ra[i] = *(const u32x4*)(ok ? dy + (size_t)pix * g.K + k : g.zero);
     }
@@ -81,11 +85,12 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
       const int n = udiv24(px, pq, rpq), rem = px - n * pq;
       const int p = udiv24(rem, g.Q, rq), q = rem - p * g.Q;
       const int h = p * g.stride - g.pad + xr, ww = q * g.stride - g.pad + xs;
-      const bool ok = pix < npix && jval && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+      const bool ok = live && pix < npix && jval && (unsigned)h < (unsigned)g.H &&
+                      (unsigned)ww < (unsigned)g.W;
       rb[i] = *(const u32x4*)(ok ? x + ((size_t)(n * g.H + h) * g.W + ww) * g.C + xc8 * 8 : g.zero);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, const u32x4 (&ra)[AR], const u32x4 (&rb)[BR]) {
     bf16* a = smem + buf * STAGE;
     bf16* b = a + BKP * LDA;
 #pragma unroll
@@ -108,44 +113,69 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
 
   const int g4 = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
-  if (pt0 < pt1) {
-    load_stage(pt0);
-    store_stage(0);
+  auto mma = [&](int buf) {
+    const bf16* a = smem + buf * STAGE;
+    const bf16* b = a + BKP * LDA;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 32 + 16 * h + 4 * g4 + tq;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const bf16x4 v = tr_read(a + row * LDA + wm * (BM / 2) + tm * 16 + 4 * tp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fa[tm][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const bf16x4 v = tr_read(b + row * LDB + wn * (BN / 2) + tn * 16 + 4 * tp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fb[tn][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+  if (pt0 < pt1 && PF == 1) {
+    u32x4 ra[AR], rb[BR];
+    load_stage(pt0, ra, rb);
+    store_stage(0, ra, rb);
     __syncthreads();
     int buf = 0;
     for (int pt = pt0; pt < pt1; ++pt) {
       const bool more = pt + 1 < pt1;
-      if (more) load_stage(pt + 1);
-      const bf16* a = smem + buf * STAGE;
-      const bf16* b = a + BKP * LDA;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fa[TM], fb[TN];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int row = kk * 32 + 16 * h + 4 * g4 + tq;
-#pragma unroll
-          for (int tm = 0; tm < TM; ++tm) {
-            const bf16x4 v = tr_read(a + row * LDA + wm * (BM / 2) + tm * 16 + 4 * tp);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fa[tm][4 * h + e] = v[e];
-          }
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) {
-            const bf16x4 v = tr_read(b + row * LDB + wn * (BN / 2) + tn * 16 + 4 * tp);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fb[tn][4 * h + e] = v[e];
-          }
-        }
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
-      }
-      if (more) store_stage(buf ^ 1);
+      if (more) load_stage(pt + 1, ra, rb);
+      mma(buf);
+      if (more) store_stage(buf ^ 1, ra, rb);
       __syncthreads();
       buf ^= 1;
+    }
+  } else if (pt0 < pt1) {
+    // two stages in flight in registers (the train-batch wgrad is latency-bound: a 64-pixel
+    // stage is ~8 MFMAs per wave, far shorter than a memory round trip), LDS double-buffered;
+    // unrolled by two so each register set is named statically
+    u32x4 ra0[AR], rb0[BR], ra1[AR], rb1[BR];
+    load_stage(pt0, ra0, rb0);
+    store_stage(0, ra0, rb0);
+    load_stage(pt0 + 1, ra1, rb1);
+    __syncthreads();
+    for (int pt = pt0; pt < pt1; pt += 2) {
+      load_stage(pt + 2, ra0, rb0);      // LDS 0 holds stage pt, ra1 stage pt + 1
+      mma(0);
+      if (pt + 1 >= pt1) break;
+      store_stage(1, ra1, rb1);
+      __syncthreads();
+      load_stage(pt + 3, ra1, rb1);      // LDS 1 holds stage pt + 1, ra0 stage pt + 2
+      mma(1);
+      if (pt + 2 >= pt1) break;
+      store_stage(0, ra0, rb0);
+      __syncthreads();
     }
   }
 

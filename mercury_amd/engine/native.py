@@ -34,7 +34,7 @@ from .. import ops
 from ..ops import hconv, tune
 from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plain_wins,
                         pgemm_plan, pgemm_pro_wins, pwconv_ok, pwconv_pro_wins, slab_bytes,
-                        wgrad_plan)
+                        stem_ok, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 from ..trainer import Trainer
@@ -177,6 +177,8 @@ class NativeEngine(object):
         self.use_pgemm = os.environ.get('MERCURY_PGEMM', '1') == '1'
         # narrow-input 1x1 convs with the input BN on the panel-resident kernel (pwconv.hip)
         self.use_pwconv = os.environ.get('MERCURY_PWCONV', '1') == '1'
+        # the first conv (<= 4 input channels) on the dense-k stem kernel (stem.hip)
+        self.use_stem = os.environ.get('MERCURY_STEM', '1') == '1'
         # depthwise convs take their input's BN + activation in their chunk loads
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
 
@@ -351,6 +353,8 @@ class NativeEngine(object):
                     if self.use_pgemm and pgemm_ok(sp) and u.b_seg is None:
                         m.plan[u.name, 'pgemm'] = pgemm_plan(sp)
                         coef = max(coef, m.G * 2 * sp.Cp)
+                    if self.use_stem and stem_ok(sp) and bi == 0 and u is blk.units[0]:
+                        m.plan[u.name, 'stem'] = True
                     if self.use_pwconv and pwconv_ok(sp) and u.b_seg is None:
                         m.plan[u.name, 'pwconv'] = True
                         coef = max(coef, m.G * 2 * sp.Cp)
@@ -450,6 +454,10 @@ class NativeEngine(object):
 
     def _conv_fwd(self, m, u, x, y, stats, pro=None):
         sp = m.spec[u.name]
+        if (u.name, 'stem') in m.plan and pro is None:
+            ops.stem_fwd(x, self.w_krsc[u.name], y, sp, stats=stats,
+                         bias=self._pview(u.b_seg) if u.b_seg is not None else None)
+            return
         if pro is not None and pro.get('pw'):
             ops.pwconv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, pro=pro)
             return

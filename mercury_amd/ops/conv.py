@@ -357,6 +357,35 @@ def pwconv_fwd(x, w, out, spec: ConvSpec, stats=None, pro=None):
     return out
 
 
+def stem_ok(spec: ConvSpec):
+    """First-layer conv for the dense-k stem kernel (csrc/stem.hip): <= 4 input channels (input
+    and weights padded to 8 in memory), 3x3 stride 1/2 or 7x7 stride 2, 32 or 64 outputs."""
+    return (spec.C <= 4 and spec.Cp == 8 and spec.R == spec.S and
+            (spec.R, spec.stride) in ((3, 1), (3, 2), (7, 2)) and spec.K in (32, 64))
+
+
+def stem_fwd(x, w, y, spec: ConvSpec, stats=None, bias=None):
+    """y[N][P][Q][K] = conv(x [N][H][W][8], w [K][R][R][8]) (+ bias) with the ghost-BN sums
+    ([G][2][K], groups of ``spec.group_rows`` output rows = whole images)."""
+    if not stem_ok(spec):
+        raise ValueError('stem: unsupported conv %s' % (spec,))
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * 8)
+    _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * 8)
+    _chk(y, torch.bfloat16, 'y', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    _chk(bias, torch.float32, 'bias', spec.K)
+    pq = spec.P * spec.Q
+    grp = spec.group_rows or spec.M
+    if grp % pq:
+        raise ValueError('stem: BN groups must be whole images')
+    ok = lib().stem_fwd(ptr(x), ptr(w), ptr(bias), ptr(y), ptr(stats), spec.N, spec.H, spec.W,
+                        spec.K, spec.R, spec.stride, spec.pad, spec.P, spec.Q, grp // pq,
+                        stream_ptr())
+    if not ok:
+        raise ValueError('stem: unsupported conv %s' % (spec,))
+    return y
+
+
 _NO_BW = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 0)
 _ACT = {None: 0, 'none': 0, 'relu': 1, 'relu6': 2}
 
