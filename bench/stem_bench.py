@@ -46,8 +46,9 @@ def main():
         slab = torch.zeros(max(1, slab_bytes(sp.M, K, *plan) // 4 + 1), device='cuda')
         t_ig = gtime(lambda: ops.conv_fwd(x, w, y, sp, stats=stats, slab=slab, plan=plan), reps=8)
         t_st = gtime(lambda: ops.stem_fwd(x, w, y, sp, stats=stats), reps=8)
+        t_ns = gtime(lambda: ops.stem_fwd(x, w, y, sp), reps=8)
         print(json.dumps(dict(stem=name, N=N, R=R, stride=st, K=K, igemm_us=round(t_ig, 1),
-                              stem_us=round(t_st, 1),
+                              stem_us=round(t_st, 1), stem_nostats_us=round(t_ns, 1),
                               stem_tfs=round(2.0 * sp.M * K * R * R * C / t_st / 1e6, 1),
                               stem_gbs=round((y.numel() * 2 + x.numel() * 2) / t_st / 1e3, 1))),
               flush=True)

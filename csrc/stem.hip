@@ -59,8 +59,8 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
     const int ks = t >> 3, ch = (t & 7) >> 1;
     *(st_u32x2*)(sw + (ks * K + k) * 64 + ((ch ^ ((k >> 1) & 3)) * 16) + (t & 1) * 8) = v;
   }
-  // per-lane LDS offsets of the two taps of each k-step (pixel-relative, in 8-byte units); a tap
-  // past the window reads the zero slot at the end of the window image
+  // per-lane LDS offsets of the two taps of each k-step (pixel-relative, in 8-byte units); -1
+  // marks a k-padding tap past R * R (contributes zeros)
   int toff[KS][2];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
@@ -84,17 +84,29 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
     for (int j = 0; j < 4; ++j) bias[kt][j] = a.bias ? a.bias[16 * kt + 4 * (lane >> 4) + j] : 0.f;
 
   const st_u32x2* xin = (const st_u32x2*)a.x + (size_t)n * a.H * a.W * 2;   // 16-byte pixels
+  // the next tile's input window is loaded into registers while this tile computes
+  constexpr int NPT = (PW * PW + ST_NT - 1) / ST_NT;
+  st_u32x2 pv[NPT];
+  auto load_window = [&](int t) {
+    const int p0 = (t / tq) * ST_T, q0 = (t % tq) * ST_T;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = tid + j * ST_NT;
+      const int r = i / PW, c = i - r * PW;
+      const int ih = p0 * S - a.pad + r, iw = q0 * S - a.pad + c;
+      const bool ok = i < PW * PW && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      pv[j] = ok ? xin[((size_t)ih * a.W + iw) * 2] : st_u32x2{0u, 0u};
+    }
+  };
+  if (t0 < t1) load_window(t0);
   for (int t = t0; t < t1; ++t) {
     const int p0 = (t / tq) * ST_T, q0 = (t % tq) * ST_T;
     __syncthreads();                                 // previous tile's window reads done
-    for (int i = tid; i < PW * PW; i += ST_NT) {
-      const int r = i / PW, c = i - r * PW;
-      const int ih = p0 * S - a.pad + r, iw = q0 * S - a.pad + c;
-      st_u32x2 v = {0u, 0u};
-      if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) v = xin[((size_t)ih * a.W + iw) * 2];
-      sp[i] = v;
-    }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j)
+      if (tid + j * ST_NT < PW * PW) sp[tid + j * ST_NT] = pv[j];
     __syncthreads();
+    if (t + 1 < t1) load_window(t + 1);
     f32x4 acc[4][KT];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -171,8 +183,9 @@ void stem_go(const StemArgs& a, int blocks, hipStream_t st) {
 int stem_fwd_launch(StemArgs a, hipStream_t st) {
   if (a.N <= 0 || a.P <= 0 || a.Q <= 0) return 1;
   const int tpi = ((a.P + ST_T - 1) / ST_T) * ((a.Q + ST_T - 1) / ST_T);
-  // enough blocks to fill the chip (~4 per CU), the rest as tiles per block
-  int tpb = (tpi * a.N) / 1024;
+  // many more blocks than CU slots (no tail round), the rest as tiles per block (each block
+  // flushes its BN sums once: fewer blocks per group, less atomic contention)
+  int tpb = (tpi * a.N) / 4096;
   tpb = tpb < 1 ? 1 : (tpb > tpi ? tpi : tpb);
   a.tpb = tpb;
   a.blocks_per_img = (tpi + tpb - 1) / tpb;

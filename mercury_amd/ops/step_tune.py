@@ -50,9 +50,9 @@ def coordinates(eng):
     out = {}
     for m in eng.modes.values():
         for (name, kind), _ in m.plan.items():
-            if kind in ('wgrad', 'hconv', 'hconv_bn', 'pgemm'):   # (halo-conv / pointwise-GEMM
-                continue                                          # plans: measured, not tuned)
-            if kind == 'fwd' and (name, 'hconv') in m.plan:
+            if kind not in ('fwd', 'dgrad'):      # (halo-conv / pointwise / stem plans:
+                continue                          # measured, not tuned; wgrad rides with dgrad)
+            if kind == 'fwd' and ((name, 'hconv') in m.plan or (name, 'stem') in m.plan):
                 continue                                  # (its igemm plan is never launched)
             sp = m.spec[name]
             ck = 'fwd' if kind == 'fwd' else 'bwd'
