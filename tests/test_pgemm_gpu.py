@@ -39,6 +39,9 @@ CASES = [
     (16, 14, 14, 64, 256, 1, 4, 0, 0),
     (10, 10, 10, 96, 200, 1, 2, 0, 0),         # 200-row groups: blocks straddle group edges
     (9, 7, 13, 128, 512, 1, 3, 0, 0),
+    # large M: 200-row groups (every other 128-row panel straddles a group edge), 16384-row groups
+    (2700, 10, 20, 32, 96, 1, 1, 0, 0),
+    (128, 64, 64, 64, 128, 1, 4, 0, 0),
 ]
 
 
@@ -53,13 +56,13 @@ def test_pgemm_matches_torch(case, kern):
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, st, gimgs, bn, grid = case
-    if kern == 'pwconv' and not _pw_ok(C, st):
+    if kern.startswith('pwconv') and not _pw_ok(C, st):
         pytest.skip('not a pwconv shape')
     if kern == 'pgemm' and bn == 0:
         pytest.skip('pwconv-only case')
 
     def run(xn, wk, out, spec, stats=None):
-        if kern == 'pwconv':
+        if kern.startswith('pwconv'):
             return ops.pwconv_fwd(xn, wk, out, spec, stats=stats)
         return ops.pgemm_fwd(xn, wk, out, spec, stats=stats, bn=bn, grid=grid)
     g = torch.Generator(device='cpu').manual_seed(hash(case) % 1000)
@@ -80,10 +83,9 @@ def test_pgemm_matches_torch(case, kern):
     close(got, ref)
     rb = bf(ref)
     per = gimgs or N
-    for gi in range(G):
-        r = rb[gi * per:(gi + 1) * per]
-        close(stats[gi, 0], r.sum((0, 2, 3)), rtol=1e-2, atol=0.5)
-        close(stats[gi, 1], r.pow(2).sum((0, 2, 3)), rtol=1e-2, atol=0.5)
+    r = rb.view(G, per, K, spec.P, spec.Q)
+    close(stats[:, 0], r.sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+    close(stats[:, 1], r.pow(2).sum((1, 3, 4)), rtol=1e-2, atol=0.5)
     # no stats: plain GEMM path, bitwise equal output
     out2 = torch.empty_like(out)
     run(xn, wk, out2, spec)
@@ -101,6 +103,7 @@ PRO_CASES = [
     (16, 14, 14, 64, 256, 4, 64, 'relu', False, False),     # R50 conv3: 64 -> 256, 4 N-tiles
     (9, 10, 10, 128, 520, 3, 64, 'relu', False, False),     # 300-row groups, N % 64 != 0
     (6, 12, 12, 96, 576, 0, 64, 'relu6', False, True),      # MobileNetV2 expand, eval
+    (2700, 10, 20, 32, 96, 1, 0, 'relu6', False, False),    # large M, 200-row groups
 ]
 
 
@@ -113,8 +116,10 @@ def test_pgemm_input_bn_prologue(case, kern):
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, gimgs, bn, act, resid, ev = case
-    if kern == 'pwconv' and not _pw_ok(C, 1, resid):
+    if kern.startswith('pwconv') and not _pw_ok(C, 1, resid):
         pytest.skip('not a pwconv shape')
+    if kern == 'pgemm' and bn == 0:
+        pytest.skip('pwconv-only case')
     g = torch.Generator(device='cpu').manual_seed(7 + C + K)
     rows = N * H * W
     y = bf(torch.randn(rows, C, generator=g) * 2 + 0.5).to(DEV)
@@ -156,7 +161,7 @@ def test_pgemm_input_bn_prologue(case, kern):
         pro.update(stats=stats.reshape(-1))
     out = torch.empty(rows, K, dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV)
-    if kern == 'pwconv':
+    if kern.startswith('pwconv'):
         ops.pwconv_fwd(yb, wk, out, spec, stats=ostats, pro=pro)
     else:
         ops.pgemm_fwd(yb, wk, out, spec, stats=ostats, bn=bn, pro=pro)
@@ -168,7 +173,10 @@ def test_pgemm_input_bn_prologue(case, kern):
                  res=rb)
     out2 = torch.empty_like(out)
     ostats2 = torch.zeros_like(ostats)
-    ops.pgemm_fwd(an, wk, out2, spec, stats=ostats2, bn=bn)
+    if kern.startswith('pwconv'):
+        ops.pwconv_fwd(an, wk, out2, spec, stats=ostats2)
+    else:
+        ops.pgemm_fwd(an, wk, out2, spec, stats=ostats2, bn=bn)
     close(out, out2, rtol=1e-2, atol=1e-2)
     close(ostats, ostats2, rtol=1e-2, atol=0.5)
     assert not torch.isnan(keep.float()).any()
