@@ -495,9 +495,13 @@ PYBIND11_MODULE(_C, m) {
     return ok;
   });
   m.def("dwconv_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int H, int W, int C,
-                           int Pp, int Q, int stride, int pad, uintptr_t st) {
+                           int Pp, int Q, int stride, int pad, uintptr_t st, uintptr_t bw_out,
+                           uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_sums,
+                           float bw_inv_count, float bw_eps, int bw_act) {
+    const DwBw bw{P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats),
+                  P<float>(bw_sums), bw_inv_count, bw_eps, bw_act};
     dwconv_dgrad_launch(P<const bf16>(dy), P<const float>(w), P<bf16>(dx), N, H, W, C, Pp, Q, stride,
-                        pad, S(st));
+                        pad, S(st), bw_sums ? &bw : nullptr);
     check_launch("dwconv_dgrad");
   });
   m.def("dwconv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C,

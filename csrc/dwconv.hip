@@ -10,9 +10,10 @@
 //           block, one global atomic per channel per block (ghost-BN groups respected).
 //   dgrad : the same strip shape over the input grid (stride 1: a correlation with the flipped
 //           taps through a sliding dy window; stride 2: parity-filtered gather).
-//   wgrad : one thread per (image, output row, chunk) walks the row with a sliding 3x3 input
-//           window (3 new loads per output at stride 1), 72 fp32 accumulators in registers, then
-//           LDS reduction across the block and one global atomic per (channel, tap) per block.
+//   wgrad : one thread per (image, output row, column segment, chunk) walks its columns with a
+//           sliding 3x3 input window (3 new loads per output at stride 1), 72 fp32 accumulators
+//           in registers, then LDS reduction across the block and one global atomic per
+//           (channel, tap) per block.
 //
 // Thread index -> (chunk fastest, then strip, row, image): adjacent lanes touch adjacent 16 B
 // chunks of the same pixel, so every wave access is a contiguous run of the NHWC row.
@@ -184,70 +185,127 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
   }
 }
 
-template <int S>
+MA_DEV float dw_mask(float out, int act) {       // (bn.hip act_mask)
+  if (act == 1) return out > 0.f ? 1.f : 0.f;
+  if (act == 2) return (out > 0.f && out < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+// BW: the dgrad also reduces the BN-backward sums of the BN feeding this conv (what
+// bn_bwd_reduce would do in a separate pass over dx, out and y): dz = dx * act'(out),
+// sums += (dz, dz * xhat), block-reduced through padded LDS rows, one atomic pair per channel.
+template <int S, bool BW>
 __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const float* w, bf16* dx, int N,
-                                                      int H, int W, int C, int P, int Q, int pad) {
+                                                      int H, int W, int C, int P, int Q, int pad,
+                                                      DwBw bw) {
+  extern __shared__ float part[];  // BW: [DT][ST_LD] per-thread (sum dz, sum dz * xhat)
   const int C8 = C >> 3, WS = (W + DWL - 1) / DWL;
   const int total = N * H * WS * C8;
   const int gt = blockIdx.x * DT + threadIdx.x;
-  if (gt >= total) return;
-  const int c8 = gt % C8;
-  int r = gt / C8;
-  const int ws = r % WS;
-  r /= WS;
-  const int h = r % H, n = r / H;
-  float wr[9][8];
-  load_w72(w, c8, wr);
-  const int x0 = ws * DWL;
-  float acc[DWL][8];
+  float sdz[8], sx[8];
 #pragma unroll
-  for (int o = 0; o < DWL; ++o)
+  for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = 0.f;
+  if (gt < total) {
+    const int c8 = gt % C8;
+    int r = gt / C8;
+    const int ws = r % WS;
+    r /= WS;
+    const int h = r % H, n = r / H;
+    float wr[9][8];
+    load_w72(w, c8, wr);
+    const int x0 = ws * DWL;
+    float acc[DWL][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+    for (int o = 0; o < DWL; ++o)
 #pragma unroll
-  for (int rr = 0; rr < 3; ++rr) {
-    const int hp = h + pad - rr;
-    if (S == 1) {
-      if (hp >= 0 && hp < P) {
-        const bf16* row = dy + (size_t)(n * P + hp) * Q * C + c8 * 8;
-        bf16x8 col[DWL + 2];  // dy columns x0+pad-2 .. x0+DWL-1+pad
+      for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
 #pragma unroll
-        for (int j = 0; j < DWL + 2; ++j) {
-          const int q = x0 + pad - 2 + j;
-          col[j] = ld8(row + (size_t)q * C, q >= 0 && q < Q);
-        }
+    for (int rr = 0; rr < 3; ++rr) {
+      const int hp = h + pad - rr;
+      if (S == 1) {
+        if (hp >= 0 && hp < P) {
+          const bf16* row = dy + (size_t)(n * P + hp) * Q * C + c8 * 8;
+          bf16x8 col[DWL + 2];  // dy columns x0+pad-2 .. x0+DWL-1+pad
 #pragma unroll
-        for (int o = 0; o < DWL; ++o)
-#pragma unroll
-          for (int t = 0; t < 3; ++t)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o + 2 - t][k]) * wr[rr * 3 + t][k];
-      }
-    } else {
-      if (hp >= 0 && (hp % S) == 0 && hp / S < P) {
-        const bf16* row = dy + (size_t)(n * P + hp / S) * Q * C + c8 * 8;
-#pragma unroll
-        for (int o = 0; o < DWL; ++o)
-#pragma unroll
-          for (int t = 0; t < 3; ++t) {
-            const int wp = x0 + o + pad - t;
-            if (wp >= 0 && (wp % S) == 0 && wp / S < Q) {
-              const bf16x8 v = *(const bf16x8*)(row + (size_t)(wp / S) * C);
-#pragma unroll
-              for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(v[k]) * wr[rr * 3 + t][k];
-            }
+          for (int j = 0; j < DWL + 2; ++j) {
+            const int q = x0 + pad - 2 + j;
+            col[j] = ld8(row + (size_t)q * C, q >= 0 && q < Q);
           }
+#pragma unroll
+          for (int o = 0; o < DWL; ++o)
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o + 2 - t][k]) * wr[rr * 3 + t][k];
+        }
+      } else {
+        if (hp >= 0 && (hp % S) == 0 && hp / S < P) {
+          const bf16* row = dy + (size_t)(n * P + hp / S) * Q * C + c8 * 8;
+#pragma unroll
+          for (int o = 0; o < DWL; ++o)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+              const int wp = x0 + o + pad - t;
+              if (wp >= 0 && (wp % S) == 0 && wp / S < Q) {
+                const bf16x8 v = *(const bf16x8*)(row + (size_t)(wp / S) * C);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(v[k]) * wr[rr * 3 + t][k];
+              }
+            }
+        }
+      }
+    }
+    const size_t rowoff = (size_t)(n * H + h) * W * C + c8 * 8;
+    float mean[8], rstd[8];
+    if constexpr (BW) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mean[k] = bw.stats[c8 * 8 + k] * bw.inv_count;
+        rstd[k] = rsqrtf(fmaxf(bw.stats[C + c8 * 8 + k] * bw.inv_count - mean[k] * mean[k], 0.f) +
+                         bw.eps);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < DWL; ++o) {
+      if (x0 + o < W) {
+        bf16x8 v;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = f2bf(acc[o][k]);
+        *(bf16x8*)(dx + rowoff + (size_t)(x0 + o) * C) = v;
+        if constexpr (BW) {
+          const bf16x8 ov = *(const bf16x8*)(bw.out + rowoff + (size_t)(x0 + o) * C);
+          const bf16x8 yv = *(const bf16x8*)(bw.y + rowoff + (size_t)(x0 + o) * C);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float dz = bf2f(v[k]) * dw_mask(bf2f(ov[k]), bw.act);
+            sdz[k] += dz;
+            sx[k] += dz * (bf2f(yv[k]) - mean[k]) * rstd[k];
+          }
+        }
       }
     }
   }
-  bf16* xrow = dx + (size_t)(n * H + h) * W * C + c8 * 8;
+  if constexpr (BW) {
+    float* mine = part + threadIdx.x * ST_LD;
 #pragma unroll
-  for (int o = 0; o < DWL; ++o) {
-    if (x0 + o < W) {
-      bf16x8 v;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = f2bf(acc[o][k]);
-      *(bf16x8*)(xrow + (size_t)(x0 + o) * C) = v;
+    for (int k = 0; k < 8; ++k) {
+      mine[k] = sdz[k];
+      mine[8 + k] = sx[k];
+    }
+    __syncthreads();
+    const int g0 = blockIdx.x * DT;
+    const int nthr = min(DT, total - g0), off = g0 % C8;
+    for (int c = threadIdx.x; c < C; c += DT) {
+      const int j0 = ((c >> 3) - off + C8) % C8;
+      float v0 = 0.f, v1 = 0.f;
+      for (int j = j0; j < nthr; j += C8) {
+        v0 += part[j * ST_LD + (c & 7)];
+        v1 += part[j * ST_LD + 8 + (c & 7)];
+      }
+      if (v0 != 0.f || v1 != 0.f) {
+        atomicAdd(bw.sums + c, v0);
+        atomicAdd(bw.sums + C + c, v1);
+      }
     }
   }
 }
@@ -259,12 +317,17 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
 // and adds 9C values into dw: no LDS atomics (the per-thread LDS atomic adds serialised on
 // the ~256/C8 threads sharing a channel).
 constexpr int WG_LD = 73;   // floats per thread row (odd: conflict-free row writes)
+// A row is split into QS column segments of QL columns (one thread each): the serial walk --
+// one memory round trip per column -- is QS x shorter and the grid QS x larger (the train-batch
+// layers otherwise launch 48-100 blocks whose threads each walk 32 dependent columns).
 template <int S>
 __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
-                                                      int H, int W, int C, int P, int Q, int pad) {
+                                                      int H, int W, int C, int P, int Q, int pad,
+                                                      int QS) {
   extern __shared__ float part[];  // [DT][WG_LD]
   const int C8 = C >> 3;
-  const int total = N * P * C8;
+  const int total = N * P * QS * C8;
+  const int QL = (Q + QS - 1) / QS;
   const int gt = blockIdx.x * DT + threadIdx.x;
   float acc[9][8];
 #pragma unroll
@@ -273,8 +336,11 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
     for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
   if (gt < total) {
     const int c8 = gt % C8;
-    const int r = gt / C8;
+    int r = gt / C8;
+    const int seg = r % QS;
+    r /= QS;
     const int p = r % P, n = r / P;
+    const int q0 = seg * QL, q1 = min(q0 + QL, Q);
     const bf16* rows[3];
     bool rok[3];
 #pragma unroll
@@ -289,16 +355,16 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
     for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const int ww = -pad + t;
-        win[rr][t] = ld8(rows[rr] + (size_t)ww * C, rok[rr] && ww >= 0 && ww < W);
+        const int ww = q0 * S - pad + t;
+        win[rr][t] = ld8(rows[rr] + (size_t)ww * C, q0 < q1 && rok[rr] && ww >= 0 && ww < W);
       }
     const bf16* grow = dy + (size_t)(n * P + p) * Q * C + c8 * 8;
-    bf16x8 g = *(const bf16x8*)grow;
-    for (int q = 0; q < Q; ++q) {
+    bf16x8 g = ld8(grow + (size_t)q0 * C, q0 < q1);
+    for (int q = q0; q < q1; ++q) {
       // column q+1's loads first
       bf16x8 n1[3], n2[3], ng = g;
       const int base = (q + 1) * S - pad;
-      const bool more = q + 1 < Q;
+      const bool more = q + 1 < q1;
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         if (S == 2) n1[rr] = ld8(rows[rr] + (size_t)(base + 1) * C, more && rok[rr] && base + 1 >= 0 && base + 1 < W);
@@ -332,7 +398,7 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
     for (int k = 0; k < 8; ++k) mine[t * 8 + k] = acc[t][k];
   __syncthreads();
   // output (tap t, channel c): the threads of chunk c/8 are j0, j0 + C8, ... (gt = base + j)
-  const int nthr = min(DT, total - (int)blockIdx.x * DT);
+  const int nthr = min(DT, total - (int)blockIdx.x * DT);   // (c8 stays the fastest index)
   const int off = (int)(((long long)blockIdx.x * DT) % C8);
   for (int i = threadIdx.x; i < 9 * C; i += DT) {
     const int c = i % C, t = i / C;
@@ -359,17 +425,29 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   }
 }
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int P,
-                         int Q, int stride, int pad, hipStream_t st) {
+                         int Q, int stride, int pad, hipStream_t st, const DwBw* bw) {
   const long long total = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
   const dim3 grid((unsigned)((total + DT - 1) / DT));
-  if (stride == 1)
-    hipLaunchKernelGGL(dw_dgrad_kernel<1>, grid, dim3(DT), 0, st, dy, w, dx, N, H, W, C, P, Q, pad);
-  else
-    hipLaunchKernelGGL(dw_dgrad_kernel<2>, grid, dim3(DT), 0, st, dy, w, dx, N, H, W, C, P, Q, pad);
+  const DwBw none{};
+  const size_t shm = bw ? (size_t)DT * ST_LD * sizeof(float) : 0;
+#define DW_DG(S_, BW_) hipLaunchKernelGGL((dw_dgrad_kernel<S_, BW_>), grid, dim3(DT), shm, st, dy, w, \
+                                          dx, N, H, W, C, P, Q, pad, bw ? *bw : none)
+  if (stride == 1) {
+    if (bw) DW_DG(1, true);
+    else DW_DG(1, false);
+  } else {
+    if (bw) DW_DG(2, true);
+    else DW_DG(2, false);
+  }
+#undef DW_DG
 }
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,
                          int Q, int stride, int pad, hipStream_t st) {
-  const long long total = (long long)N * P * (C / 8);
+  // column segments: enough threads for ~4 waves per CU, segments of >= 4 columns
+  const long long rows = (long long)N * P * (C / 8);
+  int QS = 1;
+  while (rows * QS < 256LL * 4 * 64 && (Q + 2 * QS - 1) / (2 * QS) >= 4) QS *= 2;
+  const long long total = rows * QS;
   const dim3 grid((unsigned)((total + DT - 1) / DT));
   const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // 73 KB: above the 64 KB default
   static const bool attr = [] {
@@ -381,7 +459,9 @@ void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H,
   }();
   (void)attr;
   if (stride == 1)
-    hipLaunchKernelGGL(dw_wgrad_kernel<1>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad);
+    hipLaunchKernelGGL(dw_wgrad_kernel<1>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad,
+                       QS);
   else
-    hipLaunchKernelGGL(dw_wgrad_kernel<2>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad);
+    hipLaunchKernelGGL(dw_wgrad_kernel<2>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad,
+                       QS);
 }

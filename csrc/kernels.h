@@ -271,8 +271,17 @@ struct StemArgs {                 // first conv: <= 4 input channels packed dens
   int tpb, blocks_per_img;        // set by the launcher
 };
 int stem_fwd_launch(StemArgs a, hipStream_t st);
+struct DwBw {                      // BN-backward reduce fused into the depthwise dgrad
+  const bf16* out;                 // activation act(bn(y)) of the BN feeding the dw conv (mask)
+  const bf16* y;                   // that BN's input
+  const float* stats;              // its batch sums [2][C]
+  float* sums;                     // += (sum dz, sum dz * xhat) [3][C] (zeroed by the engine)
+  float inv_count, eps;
+  int act;
+};
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
-                         int P, int Q, int stride, int pad, hipStream_t st);
+                         int P, int Q, int stride, int pad, hipStream_t st,
+                         const DwBw* bw = nullptr);
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
                          int P, int Q, int stride, int pad, hipStream_t st);
 void nchw_to_nhwc8_launch(const float* x, bf16* y, int N, int C, int H, int W, int Cpad,

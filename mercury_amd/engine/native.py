@@ -746,11 +746,16 @@ class NativeEngine(object):
             return bw is not None
         self._wgrad(m, u, dy, x)
         if u.depthwise:
-            if dx is not None:
-                assert not accumulate
-                ops.dwconv_dgrad(dy, self._pview(u.w_seg), dx, sp.N, sp.H, sp.W, sp.C, sp.P,
-                                 sp.Q, sp.stride, sp.pad)
-            return False
+            if dx is None:
+                return False
+            assert not accumulate
+            # the producer's BN-backward sums reduced in the depthwise dgrad (no bn_bwd reduce
+            # pass; one batch group in train mode, no shortcut BN)
+            if bw is not None and (not self.fuse_bn_bwd or bw.get('y2') is not None):
+                bw = None
+            ops.dwconv_dgrad(dy, self._pview(u.w_seg), dx, sp.N, sp.H, sp.W, sp.C, sp.P,
+                             sp.Q, sp.stride, sp.pad, bw=bw)
+            return bw is not None
         if dx is not None:
             if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
                 bw = None

@@ -82,8 +82,22 @@ def dwconv_fwd(x, w, y, N, H, W, C, P, Q, stride, pad, stats=None, group_rows=0,
                      group_rows or N * P * Q, stream_ptr(), *pa)
 
 
-def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad):
-    lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr())
+def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
+    """Depthwise 3x3 data gradient.  ``bw``: dict(out=, y=, stats=[2][C], sums=[3][C], act=,
+    eps=) -- also reduce the BN-backward sums of the BN feeding this conv (its activation
+    ``out``, input ``y``), as bn_bwd's reduce pass would (one batch group)."""
+    ba = (0, 0, 0, 0, 0.0, 0.0, 0)
+    if bw is not None:
+        n_in = N * H * W * C
+        for k in ('out', 'y'):
+            _chk(bw[k], torch.bfloat16, 'bw.' + k, n_in)
+        _chk(bw['stats'], torch.float32, 'bw.stats', 2 * C)
+        _chk(bw['sums'], torch.float32, 'bw.sums', 3 * C)
+        if bw.get('y2') is not None:
+            raise ValueError('dwconv_dgrad: no shortcut-BN reduce')
+        ba = (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw['sums']),
+              1.0 / (N * H * W), float(bw.get('eps', 1e-5)), _ACT[bw.get('act')])
+    lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr(), *ba)
 
 
 def dwconv_wgrad(dy, x, dw, N, H, W, C, P, Q, stride, pad):

@@ -968,3 +968,36 @@ def test_dwconv_input_bn_prologue_matches_bn_apply_then_dw(stride, ghost):
     close(out, ref, rtol=1e-2, atol=1e-2)
     assert not torch.isnan(keep.float()).any()
     close(keep, a, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('case', [(8, 96, 16, 16, 1, 'relu6'), (8, 144, 15, 15, 2, 'relu6'),
+                                  (4, 960, 4, 4, 1, 'relu6'), (6, 40, 5, 11, 1, 'relu'),
+                                  (3, 16, 7, 9, 2, 'none')])
+def test_dwconv_dgrad_fused_bn_backward_reduce(case):
+    """The depthwise dgrad with bw= reduces the feeding BN's backward sums exactly like
+    bn_bwd's reduce pass over the same dx (MobileNetV2's expand BN + ReLU6 -> dw conv)."""
+    ops = _ops()
+    N, C, H, W, st, act = case
+    torch.manual_seed(3)
+    M = N * H * W
+    y = bf(torch.randn(M, C, device=DEV) * 1.5 + 0.3).to(torch.bfloat16)
+    yf = y.float()
+    stats = torch.stack([yf.sum(0), yf.pow(2).sum(0)]).contiguous()        # [2][C]
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.2
+    out = torch.empty_like(y)
+    ops.bn_apply(y, stats.reshape(-1), gamma, beta, out, M, C, act=act)
+    P, Q = (H - 1) // st + 1, (W - 1) // st + 1
+    gy = bf(torch.randn(N, P, Q, C, device=DEV)).to(torch.bfloat16)
+    wf = torch.randn(C, 9, device=DEV)
+    dx = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ops.dwconv_dgrad(gy, wf, dx, N, H, W, C, P, Q, st, 1)
+    dx2 = torch.empty_like(dx)
+    sums = torch.zeros(3, C, device=DEV)
+    ops.dwconv_dgrad(gy, wf, dx2, N, H, W, C, P, Q, st, 1,
+                     bw=dict(out=out, y=y, stats=stats, sums=sums, act=act, eps=1e-5))
+    assert torch.equal(dx, dx2)
+    ref = torch.zeros(3, C, device=DEV)
+    scratch = torch.empty_like(y)
+    ops.bn_bwd(dx, out, y, stats.reshape(-1), gamma, ref, scratch, M, C, act=act, eps=1e-5)
+    close(sums[:2], ref[:2], 2e-3, 1e-2)
