@@ -494,6 +494,9 @@ PYBIND11_MODULE(_C, m) {
     check_launch("stem_fwd");
     return ok;
   });
+  m.def("dwconv_wgrad_slab_floats", [](int N, int Pp, int Q, int C) {
+    return (long long)dwconv_wgrad_slab_floats(N, Pp, Q, C);
+  });
   m.def("dwconv_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int H, int W, int C,
                            int Pp, int Q, int stride, int pad, uintptr_t st, uintptr_t bw_out,
                            uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_sums,
@@ -505,9 +508,10 @@ PYBIND11_MODULE(_C, m) {
     check_launch("dwconv_dgrad");
   });
   m.def("dwconv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C,
-                           int Pp, int Q, int stride, int pad, uintptr_t st) {
+                           int Pp, int Q, int stride, int pad, uintptr_t st, uintptr_t slab,
+                           long long slab_floats) {
     dwconv_wgrad_launch(P<const bf16>(dy), P<const bf16>(x), P<float>(dw), N, H, W, C, Pp, Q, stride,
-                        pad, S(st));
+                        pad, S(st), P<float>(slab), (size_t)slab_floats);
     check_launch("dwconv_wgrad");
   });
   m.def("nchw_to_nhwc8", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int Cpad,

@@ -10,10 +10,12 @@
 //           block, one global atomic per channel per block (ghost-BN groups respected).
 //   dgrad : the same strip shape over the input grid (stride 1: a correlation with the flipped
 //           taps through a sliding dy window; stride 2: parity-filtered gather).
-//   wgrad : one thread per (image, output row, column segment, chunk) walks its columns with a
-//           sliding 3x3 input window (3 new loads per output at stride 1), 72 fp32 accumulators
-//           in registers, then LDS reduction across the block and one global atomic per
-//           (channel, tap) per block.
+//   wgrad : one thread per (image, output row, chunk) walks the row with a sliding 3x3 input
+//           window (3 new loads per output at stride 1), 72 fp32 accumulators in registers, then
+//           LDS reduction across the block and one global atomic per (channel, tap) per block.
+//           With a slab the rows are split into column segments (shorter serial walks, a
+//           larger grid) and a second kernel sums the blocks' partials: with atomics the
+//           split measured slower (382 -> 568 us/step on MobileNetV2, the atomics contend).
 //
 // Thread index -> (chunk fastest, then strip, row, image): adjacent lanes touch adjacent 16 B
 // chunks of the same pixel, so every wave access is a contiguous run of the NHWC row.
@@ -202,18 +204,44 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
   const int C8 = C >> 3, WS = (W + DWL - 1) / DWL;
   const int total = N * H * WS * C8;
   const int gt = blockIdx.x * DT + threadIdx.x;
+  // BW: a capped grid walks the strips (stride a multiple of C8: a thread keeps its channels),
+  // so fewer blocks add their sums -- the per-channel atomics are what contends
+  const int T = gridDim.x * DT, stride = BW ? T - T % C8 : T;
+  const int lim = min(total, stride);
   float sdz[8], sx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) sdz[k] = sx[k] = 0.f;
-  if (gt < total) {
-    const int c8 = gt % C8;
-    int r = gt / C8;
+  float wr[9][8];
+  float mean[8], rstd[8];
+  const int c8 = gt % C8;
+  if (gt < lim) {
+    load_w72(w, c8, wr);
+    if constexpr (BW) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mean[k] = bw.stats[c8 * 8 + k] * bw.inv_count;
+        rstd[k] = rsqrtf(fmaxf(bw.stats[C + c8 * 8 + k] * bw.inv_count - mean[k] * mean[k], 0.f) +
+                         bw.eps);
+      }
+    }
+  }
+  for (int gi = gt; gi < total && gt < lim; gi += stride) {
+    int r = gi / C8;
     const int ws = r % WS;
     r /= WS;
     const int h = r % H, n = r / H;
-    float wr[9][8];
-    load_w72(w, c8, wr);
     const int x0 = ws * DWL;
+    const size_t rowoff = (size_t)(n * H + h) * W * C + c8 * 8;
+    // BW: the mask / BN-input chunks of the strip are requested with the dy loads
+    bf16x8 ov[DWL], yv[DWL];
+    if constexpr (BW) {
+#pragma unroll
+      for (int o = 0; o < DWL; ++o) {
+        const bool in = x0 + o < W;
+        ov[o] = ld8(bw.out + rowoff + (size_t)(x0 + o) * C, in);
+        yv[o] = ld8(bw.y + rowoff + (size_t)(x0 + o) * C, in);
+      }
+    }
     float acc[DWL][8];
 #pragma unroll
     for (int o = 0; o < DWL; ++o)
@@ -255,16 +283,6 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
         }
       }
     }
-    const size_t rowoff = (size_t)(n * H + h) * W * C + c8 * 8;
-    float mean[8], rstd[8];
-    if constexpr (BW) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        mean[k] = bw.stats[c8 * 8 + k] * bw.inv_count;
-        rstd[k] = rsqrtf(fmaxf(bw.stats[C + c8 * 8 + k] * bw.inv_count - mean[k] * mean[k], 0.f) +
-                         bw.eps);
-      }
-    }
 #pragma unroll
     for (int o = 0; o < DWL; ++o) {
       if (x0 + o < W) {
@@ -273,13 +291,11 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
         for (int k = 0; k < 8; ++k) v[k] = f2bf(acc[o][k]);
         *(bf16x8*)(dx + rowoff + (size_t)(x0 + o) * C) = v;
         if constexpr (BW) {
-          const bf16x8 ov = *(const bf16x8*)(bw.out + rowoff + (size_t)(x0 + o) * C);
-          const bf16x8 yv = *(const bf16x8*)(bw.y + rowoff + (size_t)(x0 + o) * C);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float dz = bf2f(v[k]) * dw_mask(bf2f(ov[k]), bw.act);
+            const float dz = bf2f(v[k]) * dw_mask(bf2f(ov[o][k]), bw.act);
             sdz[k] += dz;
-            sx[k] += dz * (bf2f(yv[k]) - mean[k]) * rstd[k];
+            sx[k] += dz * (bf2f(yv[o][k]) - mean[k]) * rstd[k];
           }
         }
       }
@@ -294,7 +310,7 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
     }
     __syncthreads();
     const int g0 = blockIdx.x * DT;
-    const int nthr = min(DT, total - g0), off = g0 % C8;
+    const int nthr = min(DT, lim - g0), off = g0 % C8;
     for (int c = threadIdx.x; c < C; c += DT) {
       const int j0 = ((c >> 3) - off + C8) % C8;
       float v0 = 0.f, v1 = 0.f;
@@ -323,7 +339,7 @@ constexpr int WG_LD = 73;   // floats per thread row (odd: conflict-free row wri
 template <int S>
 __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
                                                       int H, int W, int C, int P, int Q, int pad,
-                                                      int QS) {
+                                                      int QS, float* slab) {
   extern __shared__ float part[];  // [DT][WG_LD]
   const int C8 = C >> 3;
   const int total = N * P * QS * C8;
@@ -405,7 +421,31 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
     const int j0 = ((c >> 3) - off + C8) % C8;
     float v = 0.f;
     for (int j = j0; j < nthr; j += C8) v += part[j * WG_LD + t * 8 + (c & 7)];
-    if (v != 0.f) atomicAdd(&dw[c * 9 + t], v);
+    // slab: this block's partials, summed by dw_wgrad_reduce_kernel (no contended atomics)
+    if (slab) slab[(size_t)blockIdx.x * 9 * C + i] = v;
+    else if (v != 0.f) atomicAdd(&dw[c * 9 + t], v);
+  }
+}
+
+// dw[c][t] += sum over the wgrad blocks of their partials (slab [blocks][9][C], i = t*C + c).
+// A block sums 64 outputs over a 1/gridDim.y share of the partials (4 sub-shares per output,
+// reduced in LDS), then one atomic per output: gridDim.y-way instead of blocks-way contention,
+// and a short (blocks / (4 gridDim.y)) load chain per thread.
+__global__ __launch_bounds__(DT) void dw_wgrad_reduce_kernel(const float* slab, float* dw, int C,
+                                                             int nblk) {
+  __shared__ float red[4][64];
+  const int n9 = 9 * C;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int share = (nblk + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * share, b1 = min(nblk, b0 + share);
+  float v = 0.f;
+  if (i < n9)
+    for (int b = b0 + sub; b < b1; b += 4) v += slab[(size_t)b * n9 + i];
+  red[sub][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (sub == 0 && i < n9) {
+    const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    if (t != 0.f) atomicAdd(&dw[(i % C) * 9 + i / C], t);
   }
 }
 }  // namespace
@@ -427,7 +467,10 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int P,
                          int Q, int stride, int pad, hipStream_t st, const DwBw* bw) {
   const long long total = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
-  const dim3 grid((unsigned)((total + DT - 1) / DT));
+  // BW: at most ~one block per CU (each adds 2C atomics; C8 <= DT keeps a block's chunks whole)
+  long long blocks = (total + DT - 1) / DT;
+  if (bw && blocks > 256) blocks = 256;
+  const dim3 grid((unsigned)blocks);
   const DwBw none{};
   const size_t shm = bw ? (size_t)DT * ST_LD * sizeof(float) : 0;
 #define DW_DG(S_, BW_) hipLaunchKernelGGL((dw_dgrad_kernel<S_, BW_>), grid, dim3(DT), shm, st, dy, w, \
@@ -441,12 +484,25 @@ void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H,
   }
 #undef DW_DG
 }
-void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,
-                         int Q, int stride, int pad, hipStream_t st) {
-  // column segments: enough threads for ~4 waves per CU, segments of >= 4 columns
+size_t dwconv_wgrad_slab_floats(int N, int P, int Q, int C) {
   const long long rows = (long long)N * P * (C / 8);
   int QS = 1;
   while (rows * QS < 256LL * 4 * 64 && (Q + 2 * QS - 1) / (2 * QS) >= 4) QS *= 2;
+  return (size_t)((rows * QS + DT - 1) / DT) * 9 * C;
+}
+
+void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,
+                         int Q, int stride, int pad, hipStream_t st, float* slab,
+                         size_t slab_floats) {
+  // column segments: enough threads for ~4 waves per CU, segments of >= 4 columns; with a slab
+  // (>= dwconv_wgrad_slab_floats) the blocks' partials are summed by a second small kernel
+  // instead of contended atomics (each of the 100s of blocks adds every (channel, tap))
+  const long long rows = (long long)N * P * (C / 8);
+  int QS = 1;
+  if (slab && slab_floats >= dwconv_wgrad_slab_floats(N, P, Q, C))
+    while (rows * QS < 256LL * 4 * 64 && (Q + 2 * QS - 1) / (2 * QS) >= 4) QS *= 2;
+  else
+    slab = nullptr;
   const long long total = rows * QS;
   const dim3 grid((unsigned)((total + DT - 1) / DT));
   const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // 73 KB: above the 64 KB default
@@ -460,8 +516,13 @@ void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H,
   (void)attr;
   if (stride == 1)
     hipLaunchKernelGGL(dw_wgrad_kernel<1>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad,
-                       QS);
+                       QS, slab);
   else
     hipLaunchKernelGGL(dw_wgrad_kernel<2>, grid, dim3(DT), shm, st, dy, x, dw, N, H, W, C, P, Q, pad,
-                       QS);
+                       QS, slab);
+  if (slab) {
+    const int shares = grid.x >= 128 ? 8 : (grid.x >= 32 ? 4 : 1);
+    hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((9 * C + 63) / 64, shares), dim3(DT), 0, st, slab,
+                       dw, C, (int)grid.x);
+  }
 }

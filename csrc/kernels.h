@@ -282,7 +282,10 @@ struct DwBw {                      // BN-backward reduce fused into the depthwis
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
                          int P, int Q, int stride, int pad, hipStream_t st,
                          const DwBw* bw = nullptr);
+// slab (optional, >= dwconv_wgrad_slab_floats): per-block partials + a reduce kernel
+size_t dwconv_wgrad_slab_floats(int N, int P, int Q, int C);
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
-                         int P, int Q, int stride, int pad, hipStream_t st);
+                         int P, int Q, int stride, int pad, hipStream_t st, float* slab = nullptr,
+                         size_t slab_floats = 0);
 void nchw_to_nhwc8_launch(const float* x, bf16* y, int N, int C, int H, int W, int Cpad,
                           hipStream_t st);

@@ -321,6 +321,7 @@ class NativeEngine(object):
         H, W = self.H, self.W
         C = cpad8(self.lw.in_channels)
         slab = 0
+        dw_slab = 0
         coef = 0
         nstats = 0
         nsums = 0
@@ -340,6 +341,10 @@ class NativeEngine(object):
                 if group_imgs:
                     sp.group_rows = group_imgs * sp.P * sp.Q
                 m.spec[u.name] = sp
+                if u.depthwise and train:
+                    # per-block weight-gradient partials (summed by a second kernel); its own
+                    # buffer: the split-K slab's head holds tile counters that must stay zero
+                    dw_slab = max(dw_slab, ops.dwconv_wgrad_slab_floats(N, sp.P, sp.Q, sp.C))
                 if not u.depthwise:
                     # measured-best plans from the tuning cache (ops/tune.py) when present
                     # the scoring pass runs beside the latency-bound train chain: fewer, larger
@@ -436,6 +441,7 @@ class NativeEngine(object):
         if train:
             m.dlogits = torch.zeros(N, self.classes, device=dev)
         m.slab = torch.zeros(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
+        m.dw_slab = torch.empty(dw_slab, dtype=torch.float32, device=dev) if dw_slab else None
         # per-stream scale / shift workspace of the pointwise GEMM's input prologue (each fused
         # conv's coefficient kernel fills it right before the conv, on the same stream)
         m.coef = torch.zeros(max(1, coef), dtype=torch.float32, device=dev)
@@ -727,7 +733,8 @@ class NativeEngine(object):
         sp = m.spec[u.name]
         gw = self._pview(u.w_seg, grad=True)
         if u.depthwise:
-            ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad)
+            ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad,
+                             slab=m.dw_slab)
         else:
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 

@@ -100,8 +100,18 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
     lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr(), *ba)
 
 
-def dwconv_wgrad(dy, x, dw, N, H, W, C, P, Q, stride, pad):
-    lib().dwconv_wgrad(ptr(dy), ptr(x), ptr(dw), N, H, W, C, P, Q, stride, pad, stream_ptr())
+def dwconv_wgrad_slab_floats(N, P, Q, C):
+    """fp32 workspace for ``dwconv_wgrad(slab=...)`` (per-block partials)."""
+    return int(lib().dwconv_wgrad_slab_floats(N, P, Q, C))
+
+
+def dwconv_wgrad(dy, x, dw, N, H, W, C, P, Q, stride, pad, slab=None):
+    """dw[C][9] += depthwise 3x3 weight gradient.  ``slab`` (fp32, >= dwconv_wgrad_slab_floats
+    elements): column-segmented rows with the blocks' partials summed by a second kernel
+    instead of atomics (faster at the train batch)."""
+    _chk(slab, torch.float32, 'slab')
+    lib().dwconv_wgrad(ptr(dy), ptr(x), ptr(dw), N, H, W, C, P, Q, stride, pad, stream_ptr(),
+                       ptr(slab), 0 if slab is None else slab.numel())
 
 
 def nchw_to_nhwc8(x, y):

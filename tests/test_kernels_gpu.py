@@ -697,6 +697,12 @@ def test_depthwise_strips_ghost_stats(case):
     dw = torch.zeros(C, 9, device=DEV)
     ops.dwconv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(xx.detach()), dw, N, H, W, C, P, Q, st, 1)
     close(dw, w.grad.reshape(C, 9), 2e-2, 2e-2)
+    # column-segmented rows, block partials summed by the reduce kernel (engine path)
+    slab = torch.full((ops.dwconv_wgrad_slab_floats(N, P, Q, C),), float('nan'), device=DEV)
+    dw2 = torch.zeros(C, 9, device=DEV)
+    ops.dwconv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(xx.detach()), dw2, N, H, W, C, P, Q, st, 1,
+                     slab=slab)
+    close(dw2, w.grad.reshape(C, 9), 2e-2, 2e-2)
 
 
 def conv_pro_direct(ops, x, wk, out, spec, slab, plan, pro):
