@@ -361,9 +361,8 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
     }
     if (spread) {
       const int nt = n0 / BN;
-      // (the ticket flag lives past the [3][BN] sums in the stats area: no static LDS here, the
-      // halo kernels' dynamic LDS is sized to the limit)
-      if (spread_ticket(e, (unsigned)nt, (unsigned)((M + BM - 1) / BM), (int*)(red + 3 * BN))) {
+      __shared__ int flag;
+      if (spread_ticket(e, (unsigned)nt, (unsigned)((M + BM - 1) / BM), &flag)) {
         for (int i = tid; i < BN; i += NT) {
           const int col = n0 + i;
           if (col < N) {

@@ -566,11 +566,6 @@ void stats_spread_fill(EpiParams& e, int M, int N, int BM, int BN) {
     nctr = ntn;
   }
   if ((long long)SPREAD_R * rows * N > g_srep_floats || nctr > g_sctr_n) return;
-  // only for grids of about one wave of blocks: the ticket holds each block for two memory round
-  // trips, which a many-round grid pays per round (MobileNetV2's B = 320 convs lost), while a
-  // one-round grid pays it once in its tail
-  const long long tiles = ((M + BM - 1) / BM) * ntn;
-  if (tiles > 512) return;
   e.srep = g_srep;
   e.sctr = g_sctr;
 }
