@@ -73,11 +73,6 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
     check_launch("igemm");
   });
-  // contention-spread BN statistics workspace for the conv launches that follow (igemm.h)
-  m.def("stats_spread_set", [](uintptr_t rep, uintptr_t ctr, long long rep_floats, long long nctr) {
-    stats_spread_set(P<float>(rep), P<unsigned>(ctr), rep_floats, nctr);
-  });
-  m.attr("SPREAD_R") = SPREAD_R;
   // 1x1 conv as a persistent LDS-DMA GEMM (pgemm.hip); returns 0 if unsupported
   m.def("pgemm", [](uintptr_t a, uintptr_t b, uintptr_t out, uintptr_t stats, int M, int N, int K,
                     int ldo, int stats_ld, int group_rows, long long a_bytes, long long b_bytes,

@@ -97,31 +97,6 @@ MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, 
   }
 }
 
-// Contention-spread statistics (igemm.h SPREAD_R).  add: this block's value of (row h of
-// replica-group rg, column col) goes to replica row (mt % SPREAD_R) -- a memory-side atomic like
-// the direct form, but SPREAD_R x fewer adders per address.  ticket: after every thread's adds
-// are performed (vmcnt(0): a no-return atomic leaves the counter when it is performed) and a
-// barrier, one returning atomic per (group, column tile) counts the contributors; the block that
-// completes the count folds the replicas with atomic exchanges (read + zero at the memory side,
-// nothing cached in any XCD's L2) into the real sums and resets the counter, so the workspace
-// is clean for the next launch.  All threads must call ticket (it has barriers).
-MA_DEV void spread_add(const EpiParams& e, int nrows, int row, int mt, int N, int col, float v) {
-  atomicAdd(e.srep + ((size_t)(mt % SPREAD_R) * nrows + row) * N + col, v);
-}
-MA_DEV bool spread_ticket(const EpiParams& e, unsigned ctr_idx, unsigned expected, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) *flag = atomicAdd(e.sctr + ctr_idx, 1u) == expected - 1 ? 1 : 0;
-  __syncthreads();
-  return *flag != 0;
-}
-MA_DEV float spread_take(const EpiParams& e, int nrows, int row, int N, int col) {
-  float v = 0.f;
-#pragma unroll
-  for (int r = 0; r < SPREAD_R; ++r) v += atomicExch(e.srep + ((size_t)r * nrows + row) * N + col, 0.f);
-  return v;
-}
-
 // Waves are laid out WM x WN (WM * WN = 4): 2 x 2 for the LDS-staged loops, 4 x 1 for the
 // direct-A loop.  acc[tm][tn][j] =
 //   OUT[m0 + wm*(BM/WM) + tm*16 + (lane&15)][n0 + wn*(BN/WN) + tn*16 + 4*(lane>>4) + j]
@@ -231,8 +206,6 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
   MA_STAMP(9);
   __syncthreads();
   if (stats) {
-    const bool spread = e.srep != nullptr;
-    const int G = (M + e.group_rows - 1) / e.group_rows, mt = m0 / BM;
     for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
       float* dst = e.stats + (size_t)(g0 + gi) * 2 * e.stats_ld;
       for (int i = tid; i < BN; i += NT) {
@@ -244,35 +217,9 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
             a += red[(q * 4 + 2 * gi) * BN + i];
             b += red[(q * 4 + 2 * gi + 1) * BN + i];
           }
-          if (spread) {
-            spread_add(e, 2 * G, 2 * (g0 + gi), mt, N, col, a);
-            spread_add(e, 2 * G, 2 * (g0 + gi) + 1, mt, N, col, b);
-          } else {
-            atomicAdd(dst + col, a);
-            atomicAdd(dst + e.stats_ld + col, b);
-          }
+          atomicAdd(dst + col, a);
+          atomicAdd(dst + e.stats_ld + col, b);
         }
-      }
-    }
-    if (spread) {
-      const int ntn = (N + BN - 1) / BN, nt = n0 / BN;
-      for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
-        const int g = g0 + gi;
-        // row tiles overlapping group g
-        const int r0 = g * e.group_rows, r1 = min(M, r0 + e.group_rows) - 1;
-        const unsigned expect = (unsigned)(r1 / BM - r0 / BM + 1);
-        if (spread_ticket(e, (unsigned)(g * ntn + nt), expect, (int*)red)) {
-          float* dst = e.stats + (size_t)g * 2 * e.stats_ld;
-          for (int i = tid; i < BN; i += NT) {
-            const int col = n0 + i;
-            if (col < N) {
-              atomicAdd(dst + col, spread_take(e, 2 * G, 2 * g, N, col));
-              atomicAdd(dst + e.stats_ld + col, spread_take(e, 2 * G, 2 * g + 1, N, col));
-            }
-          }
-          if (tid == 0) atomicExch(e.sctr + g * ntn + nt, 0u);
-        }
-        __syncthreads();
       }
     }
   }
@@ -343,35 +290,12 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       }
     }
     __syncthreads();
-    const bool spread = e.srep != nullptr;
-    const int mt = m0 / BM;
     for (int i = tid; i < BN; i += NT) {
       const int col = n0 + i;
       if (col < N) {
-        if (spread) {
-          spread_add(e, 3, 0, mt, N, col, red[i]);
-          spread_add(e, 3, 1, mt, N, col, red[BN + i]);
-          if (two) spread_add(e, 3, 2, mt, N, col, red[2 * BN + i]);
-        } else {
-          atomicAdd(e.bw_sums + col, red[i]);
-          atomicAdd(e.bw_sums + e.ldo + col, red[BN + i]);
-          if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, red[2 * BN + i]);
-        }
-      }
-    }
-    if (spread) {
-      const int nt = n0 / BN;
-      __shared__ int flag;
-      if (spread_ticket(e, (unsigned)nt, (unsigned)((M + BM - 1) / BM), &flag)) {
-        for (int i = tid; i < BN; i += NT) {
-          const int col = n0 + i;
-          if (col < N) {
-            atomicAdd(e.bw_sums + col, spread_take(e, 3, 0, N, col));
-            atomicAdd(e.bw_sums + e.ldo + col, spread_take(e, 3, 1, N, col));
-            if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, spread_take(e, 3, 2, N, col));
-          }
-        }
-        if (tid == 0) atomicExch(e.sctr + nt, 0u);
+        atomicAdd(e.bw_sums + col, red[i]);
+        atomicAdd(e.bw_sums + e.ldo + col, red[BN + i]);
+        if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, red[2 * BN + i]);
       }
     }
   }

@@ -39,24 +39,7 @@ struct EpiParams {
   float* bw_sums;          // [3][ldo] or null (feature off)
   float bw_inv_count, bw_eps;
   int bw_act;
-  // Contention spreading of the stats / bw sums (filled by the launchers from the workspace
-  // registered with stats_spread_set, else null = direct atomics): a block adds into replica
-  // row (row tile % SPREAD_R) and the last contributor of each (group, column tile) folds the
-  // replicas into stats / bw_sums (conv_epi.h).
-  float* srep;
-  unsigned* sctr;
 };
-
-// Replicas of the contention-spread statistics (every block adding into the same [2][C] row
-// serialises at the memory side: B = 32 convs measured 1.5-2x slower with the atomics than
-// with plain stores, bench/stats_cost.py)
-constexpr int SPREAD_R = 8;
-// Register the (zeroed, self-cleaning) workspace used by the launches that follow on the
-// calling thread: rep_floats fp32 replicas, nctr uint32 counters; (nullptr, 0, 0) disables.
-void stats_spread_set(float* rep, unsigned* ctr, long long rep_floats, long long nctr);
-// Fill e.srep / e.sctr for an M x N output with BM x BN tiles when the workspace is large enough
-// (stats: SPREAD_R * G * 2 * N floats, G * ntn counters; bw: SPREAD_R * 3 * N, ntn).
-void stats_spread_fill(EpiParams& e, int M, int N, int BM, int BN);
 
 // Forward-only A-operand prologue: the conv reads the PRODUCING conv's raw output y and applies
 // that layer's BatchNorm + activation per input channel while staging the tile,

@@ -463,14 +463,12 @@ inline void ig_grid(const ConvGeom& g, int BM, int BN, int splits, int& gx, int&
   if (gx > SEM_INTS) gy = 1, per = ktiles;
 }
 
-
 template <int BM, int BN, bool TRANS>
 void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
                 hipStream_t st, const ProParams* pro) {
   int gx, per, gy;
   ig_grid(g, BM, BN, splits, gx, per, gy);
   if (gy == 1) e.slab = nullptr;
-  stats_spread_fill(e, g.M, g.Ncols, BM, BN);
   if (pro != nullptr && !TRANS) {
     hipLaunchKernelGGL((igemm_pro_kernel<BM, BN>), dim3(gx, gy), dim3(NT), 0, st, src, wt, g, e,
                        per, *pro);
@@ -513,7 +511,6 @@ void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, in
   int dgx, dper, dgy, wgx, wper, wgy;
   ig_grid(g, DBM, DBN, splits, dgx, dper, dgy);
   if (dgy == 1) e.slab = nullptr;
-  stats_spread_fill(e, g.M, g.Ncols, DBM, DBN);
   wgb::wg_grid(wg, WBM, WBN, wsplits, wgx, wper, wgy);
   hipLaunchKernelGGL((bwd_pair_kernel<DBM, DBN, WBM, WBN>), dim3(dgx * dgy + wgx * wgy), dim3(NT),
                      0, st, dy, wt, g, e, dper, dgx, dgy, x, wg, dw, wper, wgx, wgy);
@@ -536,38 +533,6 @@ int igemm_read_stamps(unsigned long long* host, int n) {
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits) {
   const size_t mtiles = (g.M + bm - 1) / bm, ntiles = (g.Ncols + bn - 1) / bn;
   return SEM_INTS * 4 + (size_t)splits * mtiles * ntiles * bm * bn * 4;
-}
-
-// contention-spread workspace (igemm.h stats_spread_set); host-side state read at launch (and
-// so baked into captured graphs)
-static float* g_srep = nullptr;
-static unsigned* g_sctr = nullptr;
-static long long g_srep_floats = 0, g_sctr_n = 0;
-
-void stats_spread_set(float* rep, unsigned* ctr, long long rep_floats, long long nctr) {
-  g_srep = rep;
-  g_sctr = ctr;
-  g_srep_floats = rep ? rep_floats : 0;
-  g_sctr_n = ctr ? nctr : 0;
-}
-
-void stats_spread_fill(EpiParams& e, int M, int N, int BM, int BN) {
-  e.srep = nullptr;
-  e.sctr = nullptr;
-  if (!g_srep || !g_sctr || (!e.stats && !e.bw_sums)) return;
-  const long long ntn = (N + BN - 1) / BN;
-  long long rows, nctr;
-  if (e.stats) {
-    const long long G = (M + e.group_rows - 1) / e.group_rows;
-    rows = 2 * G;
-    nctr = G * ntn;
-  } else {
-    rows = 3;
-    nctr = ntn;
-  }
-  if ((long long)SPREAD_R * rows * N > g_srep_floats || nctr > g_sctr_n) return;
-  e.srep = g_srep;
-  e.sctr = g_sctr;
 }
 
 const bf16* conv_zero_page();

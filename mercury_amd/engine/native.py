@@ -179,9 +179,6 @@ class NativeEngine(object):
         self.use_pwconv = os.environ.get('MERCURY_PWCONV', '1') == '1'
         # the first conv (<= 4 input channels) on the dense-k stem kernel (stem.hip)
         self.use_stem = os.environ.get('MERCURY_STEM', '1') == '1'
-        # conv-epilogue BN statistics spread over replica rows and folded by the last block
-        # (csrc/conv_epi.h): every block adding into one [2][C] row serialised at the memory side
-        self.spread_stats = os.environ.get('MERCURY_SPREAD_STATS', '1') == '1'
         # depthwise convs take their input's BN + activation in their chunk loads
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
 
@@ -445,12 +442,6 @@ class NativeEngine(object):
             m.dlogits = torch.zeros(N, self.classes, device=dev)
         m.slab = torch.zeros(max(1, (slab + 3) // 4), dtype=torch.float32, device=dev)
         m.dw_slab = torch.empty(dw_slab, dtype=torch.float32, device=dev) if dw_slab else None
-        # contention-spread BN statistics (replicas + per-tile counters, self-cleaning): this
-        # mode's conv launches register it before they issue (_spread)
-        maxn = max([cpad8(u.K) for u in self.units] + [cpad8(u.C) for u in self.units])
-        nrep, nctr = ops.stats_spread_sizes(maxn, m.G)
-        m.srep = torch.zeros(nrep, dtype=torch.float32, device=dev) if self.spread_stats else None
-        m.sctr = torch.zeros(nctr, dtype=torch.int32, device=dev) if self.spread_stats else None
         # per-stream scale / shift workspace of the pointwise GEMM's input prologue (each fused
         # conv's coefficient kernel fills it right before the conv, on the same stream)
         m.coef = torch.zeros(max(1, coef), dtype=torch.float32, device=dev)
@@ -611,20 +602,8 @@ class NativeEngine(object):
                         stats=stats, slab=m.slab,
                         bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
 
-    def _spread(self, m):
-        """Point the conv launches that follow at this mode's spread-statistics workspace (the
-        caller unregisters it when its launches are issued)."""
-        ops.stats_spread(m.srep, m.sctr)
-
     def forward(self, m, x=None):
         """Forward through all blocks; returns the final activation buffer."""
-        self._spread(m)
-        try:
-            return self._forward(m, x)
-        finally:
-            ops.stats_spread(None)     # never leave a (possibly freed) workspace registered
-
-    def _forward(self, m, x=None):
         x = m.input if x is None else x
         stats_on = m.train or m.group_imgs
         pend = None          # the previous block's output, not yet materialised in x's buffer
@@ -829,13 +808,6 @@ class NativeEngine(object):
         sc = blk.shortcut
 
         def top():
-            self._spread(m)
-            try:
-                _top()
-            finally:
-                ops.stats_spread(None)
-
-        def _top():
             dout = m.buf[bi, 'dout']
             out = m.buf[bi, 'out']
             if blk.pool:
@@ -851,13 +823,6 @@ class NativeEngine(object):
                 self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
 
         def unit(i):
-            self._spread(m)
-            try:
-                _unit(i)
-            finally:
-                ops.stats_spread(None)
-
-        def _unit(i):
             u = units[i]
             d = m.buf[u.name, 'dy']
             inp = x if i == 0 else m.buf[units[i - 1].name, 'a']

@@ -210,25 +210,6 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     return out
 
 
-def stats_spread(rep=None, ctr=None):
-    """Register the workspace of the contention-spread BN statistics for the conv launches that
-    follow (csrc/igemm.h): ``rep`` fp32 zeros, ``ctr`` int32 zeros (self-cleaning); None turns
-    spreading off.  Launches whose needs exceed the workspace add directly."""
-    if rep is None or ctr is None:
-        lib().stats_spread_set(0, 0, 0, 0)
-        return
-    _chk(rep, torch.float32, 'rep')
-    _chk(ctr, torch.int32, 'ctr')
-    lib().stats_spread_set(ptr(rep), ptr(ctr), rep.numel(), ctr.numel())
-
-
-def stats_spread_sizes(max_n, groups):
-    """(replica floats, counters) covering every conv of a batch mode: up to ``max_n`` output
-    channels, ``groups`` ghost-BN groups, 64-wide column tiles."""
-    R = int(lib().SPREAD_R)
-    return R * max(2 * groups, 3) * max_n, groups * (-(-max_n // 64))
-
-
 PGEMM_BM = 256
 
 

@@ -1007,67 +1007,3 @@ def test_dwconv_dgrad_fused_bn_backward_reduce(case):
     scratch = torch.empty_like(y)
     ops.bn_bwd(dx, out, y, stats.reshape(-1), gamma, ref, scratch, M, C, act=act, eps=1e-5)
     close(sums[:2], ref[:2], 2e-3, 1e-2)
-
-
-@pytest.mark.parametrize('case', [
-    # N, H, C, K, R, stride, group_imgs, plan (bm, bn, splits)
-    (32, 16, 64, 96, 3, 1, 0, (128, 64, 1)),
-    (16, 14, 32, 64, 3, 1, 4, (128, 64, 1)),      # 784-row groups: tiles straddle group edges
-    (8, 8, 256, 128, 3, 1, 0, (64, 64, 4)),       # split-K: the last slice runs the epilogue
-    (12, 9, 40, 72, 1, 1, 3, (64, 128, 1)),       # odd shapes, 243-row groups
-])
-def test_spread_stats_match_direct_atomics(case):
-    """Contention-spread statistics (replica rows + last-block fold, csrc/conv_epi.h) give the
-    direct-atomic sums, leave the workspace clean (a second launch sums the same), and the
-    dgrad's fused BN-backward sums agree too."""
-    ops = _ops()
-    from mercury_amd.ops.conv import ConvSpec, slab_bytes
-    N, H, C, K, R, st, gimgs, plan = case
-    torch.manual_seed(5)
-    sp = ConvSpec(N, H, H, C, K, R, R, st, R // 2)
-    G = N // gimgs if gimgs else 1
-    if gimgs:
-        sp.group_rows = gimgs * sp.P * sp.Q
-    x = ops.to_nhwc(bf(torch.randn(N, C, H, H, device=DEV)))
-    wk, wt = ops.pack_conv_weight(torch.randn(K, C, R, R, device=DEV) * 0.1)
-    y = torch.empty(sp.M, K, dtype=torch.bfloat16, device=DEV)
-    slab = torch.zeros(slab_bytes(max(sp.M, N * H * H), max(K, sp.Cp), *plan) // 4 + 1,
-                       device=DEV)
-    ref = torch.zeros(G, 2, K, device=DEV)
-    ops.stats_spread(None)
-    ops.conv_fwd(x, wk, y, sp, stats=ref, slab=slab, plan=plan)
-    nrep, nctr = ops.stats_spread_sizes(max(K, sp.Cp), G)
-    rep = torch.zeros(nrep, device=DEV)
-    ctr = torch.zeros(nctr, dtype=torch.int32, device=DEV)
-    try:
-        ops.stats_spread(rep, ctr)
-        for _ in range(2):
-            got = torch.zeros_like(ref)
-            y2 = torch.empty_like(y)
-            ops.conv_fwd(x, wk, y2, sp, stats=got, slab=slab, plan=plan)
-            torch.cuda.synchronize()
-            assert torch.equal(y2, y)
-            close(got, ref, 1e-4, 1e-2)
-            assert int(ctr.abs().sum()) == 0 and float(rep.abs().sum()) == 0.0
-        # dgrad with the fused BN-backward reduce (one group)
-        if st == 1:
-            spd = ConvSpec(N, H, H, C, K, R, R, 1, R // 2)
-            dy = bf(torch.randn(spd.M, K, device=DEV)).to(torch.bfloat16)
-            Mx = N * H * H
-            yb = bf(torch.randn(Mx, sp.Cp, device=DEV)).to(torch.bfloat16)
-            ob = torch.relu(yb.float()).to(torch.bfloat16)
-            bst = torch.stack([yb.float().sum(0), yb.float().pow(2).sum(0)]).contiguous()
-            outs = []
-            for spread in (False, True):
-                ops.stats_spread(rep, ctr) if spread else ops.stats_spread(None)
-                sums = torch.zeros(3, sp.Cp, device=DEV)
-                dx = torch.empty(Mx, sp.Cp, dtype=torch.bfloat16, device=DEV)
-                ops.conv_dgrad(dy, wt, dx, spd,
-                               bw=dict(out=ob, y=yb, stats=bst, sums=sums, act='relu', eps=1e-5))
-                outs.append((dx, sums))
-            torch.cuda.synchronize()
-            assert torch.equal(outs[0][0], outs[1][0])
-            close(outs[1][1][:2], outs[0][1][:2], 1e-4, 1e-2)
-            assert int(ctr.abs().sum()) == 0 and float(rep.abs().sum()) == 0.0
-    finally:
-        ops.stats_spread(None)
