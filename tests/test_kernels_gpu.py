@@ -669,7 +669,9 @@ def test_quantize_pool_dwconv():
 
 
 @pytest.mark.parametrize('case', [(8, 96, 16, 16, 1, 4), (8, 144, 15, 15, 2, 2),
-                                  (4, 960, 4, 4, 1, 2), (3, 16, 7, 9, 2, 1), (6, 40, 5, 11, 1, 3)])
+                                  (4, 960, 4, 4, 1, 2), (3, 16, 7, 9, 2, 1), (6, 40, 5, 11, 1, 3),
+                                  # one group, > 256 blocks: the grid-stride forward
+                                  (32, 96, 32, 32, 1, 1), (64, 144, 31, 33, 2, 1)])
 def test_depthwise_strips_ghost_stats(case):
     """Strip/sliding-window depthwise kernels: odd widths, stride 2, ghost-BN groups, and
     blocks that straddle two BN groups (tiny images, many channels)."""
@@ -945,11 +947,13 @@ def test_maxpool_stem_shape_bwd_matches_torch():
 
 @pytest.mark.parametrize('stride', [1, 2])
 @pytest.mark.parametrize('ghost', [False, True])
-def test_dwconv_input_bn_prologue_matches_bn_apply_then_dw(stride, ghost):
+@pytest.mark.parametrize('N', [8, 64])
+def test_dwconv_input_bn_prologue_matches_bn_apply_then_dw(stride, ghost, N):
     """Depthwise 3x3 with its input's BN + ReLU6 applied to every loaded chunk (MobileNetV2
-    expand -> dw) == bn_apply pass + plain depthwise conv; the kept activation == bn_apply's."""
+    expand -> dw) == bn_apply pass + plain depthwise conv; the kept activation == bn_apply's.
+    N = 64 without ghost groups runs the grid-stride (one statistics group) kernel."""
     ops = _ops()
-    N, H, W, C = 8, 16, 16, 96
+    H, W, C = 16, 16, 96
     P, Q = H // stride, W // stride
     g = torch.Generator(device='cpu').manual_seed(11 + stride)
     y = bf(torch.randn(N * H * W, C, generator=g) * 2 + 0.3).to(DEV).to(torch.bfloat16)
