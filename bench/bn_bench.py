@@ -29,7 +29,7 @@ def main():
                                         res=res))
         row = dict(N=N, C=C, H=H, apply_us=round(t1, 2), apply_res_us=round(t2, 2))
         if N == 32:
-            sums = torch.zeros(3 * C, device=dev)
+            sums = torch.zeros(ops.sums_numel(C), device=dev)
             dy = torch.empty_like(y)
             t3 = gtime(lambda: ops.bn_bwd(res, out, y, st, gm, sums, dy, M, C, act='relu',
                                           zero_sums=False, reduce=False))

@@ -38,7 +38,7 @@ def main():
         dout, out, y = (t(M * C).to(torch.bfloat16) for _ in range(3))
         stats = torch.stack([t(C) * M * 0.1, (t(C).abs() + 1) * M]).contiguous()
         gamma = torch.ones(C, device='cuda')
-        sums = torch.zeros(3 * C, device='cuda')
+        sums = torch.zeros(ops.sums_numel(C), device='cuda')
         dy = torch.empty_like(y)
         r = gtime(lambda: ops.bn_bwd(dout, out, y, stats, gamma, sums, dy, M, C,
                                      zero_sums=False, reduce=True), reps=8)

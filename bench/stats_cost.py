@@ -43,6 +43,30 @@ def main():
         t0 = gtime(lambda: ops.conv_fwd(x, w, y, sp, slab=slab, plan=plan), reps=8)
         print(json.dumps(dict(kind='conv', N=N, H=H, C=C, K=K, R=R, stride=st, plan=list(plan),
                               stats_us=round(t1, 1), nostats_us=round(t0, 1))), flush=True)
+    # the dgrad + wgrad pair with / without the fused BN-backward sums (train batch)
+    from mercury_amd.ops.conv import dgrad_plan, wgrad_plan
+    for N, H, C, K, R, st in [(32, 32, 64, 64, 3, 1), (32, 16, 128, 128, 3, 1),
+                              (32, 32, 96, 16, 1, 1), (32, 32, 16, 96, 1, 1)]:
+        sp = ConvSpec(N, H, H, C, K, R, R, st, R // 2)
+        Mx = N * H * H
+        x = torch.randn(Mx * sp.Cp, device='cuda').to(torch.bfloat16)
+        wt = (torch.randn(C * R * R * K, device='cuda') * 0.05).to(torch.bfloat16)
+        dy = torch.randn(sp.M * K, device='cuda').to(torch.bfloat16)
+        dx = torch.empty(Mx * sp.Cp, device='cuda', dtype=torch.bfloat16)
+        dw = torch.zeros(K * R * R * C, device='cuda')
+        yb = torch.randn(Mx * sp.Cp, device='cuda').to(torch.bfloat16)
+        ob = torch.relu(yb.float()).to(torch.bfloat16)
+        bst = torch.stack([yb.float().view(Mx, -1).sum(0), yb.float().view(Mx, -1).pow(2).sum(0)])
+        sums = torch.zeros(ops.sums_numel(sp.Cp), device='cuda')
+        bw = dict(out=ob, y=yb, stats=bst.contiguous().view(-1), sums=sums, act='relu', eps=1e-5)
+        dp, wp = dgrad_plan(sp), wgrad_plan(sp)
+        slab = torch.zeros(max(1, slab_bytes(Mx, sp.Cp, *dp) // 4 + 1), device='cuda')
+        t1 = gtime(lambda: ops.conv_bwd(dy, wt, dx, x, dw, sp, dplan=dp, wplan=wp, slab=slab,
+                                        bw=bw), reps=8)
+        t0 = gtime(lambda: ops.conv_bwd(dy, wt, dx, x, dw, sp, dplan=dp, wplan=wp, slab=slab),
+                   reps=8)
+        print(json.dumps(dict(kind='bwd_pair', N=N, H=H, C=C, K=K, R=R, dplan=list(dp),
+                              bw_us=round(t1, 1), nobw_us=round(t0, 1))), flush=True)
     for N, H, C, st in DW:
         P = (H - 1) // st + 1
         x = torch.randn(N * H * H * C, device='cuda').to(torch.bfloat16)

@@ -73,6 +73,7 @@ PYBIND11_MODULE(_C, m) {
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
     check_launch("igemm");
   });
+  m.attr("SUMS_R") = SUMS_R;   // replicas of the BN-backward sums ([SUMS_R][3][C])
   // 1x1 conv as a persistent LDS-DMA GEMM (pgemm.hip); returns 0 if unsupported
   m.def("pgemm", [](uintptr_t a, uintptr_t b, uintptr_t out, uintptr_t stats, int M, int N, int K,
                     int ldo, int stats_ld, int group_rows, long long a_bytes, long long b_bytes,

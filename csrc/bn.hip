@@ -194,11 +194,31 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
   }
   __syncthreads();
+  float* sums = a.sums + (size_t)(blockIdx.x % SUMS_R) * 3 * a.C;   // replica (common.h)
   for (int j = threadIdx.x; j < a.C; j += NT) {
-    atomicAdd(&a.sums[j], red[j]);
-    atomicAdd(&a.sums[a.C + j], red[a.C + j]);
-    if (two) atomicAdd(&a.sums[2 * a.C + j], red[2 * a.C + j]);
+    atomicAdd(&sums[j], red[j]);
+    atomicAdd(&sums[a.C + j], red[a.C + j]);
+    if (two) atomicAdd(&sums[2 * a.C + j], red[2 * a.C + j]);
   }
+}
+
+// sum of the SUMS_R replicas of row h, channels c..c+7 of [SUMS_R][3][C] sums
+MA_DEV void load_sums8(const float* sums, int C, int h, int c, float (&v)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = 0.f;
+#pragma unroll
+  for (int r = 0; r < SUMS_R; ++r) {
+    float t[8];
+    load8(sums + ((size_t)r * 3 + h) * C + c, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+}
+MA_DEV float sum_sums(const float* sums, int C, int h, int j) {
+  float v = 0.f;
+#pragma unroll
+  for (int r = 0; r < SUMS_R; ++r) v += sums[((size_t)r * 3 + h) * C + j];
+  return v;
 }
 
 template <int ACT, bool TWO>
@@ -208,11 +228,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const float inv = 1.f / (float)a.M;
   if (blockIdx.x == 0) {  // parameter gradients
     for (int j = threadIdx.x; j < a.C; j += NT) {
-      if (a.dgamma) a.dgamma[j] = a.sums[a.C + j];
-      if (a.dbeta) a.dbeta[j] = a.sums[j];
+      const float s0 = sum_sums(a.sums, a.C, 0, j);
+      if (a.dgamma) a.dgamma[j] = sum_sums(a.sums, a.C, 1, j);
+      if (a.dbeta) a.dbeta[j] = s0;
       if (two) {
-        if (a.dgamma2) a.dgamma2[j] = a.sums[2 * a.C + j];
-        if (a.dbeta2) a.dbeta2[j] = a.sums[j];
+        if (a.dgamma2) a.dgamma2[j] = sum_sums(a.sums, a.C, 2, j);
+        if (a.dbeta2) a.dbeta2[j] = s0;
       }
     }
   }
@@ -237,12 +258,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
   mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
   load8(a.gamma + c, gm);
-  load8(a.sums + c, sdz);
-  load8(a.sums + a.C + c, sx);
+  load_sums8(a.sums, a.C, 0, c, sdz);
+  load_sums8(a.sums, a.C, 1, c, sx);
   if (two) {
     mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
     load8(a.gamma2 + c, gm2);
-    load8(a.sums + 2 * a.C + c, sx2);
+    load_sums8(a.sums, a.C, 2, c, sx2);
   }
   float k1[8], k2[8], q1[8], k3[8], q2[8];
 #pragma unroll

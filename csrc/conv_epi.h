@@ -290,12 +290,14 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       }
     }
     __syncthreads();
+    // replica (row tile % SUMS_R) of the [SUMS_R][3][ldo] sums (common.h)
+    float* sums = e.bw_sums + (size_t)((m0 / BM) % SUMS_R) * 3 * e.ldo;
     for (int i = tid; i < BN; i += NT) {
       const int col = n0 + i;
       if (col < N) {
-        atomicAdd(e.bw_sums + col, red[i]);
-        atomicAdd(e.bw_sums + e.ldo + col, red[BN + i]);
-        if (two) atomicAdd(e.bw_sums + 2 * e.ldo + col, red[2 * BN + i]);
+        atomicAdd(sums + col, red[i]);
+        atomicAdd(sums + e.ldo + col, red[BN + i]);
+        if (two) atomicAdd(sums + 2 * e.ldo + col, red[2 * BN + i]);
       }
     }
   }

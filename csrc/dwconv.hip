@@ -324,9 +324,10 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
         v0 += part[j * ST_LD + (c & 7)];
         v1 += part[j * ST_LD + 8 + (c & 7)];
       }
-      if (v0 != 0.f || v1 != 0.f) {
-        atomicAdd(bw.sums + c, v0);
-        atomicAdd(bw.sums + C + c, v1);
+      if (v0 != 0.f || v1 != 0.f) {     // replica blockIdx % SUMS_R of [SUMS_R][3][C]
+        float* sums = bw.sums + (size_t)(blockIdx.x % SUMS_R) * 3 * C;
+        atomicAdd(sums + c, v0);
+        atomicAdd(sums + C + c, v1);
       }
     }
   }

@@ -36,7 +36,7 @@ struct EpiParams {
   const float* bw_stats;   // [2][ldo] batch sum, sumsq of bw_y
   const bf16* bw_y2;       // optional shortcut BN sharing dz
   const float* bw_stats2;
-  float* bw_sums;          // [3][ldo] or null (feature off)
+  float* bw_sums;          // [SUMS_R][3][ldo] replicas (common.h) or null (feature off)
   float bw_inv_count, bw_eps;
   int bw_act;
 };

@@ -38,7 +38,7 @@ struct BnBwdArgs {
   const bf16* y2;                // optional shortcut conv output sharing dz
   const float* stats2;
   const float* gamma2;
-  float* sums;                   // workspace [3][C]
+  float* sums;                   // workspace [SUMS_R][3][C] (replicas, common.h)
   bf16* dy;                      // grad wrt y
   bf16* dy2;                     // grad wrt y2
   bf16* dz;                      // optional: grad wrt pre-activation (identity residual)
@@ -275,7 +275,7 @@ struct DwBw {                      // BN-backward reduce fused into the depthwis
   const bf16* out;                 // activation act(bn(y)) of the BN feeding the dw conv (mask)
   const bf16* y;                   // that BN's input
   const float* stats;              // its batch sums [2][C]
-  float* sums;                     // += (sum dz, sum dz * xhat) [3][C] (zeroed by the engine)
+  float* sums;                     // += (sum dz, sum dz * xhat) [SUMS_R][3][C] (zeroed)
   float inv_count, eps;
   int act;
 };

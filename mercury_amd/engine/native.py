@@ -398,7 +398,7 @@ class NativeEngine(object):
                 if train:
                     m.buf[u.name, 'dy'] = act(sp.M, u.K)
                     m.buf[u.name, 'sums'] = nsums
-                    nsums += 3 * u.K
+                    nsums += ops.sums_numel(u.K)      # [SUMS_R][3][K] replicas
                     if u is not blk.units[-1] and u is not blk.shortcut:
                         m.buf[u.name, 'da'] = act(sp.M, u.K)
                 if u is not blk.shortcut:
@@ -432,7 +432,7 @@ class NativeEngine(object):
             m.stats[key] = m.stats_arena[off:off + m.G * 2 * u.K]
             if train:
                 so = m.buf[u.name, 'sums']
-                m.buf[u.name, 'sums'] = m.sums_arena[so:so + 3 * u.K]
+                m.buf[u.name, 'sums'] = m.sums_arena[so:so + ops.sums_numel(u.K)]
         m.final_hw = H * W
         m.final_C = C
         m.pooled = torch.zeros(N, C, device=dev)

@@ -34,16 +34,27 @@ def bn_apply(y, stats, gamma, beta, out, M, C, group_rows=0, act='relu', eps=1e-
     return out
 
 
+def sums_numel(C):
+    """fp32 elements of a BN-backward sums workspace for C channels: [SUMS_R][3][C]."""
+    return int(lib().SUMS_R) * 3 * C
+
+
+def sums_total(sums, C):
+    """[3][C] totals of a [SUMS_R][3][C] BN-backward sums workspace."""
+    return sums.reshape(-1, 3, C).sum(0)
+
+
 def bn_bwd(dout, out, y, stats, gamma, sums, dy, M, C, act='relu', eps=1e-5, y2=None,
            stats2=None, gamma2=None, dy2=None, dz=None, dgamma=None, dbeta=None, dgamma2=None,
            dbeta2=None, zero_sums=True, reduce=True):
     """BN(+shortcut BN)+activation backward for one stat group.
 
-    ``sums``: [3][C] fp32 workspace that must be zero on entry; ``zero_sums=False`` when
+    ``sums``: [SUMS_R][3][C] fp32 workspace (replicas the producers spread their atomics over,
+    summed when applied: ``sums_total``) that must be zero on entry; ``zero_sums=False`` when
     the caller zeroes a whole arena once per step (one memset instead of one per layer).
     ``reduce=False``: the sums were already reduced by the producing dgrad's epilogue
     (``conv_dgrad(bw=...)``) -- only the apply pass runs."""
-    _chk(sums, torch.float32, 'sums', 3 * C)
+    _chk(sums, torch.float32, 'sums', sums_numel(C))
     if zero_sums and reduce:
         sums.zero_()
     lib().bn_bwd(ptr(dout), ptr(out), ptr(y), ptr(stats), ptr(gamma), ptr(y2), ptr(stats2),

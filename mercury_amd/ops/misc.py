@@ -83,7 +83,7 @@ def dwconv_fwd(x, w, y, N, H, W, C, P, Q, stride, pad, stats=None, group_rows=0,
 
 
 def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
-    """Depthwise 3x3 data gradient.  ``bw``: dict(out=, y=, stats=[2][C], sums=[3][C], act=,
+    """Depthwise 3x3 data gradient.  ``bw``: dict(out=, y=, stats=[2][C], sums=[SUMS_R][3][C], act=,
     eps=) -- also reduce the BN-backward sums of the BN feeding this conv (its activation
     ``out``, input ``y``), as bn_bwd's reduce pass would (one batch group)."""
     ba = (0, 0, 0, 0, 0.0, 0.0, 0)
@@ -92,7 +92,7 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
         for k in ('out', 'y'):
             _chk(bw[k], torch.bfloat16, 'bw.' + k, n_in)
         _chk(bw['stats'], torch.float32, 'bw.stats', 2 * C)
-        _chk(bw['sums'], torch.float32, 'bw.sums', 3 * C)
+        _chk(bw['sums'], torch.float32, 'bw.sums', int(lib().SUMS_R) * 3 * C)
         if bw.get('y2') is not None:
             raise ValueError('dwconv_dgrad: no shortcut-BN reduce')
         ba = (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw['sums']),

@@ -153,7 +153,7 @@ def test_conv_dgrad_fused_bn_backward_reduce(case, two):
     out = bf(torch.relu(torch.randn(Mx, C, device=DEV))).to(torch.bfloat16)
     stats = torch.stack([y.float().sum(0), y.float().pow(2).sum(0)]).contiguous()
     stats2 = torch.stack([y2.float().sum(0), y2.float().pow(2).sum(0)]).contiguous()
-    sums = torch.zeros(3, C, device=DEV)
+    sums = torch.zeros(ops.sums_numel(C), device=DEV)
     prior = bf(torch.randn(Mx, C, device=DEV)).to(torch.bfloat16)
     dx = prior.clone()
     bw = dict(out=out, y=y, stats=stats, sums=sums, act='relu', eps=1e-5)
@@ -169,12 +169,13 @@ def test_conv_dgrad_fused_bn_backward_reduce(case, two):
         return (t.float() - mu) / torch.sqrt(var + 1e-5)
     ref0 = dz.sum(0)
     ref1 = (dz * xhat(y, stats)).sum(0)
-    close(sums[0], ref0, 1e-3, 1e-2)
-    close(sums[1], ref1, 1e-3, 1e-2)
+    tot = ops.sums_total(sums, C)          # (the producers spread over SUMS_R replicas)
+    close(tot[0], ref0, 1e-3, 1e-2)
+    close(tot[1], ref1, 1e-3, 1e-2)
     if two:
-        close(sums[2], (dz * xhat(y2, stats2)).sum(0), 1e-3, 1e-2)
+        close(tot[2], (dz * xhat(y2, stats2)).sum(0), 1e-3, 1e-2)
     else:
-        assert float(sums[2].abs().max()) == 0.0
+        assert float(tot[2].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize('case', [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0])
@@ -257,7 +258,7 @@ def test_bn_apply_and_bwd_with_bn_shortcut():
     close(ops.from_nhwc(out.view(N, H, W, C)), ref)
     dout = bf(torch.randn_like(ref))
     ref.backward(dout)
-    sums = torch.zeros(3, C, device=DEV)
+    sums = torch.zeros(ops.sums_numel(C), device=DEV)
     dy = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
     dy2 = torch.empty_like(dy)
     dz = torch.empty_like(dy)
@@ -824,13 +825,14 @@ def test_fused_bn_paths_propagate_nan_like_bn_hip():
     dx = torch.empty(N * H * W, C, dtype=torch.bfloat16, device=DEV)
     yc = bf(torch.randn(N * H * W, C, device=DEV)).to(torch.bfloat16)
     stats = torch.stack([yc.float().sum(0), yc.float().pow(2).sum(0)]).contiguous()
-    sums = torch.zeros(3, C, device=DEV)
+    sums = torch.zeros(ops.sums_numel(C), device=DEV)
     dplan = dgrad_plan(dspec)
     dslab = torch.zeros(max(1, slab_bytes(N * H * W, C, *dplan) // 4), device=DEV)
     ops.conv_dgrad(gy, wt, dx, dspec, slab=dslab, plan=dplan,
                    bw=dict(out=an, y=yc, stats=stats, sums=sums, act='none', eps=1e-5))
-    assert torch.isfinite(sums[:2]).all()
-    close(sums[0], dx.float().sum(0), 1e-3, 1e-2)
+    tot = ops.sums_total(sums, C)
+    assert torch.isfinite(tot[:2]).all()
+    close(tot[0], dx.float().sum(0), 1e-3, 1e-2)
 
 
 def _halo_case(ops, case, plan, gimgs):
@@ -1003,11 +1005,11 @@ def test_dwconv_dgrad_fused_bn_backward_reduce(case):
     dx = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
     ops.dwconv_dgrad(gy, wf, dx, N, H, W, C, P, Q, st, 1)
     dx2 = torch.empty_like(dx)
-    sums = torch.zeros(3, C, device=DEV)
+    sums = torch.zeros(ops.sums_numel(C), device=DEV)
     ops.dwconv_dgrad(gy, wf, dx2, N, H, W, C, P, Q, st, 1,
                      bw=dict(out=out, y=y, stats=stats, sums=sums, act=act, eps=1e-5))
     assert torch.equal(dx, dx2)
-    ref = torch.zeros(3, C, device=DEV)
+    ref = torch.zeros(ops.sums_numel(C), device=DEV)
     scratch = torch.empty_like(y)
     ops.bn_bwd(dx, out, y, stats.reshape(-1), gamma, ref, scratch, M, C, act=act, eps=1e-5)
-    close(sums[:2], ref[:2], 2e-3, 1e-2)
+    close(ops.sums_total(sums, C)[:2], ops.sums_total(ref, C)[:2], 2e-3, 1e-2)
