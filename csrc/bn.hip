@@ -194,7 +194,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
   }
   __syncthreads();
-  float* sums = a.sums + (size_t)(blockIdx.x % SUMS_R) * 3 * a.C;   // replica (common.h)
+  float* sums = a.sums + (size_t)(blockIdx.x % SUMS_R) * 3 * a.C;   // replica (igemm.h SUMS_R)
   for (int j = threadIdx.x; j < a.C; j += NT) {
     atomicAdd(&sums[j], red[j]);
     atomicAdd(&sums[a.C + j], red[a.C + j]);

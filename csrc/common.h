@@ -22,12 +22,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define MA_DEV __device__ __forceinline__
 
-// BN-backward sums are kept as SUMS_R replicas [SUMS_R][3][C]: a producer block adds into
-// replica (its tile / block index % SUMS_R) and bn_bwd_apply, their one consumer, sums the
-// replicas when it loads them.  Every block adding into ONE [3][C] row serialised at the memory
-// side (bench/stats_cost.py: the ResNet-18 layer-1 dgrad+wgrad pair 32.8 us with the fused sums,
-// 20.5 without).
-constexpr int SUMS_R = 8;
 
 MA_DEV float bf2f(bf16 x) { return (float)x; }
 MA_DEV bf16 f2bf(float x) { return (bf16)x; }

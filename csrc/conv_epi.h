@@ -290,7 +290,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
       }
     }
     __syncthreads();
-    // replica (row tile % SUMS_R) of the [SUMS_R][3][ldo] sums (common.h)
+    // replica (row tile % SUMS_R) of the [SUMS_R][3][ldo] sums (igemm.h)
     float* sums = e.bw_sums + (size_t)((m0 / BM) % SUMS_R) * 3 * e.ldo;
     for (int i = tid; i < BN; i += NT) {
       const int col = n0 + i;

@@ -18,6 +18,13 @@ struct ConvGeom {
   const bf16* zero;  // 16-byte zero page for padding taps (set by the launcher; kernel arg -> SGPR)
 };
 
+// BN-backward sums are kept as SUMS_R replicas [SUMS_R][3][C]: a producer block adds into
+// replica (its tile / block index % SUMS_R) and bn_bwd_apply, their one consumer, sums the
+// replicas when it loads them.  Every block adding into ONE [3][C] row serialised at the memory
+// side (bench/stats_cost.py: the ResNet-18 layer-1 dgrad+wgrad pair 32.8 us with the fused sums,
+// 20.5 without).
+constexpr int SUMS_R = 8;
+
 struct EpiParams {
   bf16* out;          // [M][ldo] bf16
   int ldo;
@@ -36,7 +43,7 @@ struct EpiParams {
   const float* bw_stats;   // [2][ldo] batch sum, sumsq of bw_y
   const bf16* bw_y2;       // optional shortcut BN sharing dz
   const float* bw_stats2;
-  float* bw_sums;          // [SUMS_R][3][ldo] replicas (common.h) or null (feature off)
+  float* bw_sums;          // [SUMS_R][3][ldo] replicas (SUMS_R above) or null (feature off)
   float bw_inv_count, bw_eps;
   int bw_act;
 };
