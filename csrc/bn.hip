@@ -202,18 +202,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
-// sum of the SUMS_R replicas of row h, channels c..c+7 of [SUMS_R][3][C] sums
-MA_DEV void load_sums8(const float* sums, int C, int h, int c, float (&v)[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = 0.f;
-#pragma unroll
-  for (int r = 0; r < SUMS_R; ++r) {
-    float t[8];
-    load8(sums + ((size_t)r * 3 + h) * C + c, t);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += t[k];
-  }
-}
+// total of the SUMS_R replicas of [SUMS_R][3][C] sums at (row h, channel j)
 MA_DEV float sum_sums(const float* sums, int C, int h, int j) {
   float v = 0.f;
 #pragma unroll
@@ -223,17 +212,21 @@ MA_DEV float sum_sums(const float* sums, int C, int h, int j) {
 
 template <int ACT, bool TWO>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
+  __shared__ float tot[3 * 2048];   // the replicas' totals [3][C] (C <= 2048)
   const int C8 = a.C >> 3;
   constexpr bool two = TWO;
   const float inv = 1.f / (float)a.M;
+  // fold the SUMS_R replicas once per block (each value SUMS_R loads, shared by every thread)
+  for (int j = threadIdx.x; j < (two ? 3 : 2) * a.C; j += NT)
+    tot[j] = sum_sums(a.sums, a.C, j / a.C, j % a.C);
+  __syncthreads();
   if (blockIdx.x == 0) {  // parameter gradients
     for (int j = threadIdx.x; j < a.C; j += NT) {
-      const float s0 = sum_sums(a.sums, a.C, 0, j);
-      if (a.dgamma) a.dgamma[j] = sum_sums(a.sums, a.C, 1, j);
-      if (a.dbeta) a.dbeta[j] = s0;
+      if (a.dgamma) a.dgamma[j] = tot[a.C + j];
+      if (a.dbeta) a.dbeta[j] = tot[j];
       if (two) {
-        if (a.dgamma2) a.dgamma2[j] = sum_sums(a.sums, a.C, 2, j);
-        if (a.dbeta2) a.dbeta2[j] = s0;
+        if (a.dgamma2) a.dgamma2[j] = tot[2 * a.C + j];
+        if (a.dbeta2) a.dbeta2[j] = tot[j];
       }
     }
   }
@@ -258,12 +251,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
   mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
   load8(a.gamma + c, gm);
-  load_sums8(a.sums, a.C, 0, c, sdz);
-  load_sums8(a.sums, a.C, 1, c, sx);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sdz[k] = tot[c + k];
+    sx[k] = tot[a.C + c + k];
+  }
   if (two) {
     mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
     load8(a.gamma2 + c, gm2);
-    load_sums8(a.sums, a.C, 2, c, sx2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sx2[k] = tot[2 * a.C + c + k];
   }
   float k1[8], k2[8], q1[8], k3[8], q2[8];
 #pragma unroll

@@ -38,7 +38,7 @@ struct BnBwdArgs {
   const bf16* y2;                // optional shortcut conv output sharing dz
   const float* stats2;
   const float* gamma2;
-  float* sums;                   // workspace [SUMS_R][3][C] (replicas, common.h)
+  float* sums;                   // workspace [SUMS_R][3][C] (replicas, igemm.h SUMS_R)
   bf16* dy;                      // grad wrt y
   bf16* dy2;                     // grad wrt y2
   bf16* dz;                      // optional: grad wrt pre-activation (identity residual)

@@ -36,7 +36,7 @@ def bn_apply(y, stats, gamma, beta, out, M, C, group_rows=0, act='relu', eps=1e-
 
 def sums_numel(C):
     """fp32 elements of a BN-backward sums workspace for C channels: [SUMS_R][3][C]."""
-    return int(lib().SUMS_R) * 3 * C
+    return int(getattr(lib(), 'SUMS_R', 1)) * 3 * C     # (1: a build without replicas)
 
 
 def sums_total(sums, C):

@@ -400,7 +400,7 @@ def _bw_args(bw, Mx, Cp):
     for k in ('out', 'y', 'y2'):
         if bw.get(k) is not None:
             _chk(bw[k], torch.bfloat16, 'bw.' + k, Mx * Cp)
-    _chk(bw['sums'], torch.float32, 'bw.sums', int(lib().SUMS_R) * 3 * Cp)
+    _chk(bw['sums'], torch.float32, 'bw.sums', int(getattr(lib(), 'SUMS_R', 1)) * 3 * Cp)
     _chk(bw['stats'], torch.float32, 'bw.stats', 2 * Cp)
     return (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw.get('y2')),
             ptr(bw.get('stats2')), ptr(bw['sums']), 1.0 / Mx, float(bw.get('eps', 1e-5)),

@@ -92,7 +92,7 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
         for k in ('out', 'y'):
             _chk(bw[k], torch.bfloat16, 'bw.' + k, n_in)
         _chk(bw['stats'], torch.float32, 'bw.stats', 2 * C)
-        _chk(bw['sums'], torch.float32, 'bw.sums', int(lib().SUMS_R) * 3 * C)
+        _chk(bw['sums'], torch.float32, 'bw.sums', int(getattr(lib(), 'SUMS_R', 1)) * 3 * C)
         if bw.get('y2') is not None:
             raise ValueError('dwconv_dgrad: no shortcut-BN reduce')
         ba = (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw['sums']),
