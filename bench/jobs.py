@@ -14,7 +14,8 @@ jobs
   trace     [--args BENCH_ARGS]      rocprofv3 kernel trace -> per-queue timeline + graph times
   pmc       [--counters C ...]       one PMC pass (<= 8 SQ counters) over the headline step
   presets                            every BASELINE config's bench (configs 2-5)
-  ab        --env "A=1" "A=0" ...    same-box interleaved A/B of env settings (2 rounds)
+  ab        --env "A=1" "A=0" ...    same-box interleaved A/B of env settings (2 rounds;
+            [--args BENCH_ARGS]      --args e.g. '--config mobilenetv2-cifar100')
   ab-ext    --old OLD.so             same-box A/B of another build (MERCURY_EXT_PATH)
   ab-preset --old OLD.so --args CFG  ... on one BASELINE preset
   ab-kernel --old OLD.so --args CMD  ... on a microbenchmark (bench/pool_bench.py, ...)
@@ -140,8 +141,8 @@ def job_ab(o, a):
         for j, e in enumerate(envs):
             kv = dict(x.split('=', 1) for x in e.split())
             out = os.path.join(o, 'v%d_%d.json' % (j + 1, rnd + 1))
-            run([PY, 'bench.py', '--steps', '300', '--warmup', '30', '--no-overhead'], out, 200,
-                env=kv)
+            run([PY, 'bench.py'] + shlex.split(a.args or '') +
+                ['--steps', '300', '--warmup', '30', '--no-overhead'], out, 200, env=kv)
             with open(out) as f:
                 res[e].append(json.loads(f.read().strip().splitlines()[-1])['ms_per_step'])
     for e, v in res.items():

@@ -22,6 +22,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define MA_DEV __device__ __forceinline__
 
+// Timing probe only (bench/build_variant.py with -DMERCURY_SPREAD_PROBE=<floats>): forward BN
+// statistics atomics go to one of 8 replicas by block (consumers read replica 0 only, so the
+// statistics are WRONG) -- measures what the same-address atomic contention costs the step.
+#ifdef MERCURY_SPREAD_PROBE
+#define MA_SPREAD(p) ((p) + (size_t)(blockIdx.x & 7) * (MERCURY_SPREAD_PROBE))
+#else
+#define MA_SPREAD(p) (p)
+#endif
+
 
 MA_DEV float bf2f(bf16 x) { return (float)x; }
 MA_DEV bf16 f2bf(float x) { return (bf16)x; }

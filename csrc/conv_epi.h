@@ -207,7 +207,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
   __syncthreads();
   if (stats) {
     for (int gi = 0; gi < (straddle ? 2 : 1); ++gi) {
-      float* dst = e.stats + (size_t)(g0 + gi) * 2 * e.stats_ld;
+      float* dst = MA_SPREAD(e.stats + (size_t)(g0 + gi) * 2 * e.stats_ld);
       for (int i = tid; i < BN; i += NT) {
         const int col = n0 + i;
         if (col < N) {

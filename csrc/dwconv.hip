@@ -158,7 +158,7 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
       }
     }
     if (a.stats && !lds_stats) {  // block straddles two BN groups (tiny images): global atomics
-      float* dst = a.stats + (size_t)(n / imgs_per_group) * 2 * a.C;
+      float* dst = MA_SPREAD(a.stats + (size_t)(n / imgs_per_group) * 2 * a.C);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         atomicAdd(dst + c8 * 8 + k, s[k]);
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
     }
     __syncthreads();
     const int nthr = min(DT, lim - g0), off = g0 % C8;
-    float* dst = a.stats + (size_t)gfirst * 2 * a.C;
+    float* dst = MA_SPREAD(a.stats + (size_t)gfirst * 2 * a.C);
     for (int c = threadIdx.x; c < a.C; c += DT) {
       const int j0 = ((c >> 3) - off + C8) % C8;
       float v0 = 0.f, v1 = 0.f;

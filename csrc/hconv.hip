@@ -492,7 +492,7 @@ MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
         a += red[q * 2 * BN + tid];
         b += red[q * 2 * BN + BN + tid];
       }
-      float* dst = e.stats + (size_t)(m0 / e.group_rows) * 2 * e.stats_ld + n0 + tid;
+      float* dst = MA_SPREAD(e.stats + (size_t)(m0 / e.group_rows) * 2 * e.stats_ld + n0 + tid);
       atomicAdd(dst, a);
       atomicAdd(dst + e.stats_ld, b);
     }

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro p
         a += red[(q * 2) * BN + tid];
         c += red[(q * 2 + 1) * BN + tid];
       }
-      float* dst = g.stats + (size_t)grp * 2 * g.stats_ld + n0 + tid;
+      float* dst = MA_SPREAD(g.stats + (size_t)grp * 2 * g.stats_ld + n0 + tid);
       atomicAdd(dst, a);
       atomicAdd(dst + g.stats_ld, c);
     }

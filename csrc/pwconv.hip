@@ -223,7 +223,7 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
         }
         pw_bar_lds();
         if (tid < BN && nt * BN + tid < g.N) {
-          float* dst = g.stats + (size_t)(gs + part) * 2 * g.stats_ld + nt * BN + tid;
+          float* dst = MA_SPREAD(g.stats + (size_t)(gs + part) * 2 * g.stats_ld + nt * BN + tid);
           atomicAdd(dst, red[tid] + red[2 * BN + tid]);
           atomicAdd(dst + g.stats_ld, red[BN + tid] + red[3 * BN + tid]);
         }

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
   if (tid < 2 * K) {
     const int h = tid / K, k = tid - h * K;
     const float v = red[0][h][k] + red[1][h][k] + red[2][h][k] + red[3][h][k];
-    atomicAdd(a.stats + ((size_t)(n / a.group_imgs) * 2 + h) * K + k, v);
+    atomicAdd(MA_SPREAD(a.stats + ((size_t)(n / a.group_imgs) * 2 + h) * K + k), v);
   }
 }
 

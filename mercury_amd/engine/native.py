@@ -425,7 +425,10 @@ class NativeEngine(object):
                 h, w = P_, Q_
             m.buf[bi, 'hw'] = (h, w)
             H, W, C = h, w, K
-        m.stats_arena = torch.zeros(max(nstats, 1), device=dev)
+        # (timing probe builds with -DMERCURY_SPREAD_PROBE=F add 8 replicas of F floats past it)
+        spread = int(os.environ.get('MERCURY_SPREAD_PROBE_FLOATS', '0'))
+        m.stats_store = torch.zeros(max(nstats, 1) + 8 * spread, device=dev)
+        m.stats_arena = m.stats_store[:max(nstats, 1)]
         m.sums_arena = torch.zeros(max(nsums, 1), device=dev)
         for key, off in list(m.stats.items()):
             u = next(x for x in self.units if x.name == key)
