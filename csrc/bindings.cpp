@@ -149,13 +149,14 @@ PYBIND11_MODULE(_C, m) {
                             uintptr_t bw_y2, uintptr_t bw_stats2, uintptr_t bw_sums,
                             float bw_inv_count, float bw_eps, int bw_act, uintptr_t x,
                             uintptr_t dw, int N, int H, int W, int C, int Pp, int Q, int K,
-                            int Creal, int wbm, int wbn, int wsplits, uintptr_t st) {
+                            int Creal, int wbm, int wbn, int wsplits, uintptr_t wslab,
+                            uintptr_t st) {
     ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
     EpiParams e{P<bf16>(dx), ldo, nullptr, nullptr, 0, M, accumulate, P<float>(slab),
                 P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats),
                 P<const bf16>(bw_y2), P<const float>(bw_stats2), P<float>(bw_sums), bw_inv_count,
                 bw_eps, bw_act};
-    WgradGeom wg{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal};
+    WgradGeom wg{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal, nullptr, P<float>(wslab)};
     const int ok = conv_bwd_pair_launch(P<const bf16>(dy), P<const bf16>(wt), g, e, bm, bn, splits,
                                         P<const bf16>(x), wg, P<float>(dw), wbm, wbn, wsplits, S(st));
     if (ok) check_launch("conv_bwd_pair");
@@ -230,8 +231,8 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C, int Pp,
                     int Q, int K, int R, int Sk, int stride, int pad, int Creal, int bm, int bn,
-                    int splits, uintptr_t st) {
-    WgradGeom g{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal};
+                    int splits, uintptr_t slab, uintptr_t st) {
+    WgradGeom g{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal, nullptr, P<float>(slab)};
     wgrad_launch(P<const bf16>(dy), P<const bf16>(x), g, P<float>(dw), bm, bn, splits, S(st));
     check_launch("wgrad");
   });

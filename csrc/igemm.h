@@ -82,6 +82,8 @@ struct WgradGeom {
   int R, S, stride, pad;
   int Creal;          // unpadded input channels (layout of dW)
   const bf16* zero;   // 16-byte zero page (set by the launcher)
+  float* slab;        // split-K partial tiles behind WG_SEM_INTS tile counters, or null
+                      // (null: the pixel splits add into dW with fp32 atomics)
 };
 void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
                   int splits, hipStream_t st);

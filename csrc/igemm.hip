@@ -507,11 +507,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict_
 
 template <int DBM, int DBN, int WBM, int WBN>
 void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
-              const bf16* x, const WgradGeom& wg, float* dw, int wsplits, hipStream_t st) {
+              const bf16* x, WgradGeom wg, float* dw, int wsplits, hipStream_t st) {
   int dgx, dper, dgy, wgx, wper, wgy;
   ig_grid(g, DBM, DBN, splits, dgx, dper, dgy);
   if (dgy == 1) e.slab = nullptr;
   wgb::wg_grid(wg, WBM, WBN, wsplits, wgx, wper, wgy);
+  if (wgx > wgb::WG_SEM_INTS) wg.slab = nullptr;
   hipLaunchKernelGGL((bwd_pair_kernel<DBM, DBN, WBM, WBN>), dim3(dgx * dgy + wgx * wgy), dim3(NT),
                      0, st, dy, wt, g, e, dper, dgx, dgy, x, wg, dw, wper, wgx, wgy);
 }

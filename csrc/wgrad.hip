@@ -17,8 +17,10 @@
 // half reads 8 consecutive rows: conflict-free tr reads.  The permutation is a
 // relabelling of the summation index, so the result is unchanged.
 //
-// Split-K over pixels (gridDim.y) accumulates with fp32 atomics into the flat
-// gradient buffer; without splitting it stores.  The output is written in the
+// Split-K over pixels (gridDim.y) either reduces through a slab (the last split to arrive
+// on a tile sums the partial tiles and stores: the large-pixel-count convs, where the split
+// count is high) or accumulates with fp32 atomics into the flat gradient buffer; without
+// splitting it stores.  The output is written in the
 // engine's master layout [K][R][S][Creal] (channel padding dropped).
 
 #include "wgrad_body.h"
@@ -41,7 +43,9 @@ void wlaunch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int s
              hipStream_t st) {
   int gx, per, gy;
   wg_grid(g, BM, BN, splits, gx, per, gy);
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(gx, gy), dim3(NT), 0, st, dy, x, g, dw, per);
+  WgradGeom gg = g;
+  if (gx > WG_SEM_INTS) gg.slab = nullptr;   // counters would not fit: atomic splits
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(gx, gy), dim3(NT), 0, st, dy, x, gg, dw, per);
 }
 }  // namespace
 

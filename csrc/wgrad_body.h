@@ -7,6 +7,7 @@
 namespace wgb {
 constexpr int WG_NT = 256;
 constexpr int WG_BKP = 64;  // pixels per stage
+constexpr int WG_SEM_INTS = 1024;   // tile counters at the head of a wgrad slab (4 KB)
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
 
@@ -62,33 +63,74 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
   }
   const int acc_ = tid % ACH;
 
-  const float rpq = 1.f / (float)(g.P * g.Q), rq = 1.f / (float)g.Q;
-  // stage loads into a register set; a stage past this split's range loads the zero page, so
-  // every trip issues the same number of loads and hipcc's counted vmcnt stays exact
+  // Operands through buffer resources with 32-bit byte offsets: an invalid row (padding tap,
+  // past the pixel range, past K) gets an offset beyond the resource and loads zeros -- no
+  // zero-page select, no exec-masked branch, no 64-bit address math per row (the per-row
+  // 64-bit multiplies and the two pixel divisions per stage made the loop VALU-bound).
+  const auto rdy = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, npix * g.K * 2, 0x00020000);
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, g.N * g.H * g.W * g.C * 2,
+                                                    0x00020000);
+  constexpr unsigned BAD = 0x80000000u;
+  // A (dy) rows: pixel pixA + i * (NT / ACH), channel chunk k; advanced by BKP pixels a stage
+  const int k = m0 + acc_ * 8;
+  int pixA = pt0 * BKP + tid / ACH;
+  // B (x) rows: the source pixel's (n, p, q), advanced by BKP pixels a stage without a division
+  // (q += BKP % Q, p += BKP / Q, carries); a 1x1 stride-1 conv reads x at the dy pixel itself
+  const bool pw = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+  const int aq = BKP % g.Q, ap = BKP / g.Q;
+  int pixB = pt0 * BKP + tid / BCH;
+  int bn_[BR], bp_[BR], bq_[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int pix = pixB + i * (NT / BCH);
+    const int pq = g.P * g.Q;
+    bn_[i] = pix / pq;
+    const int rem = pix - bn_[i] * pq;
+    bp_[i] = rem / g.Q;
+    bq_[i] = rem - bp_[i] * g.Q;
+  }
+  // stage loads into a register set; a stage past this split's range loads zeros, so every
+  // trip issues the same number of loads and hipcc's counted vmcnt stays exact
   auto load_stage = [&](int pt, u32x4 (&ra)[AR], u32x4 (&rb)[BR]) {
     const bool live = pt < pt1;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const int row = tid / ACH + i * (NT / ACH);
-      const int pix = pt * BKP + row;
-      const int k = m0 + acc_ * 8;
+      const int pix = pixA + i * (NT / ACH);
       const bool ok = live && pix < npix && k < g.K;
-      // select the address, load unconditionally (no exec-masked branch per row)
-      ra[i] = *(const u32x4*)(ok ? dy + (size_t)pix * g.K + k : g.zero);
+      ra[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rdy, ok ? (unsigned)(pix * g.K + k) * 2u : BAD, 0, 0));
     }
+    pixA += BKP;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int row = tid / BCH + i * (NT / BCH);
-      const int pix = pt * BKP + row;
-      const int px = pix < npix ? pix : 0;
-      const int pq = g.P * g.Q;
-      const int n = udiv24(px, pq, rpq), rem = px - n * pq;
-      const int p = udiv24(rem, g.Q, rq), q = rem - p * g.Q;
-      const int h = p * g.stride - g.pad + xr, ww = q * g.stride - g.pad + xs;
-      const bool ok = live && pix < npix && jval && (unsigned)h < (unsigned)g.H &&
-                      (unsigned)ww < (unsigned)g.W;
-      rb[i] = *(const u32x4*)(ok ? x + ((size_t)(n * g.H + h) * g.W + ww) * g.C + xc8 * 8 : g.zero);
+      unsigned off;
+      bool ok;
+      if (pw) {                          // kernel-uniform
+        const int pix = pixB + i * (NT / BCH);
+        ok = live && jval && pix < npix;
+        off = (unsigned)(pix * g.C + xc8 * 8) * 2u;
+      } else {
+        const int h = bp_[i] * g.stride - g.pad + xr, ww = bq_[i] * g.stride - g.pad + xs;
+        ok = live && jval && bn_[i] < g.N && (unsigned)h < (unsigned)g.H &&
+             (unsigned)ww < (unsigned)g.W;
+        off = (unsigned)(((bn_[i] * g.H + h) * g.W + ww) * g.C + xc8 * 8) * 2u;
+        int q = bq_[i] + aq, p = bp_[i] + ap, n = bn_[i];
+        if (q >= g.Q) {
+          q -= g.Q;
+          ++p;
+        }
+        while (p >= g.P) {
+          p -= g.P;
+          ++n;
+        }
+        bn_[i] = n;
+        bp_[i] = p;
+        bq_[i] = q;
+      }
+      rb[i] = __builtin_bit_cast(u32x4,
+                                 __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? off : BAD, 0, 0));
     }
+    pixB += BKP;
   };
   auto store_stage = [&](int buf, const u32x4 (&ra)[AR], const u32x4 (&rb)[BR]) {
     bf16* a = smem + buf * STAGE;
@@ -179,7 +221,51 @@ MA_DEV void wgrad_body(const bf16* __restrict__ dy, const bf16* __restrict__ x, 
     }
   }
 
-  const bool atomic = gy > 1;
+  // Split-K over pixels with a slab (large pixel counts: many splits, no contended atomics):
+  // each split writes its fp32 partial tile write-through (16 B per lane, coalesced), takes a
+  // ticket on the tile's counter, and the LAST split to arrive sums the others and stores dW
+  // (same hand-off as the dgrad split-K, conv_epi.h finish()).  Without a slab, splits add
+  // into dW with fp32 atomics.
+  bool atomic = gy > 1;
+  if (atomic && g.slab != nullptr) {
+    atomic = false;
+    const int ntiles = (g.K + BM - 1) / BM * ntn;
+    int* sem = (int*)g.slab;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(g.slab + WG_SEM_INTS), 0,
+                                                      0x7fffffff, 0x00020000);
+    constexpr int tile_bytes = TM * TN * NT * 16;
+    const int mine = (by * ntiles + bx) * tile_bytes + tid * 16;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[tm][tn]), rs,
+                                               mine + (tm * TN + tn) * NT * 16, 0, 16 /*sc1*/);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+    int* flag = (int*)smem;
+    __syncthreads();                                     // (also: the last stage's LDS reads)
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(&sem[bx], 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == gy - 1;
+      if (last) __hip_atomic_store(&sem[bx], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the ticket
+    for (int sp = 0; sp < gy; ++sp) {
+      if (sp == by) continue;
+      const int base = (sp * ntiles + bx) * tile_bytes + tid * 16;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] += __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (tm * TN + tn) * NT * 16, 0,
+                                                           16 /*sc1*/));
+    }
+  }
   const int RSCr = g.R * g.S * g.Creal;
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
@@ -210,5 +296,10 @@ inline void wg_grid(const WgradGeom& g, int bm, int bn, int splits, int& gx, int
   per = (ptiles + splits - 1) / splits;
   gy = (ptiles + per - 1) / per;
   gx = mtiles * ntiles;
+}
+
+// bytes of the slab a split launch needs (counters + one partial tile per (split, tile))
+inline size_t wg_slab_bytes(int gx, int gy, int bm, int bn) {
+  return (size_t)WG_SEM_INTS * 4 + (size_t)gx * gy * bm * bn * 4;
 }
 }  // namespace wgb

@@ -17,6 +17,7 @@ import torch
 from . import _chk, lib, ptr, stream_ptr
 
 CU = 256
+WG_SEM_INTS = 1024          # tile counters at the head of a wgrad slab (csrc/wgrad_body.h)
 
 
 def cpad8(c):
@@ -112,11 +113,63 @@ def dgrad_plan(spec: ConvSpec):
 ATOMIC_BUDGET = 1_200_000   # fp32 atomic adds per wgrad launch before splitting stops paying
 
 
+# ResNet-50/224 train batch (B = 128): measured best atomic-split plans, keyed (N, H_in, C, K,
+# R, stride) (bench/r50_bwd_cmp.py --sweep, profiles/r3/r50_bwd_sweep.jsonl).  At these pixel
+# counts the wgrad is latency-bound per block: many more splits than the B = 32 atomic budget
+# allows pay off (4.37 -> 3.02 ms over the net's wgrads).
+MEASURED_WGRAD = {
+    (128, 56, 64, 64, 1, 1): (64, 64, 128),   # 30.1 us (default 46.5)
+    (128, 56, 256, 64, 1, 1): (64, 128, 128),   # 53.7 us (default 60.3)
+    (128, 56, 64, 64, 3, 1): (64, 128, 128),   # 110.2 us (default 142.3)
+    (128, 56, 64, 256, 1, 1): (128, 64, 128),   # 53.5 us (default 60.8)
+    (128, 56, 256, 128, 1, 1): (128, 128, 128),   # 76.7 us (default 119.5)
+    (128, 56, 128, 128, 3, 2): (128, 128, 32),   # 87.7 us (default 137.9)
+    (128, 56, 256, 512, 1, 2): (64, 128, 32),   # 71.7 us (default 118.3)
+    (128, 28, 512, 128, 1, 1): (128, 128, 64),   # 47.2 us (default 52.0)
+    (128, 28, 128, 128, 3, 1): (64, 64, 64),   # 73.6 us (default 134.5)
+    (128, 28, 128, 512, 1, 1): (128, 128, 64),   # 46.6 us (default 48.2)
+    (128, 28, 512, 256, 1, 1): (64, 128, 32),   # 71.9 us (default 93.1)
+    (128, 28, 256, 256, 3, 2): (64, 64, 16),   # 74.4 us (default 129.1)
+    (128, 28, 512, 1024, 1, 2): (128, 128, 16),   # 66.9 us (default 117.6)
+    (128, 14, 1024, 256, 1, 1): (64, 64, 16),   # 37.6 us (default 48.3)
+    (128, 14, 256, 256, 3, 1): (64, 64, 16),   # 73.6 us (default 132.8)
+    (128, 14, 256, 1024, 1, 1): (64, 128, 16),   # 39.1 us (default 49.1)
+    (128, 14, 1024, 512, 1, 1): (128, 64, 8),   # 58.1 us (default 89.4)
+    (128, 14, 512, 512, 3, 2): (64, 64, 4),   # 77.1 us (default 133.8)
+    (128, 14, 1024, 2048, 1, 2): (128, 64, 2),   # 62.3 us (default 133.0)
+    (128, 7, 2048, 512, 1, 1): (64, 64, 4),   # 37.1 us (default 46.8)
+    (128, 7, 512, 512, 3, 1): (64, 64, 4),   # 76.0 us (default 135.6)
+    (128, 7, 512, 2048, 1, 1): (64, 128, 4),   # 40.6 us (default 48.5)
+}
+WG_SPLIT_PIX = 4096          # pixels per split of the large-M heuristic
+WG_SPLIT_MAX = 128
+
+
+def _wgrad_plan_large(spec: ConvSpec):
+    """Large pixel counts (>= 32k): splits ~ M / 4096 (a power of two, <= 128), the largest
+    tile that still gives >= 256 blocks (fitted on the ResNet-50 sweep: 3.37 ms vs the 3.02
+    per-shape optimum and 4.37 for the B = 32 rule)."""
+    ncols = spec.R * spec.S * spec.Cp
+    s = min(WG_SPLIT_MAX, 2 ** round(math.log2(max(1.0, spec.M / WG_SPLIT_PIX))))
+    for bm, bn in ((128, 128), (128, 64), (64, 128), (64, 64)):
+        if (bm > 64 and bm > spec.K) or (bn > 64 and bn > ncols):
+            continue
+        if math.ceil(spec.K / bm) * math.ceil(ncols / bn) * s >= 256:
+            return bm, bn, s
+    return 64, 64, s
+
+
 def wgrad_plan(spec: ConvSpec):
     """wgrad tiles + pixel split.  Measured (bench/bwd_pair_sweep.py, MI355X, B=32): ~1 block
     per CU, each K-split covering >= 4 pixel tiles, and at most ~1.2M fp32 atomics per launch
     (layer4 3x3 512->512: split 1 = 22 us vs split 2 = 36 us); 64x64 tiles unless the weight
-    gradient itself exceeds that budget (then 128x128, unsplit)."""
+    gradient itself exceeds that budget (then 128x128, unsplit).  Large pixel counts (the
+    ResNet-50 train batch): MEASURED_WGRAD, else _wgrad_plan_large."""
+    p = MEASURED_WGRAD.get((spec.N, spec.H, spec.C, spec.K, spec.R, spec.stride))
+    if p is not None and spec.H == spec.W:
+        return p
+    if spec.M >= 32768 and spec.N > 32:
+        return _wgrad_plan_large(spec)
     ncols = spec.R * spec.S * spec.Cp
     out = spec.K * ncols                      # fp32 elements each K-split adds atomically
     if out <= ATOMIC_BUDGET:
@@ -430,22 +483,56 @@ def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=Fals
     return dx
 
 
-def conv_wgrad(dy, x, dw, spec: ConvSpec, plan=None):
-    """dw[K][R][S][C] (fp32, channel padding dropped) += / = wgrad(dy, x)."""
+def wgrad_slab_bytes(spec: ConvSpec, plan):
+    """Slab bytes of a split wgrad that reduces through a slab (csrc/wgrad_body.h): 4 KB of
+    tile counters + one fp32 partial tile per (pixel split, output tile); 0 when unsplit."""
+    bm, bn, splits = plan[:3]
+    ncols = spec.R * spec.S * spec.Cp
+    gx = math.ceil(spec.K / bm) * math.ceil(ncols / bn)
+    ptiles = math.ceil(spec.M / 64)
+    splits = max(1, min(splits, ptiles))
+    per = math.ceil(ptiles / splits)
+    gy = math.ceil(ptiles / per)
+    if gy <= 1 or gx > WG_SEM_INTS:
+        return 0
+    return WG_SEM_INTS * 4 + gx * gy * bm * bn * 4
+
+
+def conv_wgrad(dy, x, dw, spec: ConvSpec, plan=None, slab=None):
+    """dw[K][R][S][C] (fp32, channel padding dropped) += / = wgrad(dy, x).  With ``slab``
+    (>= wgrad_slab_bytes, zero-initialised once) the pixel splits reduce through it and dw is
+    stored; without, split plans add into dw atomically (dw must start at zero)."""
     _chk(dy, torch.bfloat16, 'dy', spec.M * spec.K)
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * spec.Cp)
     _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
     if spec.K % 8:
         raise ValueError('wgrad needs K % 8 == 0')
-    bm, bn, splits = plan or wgrad_plan(spec)
+    _wg_range(spec)
+    bm, bn, splits = (plan or wgrad_plan(spec))[:3]
     lib().wgrad(ptr(dy), ptr(x), ptr(dw), spec.N, spec.H, spec.W, spec.Cp, spec.P, spec.Q,
                 spec.K, spec.R, spec.S, spec.stride, spec.pad, spec.C, bm, bn, splits,
-                stream_ptr())
+                _wslab_ptr(spec, (bm, bn, splits), slab), stream_ptr())
     return dw
 
 
+def _wg_range(spec):
+    # the wgrad kernel addresses dy and x through buffer resources with 32-bit byte offsets
+    if max(spec.M * spec.K, spec.N * spec.H * spec.W * spec.Cp) * 2 >= 2 ** 31:
+        raise ValueError('wgrad: an operand exceeds 2 GiB (32-bit buffer offsets)')
+
+
+def _wslab_ptr(spec, plan, slab):
+    need = wgrad_slab_bytes(spec, plan)
+    if slab is None or need == 0:
+        return 0
+    if slab.numel() * slab.element_size() < need:
+        raise ValueError('wgrad slab too small (%d < %d bytes)'
+                         % (slab.numel() * slab.element_size(), need))
+    return ptr(slab)
+
+
 def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=None,
-             accumulate=False, bw=None):
+             accumulate=False, bw=None, wslab=None):
     """Both backward GEMMs of one conv in ONE launch (csrc/igemm.hip bwd_pair_kernel):
     dx (= conv_dgrad, optional fused BN-backward reduce ``bw``) and dw (= conv_wgrad)."""
     if spec.stride not in (1, 2) or spec.K % 8:
@@ -456,8 +543,9 @@ def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=Non
     _chk(dx, torch.bfloat16, 'dx', spec.N * spec.H * spec.W * Cp)
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
     _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
+    _wg_range(spec)
     bm, bn, splits = dplan or dgrad_plan(spec)
-    wbm, wbn, wsplits = wplan or wgrad_plan(spec)
+    wbm, wbn, wsplits = (wplan or wgrad_plan(spec))[:3]
     Mx = spec.N * spec.H * spec.W
     if splits > 1:
         slab = _slab(slab, slab_bytes(Mx, Cp, bm, bn, splits), dy.device)
@@ -466,9 +554,9 @@ def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=Non
         spec.P, spec.Q, spec.K, spec.H, spec.W, spec.R, spec.S, spec.stride, spec.pad,
         spec.R * spec.S * spec.K // 8, Cp, Mx, bm, bn, splits, *_bw_args(bw, Mx, Cp),
         ptr(x), ptr(dw), spec.N, spec.H, spec.W, Cp, spec.P, spec.Q, spec.K, spec.C, wbm, wbn,
-        wsplits, stream_ptr())
+        wsplits, _wslab_ptr(spec, (wbm, wbn, wsplits), wslab), stream_ptr())
     if not ok:
-        conv_wgrad(dy, x, dw, spec, plan=(wbm, wbn, wsplits))
+        conv_wgrad(dy, x, dw, spec, plan=(wbm, wbn, wsplits), slab=wslab)
         conv_dgrad(dy, wt, dx, spec, slab=slab, plan=(bm, bn, splits), accumulate=accumulate,
                    bw=bw)
     return dx, dw

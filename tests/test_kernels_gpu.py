@@ -207,6 +207,13 @@ def test_conv_bwd_pair_matches_separate_launches(case):
         assert torch.equal(dx, dx2)
     close(dx.float(), dx2.float(), 1e-2, 1e-2)
     close(dw, dw2, 1e-4, 1e-4)
+    # the pair with the wgrad pixel splits reduced through a slab
+    from mercury_amd.ops.conv import wgrad_slab_bytes
+    wp2 = (64, 64, 4)
+    wslab = torch.zeros(max(1, wgrad_slab_bytes(spec, wp2)) // 4 + 1, device=DEV)
+    dw3 = torch.full_like(dw, 3.0)
+    ops.conv_bwd(gyn, wt, dx2, xn, dw3, spec, dplan=dplan, wplan=wp2, slab=slab, wslab=wslab)
+    close(dw3, dw2, 1e-4, 1e-4)
     close(ops.from_nhwc(dx.view(N, H, W, spec.Cp), C), xr.grad)
     close(dw.view(K, R, S, C).permute(0, 3, 1, 2), wr.grad, 2e-2, 2e-2)
 
@@ -226,10 +233,20 @@ def test_conv_wgrad(case):
     dw = torch.zeros(K, R, S, C, device=DEV)
     ops.conv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(x), dw, spec)
     close(dw.permute(0, 3, 1, 2), wr.grad, rtol=2e-2, atol=1e-2)
-    for plan in [(64, 64, 1), (128, 128, 3), (64, 128, 2), (128, 64, 5)]:
+    from mercury_amd.ops.conv import wgrad_slab_bytes
+    plans = [(64, 64, 1), (128, 128, 3), (64, 128, 2), (128, 64, 5)]
+    wslab = torch.zeros(max(wgrad_slab_bytes(spec, p) for p in plans) // 4 + 1, device=DEV)
+    for plan in plans:
         dw2 = torch.zeros_like(dw)
         ops.conv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(x), dw2, spec, plan=plan)
         close(dw2, dw, rtol=1e-2, atol=1e-2)
+        # split plans reduced through the slab (stores dw: a non-zero start is overwritten);
+        # twice, so the tile counters the last arriver resets are exercised
+        for _ in range(2):
+            dw3 = torch.full_like(dw, 7.0)
+            ops.conv_wgrad(ops.to_nhwc(gy), ops.to_nhwc(x), dw3, spec, plan=plan, slab=wslab)
+            close(dw3, dw, rtol=1e-2, atol=1e-2)
+    assert int(wslab[:1024].abs().sum()) == 0          # counters back at zero
 
 
 def _bn_ref(y, gamma, beta, eps=1e-5):
