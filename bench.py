@@ -100,7 +100,35 @@ def diagnostics(eng, steps, ws):
     if eng.check_order:
         dp['order_violations'] = eng.order_violations()[0]
     out['dp'] = dp
+    if ws == 1 and not eng.dp and eng.graphs:
+        out['solo_ms'] = solo_graph_ms(eng)
     return out
+
+
+def solo_graph_ms(eng, reps=5):
+    """Each step graph replayed ALONE (no concurrent stream): how much of the step is
+    contention between the scoring and the training stream.  Untimed diagnostic, after the
+    timed loop."""
+    import torch
+    g = eng.graphs
+
+    def t(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / reps, 4)
+
+    def score():
+        g['score'].replay()
+        if 'score_sample' in g:
+            g['score_sample'].replay()
+    return {'score': t(score), 'train': t(lambda: [x.replay() for x, _ in g['train']]),
+            'tail': t(lambda: g['tail'].replay())}
 
 
 def main():

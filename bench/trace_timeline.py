@@ -60,15 +60,20 @@ def main():
         union += ce - cs
     print('any-queue busy %.1f us/step (%.1f%%), all-idle %.1f us/step'
           % (union / 1e3 / nsteps, 100 * union / 1e3 / nsteps / wall, wall - union / 1e3 / nsteps))
-    names = defaultdict(lambda: [0, 0])
-    for r in win:
-        n = r['Kernel_Name'].replace('(anonymous namespace)::', '').replace('void ', '')
-        n = n.split('(')[0][:60]
-        names[n][0] += 1
-        names[n][1] += r['e'] - r['s']
-    print('%-62s %8s %10s' % ('kernel', 'n/step', 'us/step'))
-    for n, (c, d) in sorted(names.items(), key=lambda x: -x[1][1])[:30]:
-        print('%-62s %8.1f %10.1f' % (n, c / nsteps, d / 1e3 / nsteps))
+    def table(rows, top):
+        names = defaultdict(lambda: [0, 0])
+        for r in rows:
+            n = r['Kernel_Name'].replace('(anonymous namespace)::', '').replace('void ', '')
+            n = n.split('(')[0][:60]
+            names[n][0] += 1
+            names[n][1] += r['e'] - r['s']
+        print('%-62s %8s %10s' % ('kernel', 'n/step', 'us/step'))
+        for n, (c, d) in sorted(names.items(), key=lambda x: -x[1][1])[:top]:
+            print('%-62s %8.1f %10.1f' % (n, c / nsteps, d / 1e3 / nsteps))
+    table(win, 30)
+    for q, ks in sorted(byq.items()):
+        print('--- queue %s' % q)
+        table(ks, 15)
 
 
 if __name__ == '__main__':

@@ -103,6 +103,15 @@ MA_DEV void bn_mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, 
 template <int BM, int BN, int WM>
 using AccT = f32x4[BM / (16 * WM)][BN * WM / 64];
 
+// output row of GEMM row ``row`` (identity unless a stride-2 dgrad parity class, EpiParams.rm_*)
+MA_DEV int phys_row(const EpiParams& e, int row) {
+  if (e.rm_hc == 0) return row;
+  const int per = e.rm_hc * e.rm_wc;
+  const int n = udiv24(row, per, 1.f / (float)per), rem = row - n * per;
+  const int i = udiv24(rem, e.rm_wc, 1.f / (float)e.rm_wc), j = rem - i * e.rm_wc;
+  return (n * e.rm_h + 2 * i + e.rm_ph) * e.rm_w + 2 * j + e.rm_pw;
+}
+
 template <int BM, int BN, int WM = 2>
 MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int M, int N,
                      int m0, int n0) {
@@ -246,7 +255,7 @@ MA_DEV void epilogue(AccT<BM, BN, WM>& acc, char* smem, const EpiParams& e, int 
     const int row = m0 + rl, col = colc;
     if (row >= M || col >= N) continue;
     bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
-    const size_t off = (size_t)row * e.ldo + col;
+    const size_t off = (size_t)phys_row(e, row) * e.ldo + col;
     bf16* dst = e.out + off;
     if (e.accumulate) {
       const bf16x8 o = *(const bf16x8*)dst;

@@ -16,6 +16,11 @@ struct ConvGeom {
   int Ncols;         // GEMM N (output channels)
   int M;             // GEMM M = images * RP * RQ
   const bf16* zero;  // 16-byte zero page for padding taps (set by the launcher; kernel arg -> SGPR)
+  // stride-2 dgrad parity class (dgrad_s2_launch): the class is a stride-1 FORWARD gather of dy
+  // whose virtual tap (r', s') reads the real weight tap (trb - 2 r', tsb - 2 s') of a [C][R][S][K]
+  // weight with row stride ldb; trb < 0: plain (B chunk = k chunk, row stride Kc * 8)
+  int ldb = 0;
+  int trb = -1, tsb = 0, tS = 0;
 };
 
 // BN-backward sums are kept as SUMS_R replicas [SUMS_R][3][C]: a producer block adds into
@@ -46,6 +51,9 @@ struct EpiParams {
   float* bw_sums;          // [SUMS_R][3][ldo] replicas (SUMS_R above) or null (feature off)
   float bw_inv_count, bw_eps;
   int bw_act;
+  // output row remap of a stride-2 dgrad parity class: GEMM row (n, i, j) over rm_hc x rm_wc is
+  // the output pixel (n, 2i + rm_ph, 2j + rm_pw) of an rm_h x rm_w image; rm_hc == 0: identity
+  int rm_hc = 0, rm_wc = 0, rm_h = 0, rm_w = 0, rm_ph = 0, rm_pw = 0;
 };
 
 // Forward-only A-operand prologue: the conv reads the PRODUCING conv's raw output y and applies
@@ -87,6 +95,12 @@ struct WgradGeom {
 };
 void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, int bm, int bn,
                   int splits, hipStream_t st);
+
+// stride-2 dgrad as four parity classes of input pixels in ONE launch (each class a stride-1
+// forward gather of dy over only the taps that reach it: 1/2/2/4 of a 3x3's 9); returns 0 when
+// the conv does not qualify (stride 2, 3x3 pad 1 or 1x1 pad 0, dy channels % 64)
+int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
+                    int bn, int H, int W, int N, hipStream_t st);
 
 // dgrad (TRANS igemm) + wgrad in ONE launch (returns 0 if the tile pair is not instantiated)
 int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,

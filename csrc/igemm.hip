@@ -236,10 +236,11 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
     if (off < 0) ah[i] = -(1 << 28);
   }
   int boff[BR];
+  const int ldb = g.ldb ? g.ldb : Kelems;
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int n = n0 + (tid >> 3) + 32 * i;
-    boff[i] = n < g.Ncols ? n * Kelems : -1;
+    boff[i] = n < g.Ncols ? n * ldb : -1;
   }
   KCursor kc;
   kc.init(g, kt0);
@@ -277,6 +278,9 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       pz = 0;
     }
     const int toff = tap_offset<TRANS>(g, r, s) + c8 * 8;
+    // B chunk: the k chunk itself, or (parity class) the real weight tap of virtual tap (r, s)
+    const int bch = g.trb < 0 ? kt * 8 + cc
+                              : ((g.trb - 2 * r) * g.tS + (g.tsb - 2 * s)) * (g.SC >> 3) + c8;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const bool ok = kval && tap_ok<TRANS>(g, ah[i], aw[i], r, s);
@@ -290,7 +294,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const bool ok = kval && boff[i] >= 0;
-      rb[i] = *(const u32x4*)(ok ? wt + boff[i] + (kt * 8 + cc) * 8 : zp);
+      rb[i] = *(const u32x4*)(ok ? wt + boff[i] + bch * 8 : zp);
     }
   };
   auto store_stage = [&](int buf, u32x4 (&ra)[AR], const u32x4 (&rb)[BR]) {
@@ -477,6 +481,54 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
   launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), st);
 }
 
+// ---------------------------------------------------------------- stride-2 dgrad classes
+// A stride-2 dgrad as a TRANS gather evaluates all R*S taps for every input pixel although only
+// the taps whose parity matches the pixel's reach it (3x3 pad 1: 1, 2, 2 or 4 of 9; 1x1: 1 or
+// 0 of 1) -- 3/4 of its MFMAs multiply the zero page.  Split the input pixels into the four
+// parity classes (h % 2, w % 2): class (ph, pw) is a stride-1 FORWARD gather of dy over
+// (N, ceil-half H, ceil-half W) rows with only its own taps, and its output rows scatter to
+// (n, 2i + ph, 2j + pw) (EpiParams rm_*).  The four classes run as one launch; a class with
+// no taps (1x1: all but (0, 0)) writes zeros.
+struct S2Geom {
+  ConvGeom g[4];
+  int pre[5];          // tile prefix over the classes
+  int hc[4], wc[4];    // class row-space dims
+  int H, W;            // dx spatial dims
+};
+
+template <int BM, int BN, int PF>
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void dgrad_s2_kernel(const bf16* __restrict__ dy,
+                                                           const bf16* __restrict__ wt,
+                                                           S2Geom sg, EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
+  const int b = blockIdx.x;
+  const int c = (b >= sg.pre[1]) + (b >= sg.pre[2]) + (b >= sg.pre[3]);   // uniform
+  EpiParams ec = e;
+  ec.rm_hc = sg.hc[c];
+  ec.rm_wc = sg.wc[c];
+  ec.rm_h = sg.H;
+  ec.rm_w = sg.W;
+  ec.rm_ph = c >> 1;
+  ec.rm_pw = c & 1;
+  const ProParams none{};
+  const int bx = b - sg.pre[c];
+  igemm_nt_body<BM, BN, false, false, PF>(dy, wt, sg.g[c], ec, 1 << 20, smem, bx, 0,
+                                          sg.pre[c + 1] - sg.pre[c], 1, none);
+}
+
+template <int BM, int BN>
+void s2_cfg(const bf16* dy, const bf16* wt, const S2Geom& sg, const EpiParams& e, hipStream_t st) {
+  const int grid = sg.pre[4];
+  if (grid == 0) return;
+  if constexpr (PAIR_PF<BM, BN>() == 2) {
+    if (grid <= 512) {
+      hipLaunchKernelGGL((dgrad_s2_kernel<BM, BN, 2>), dim3(grid), dim3(NT), 0, st, dy, wt, sg, e);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((dgrad_s2_kernel<BM, BN, 1>), dim3(grid), dim3(NT), 0, st, dy, wt, sg, e);
+}
+
 // ---------------------------------------------------------------- dgrad + wgrad pair launch
 // The two backward GEMMs of a conv read the same dy and are independent; at small batch each
 // alone leaves most of the 256 CUs idle, and a second stream costs a cross-queue graph edge per
@@ -566,6 +618,73 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const E
   MA_CASE(256, 64)
   MA_CASE(256, 128)
 #undef MA_CASE
+}
+
+int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const EpiParams& e_in,
+                    int bm, int bn, int H, int W, int N, hipStream_t st) {
+  // gt: the TRANS geometry (SH, SW = dy spatial, SC = dy channels, R, S, stride, pad, Ncols = C)
+  if (gt.stride != 2 || (gt.SC & 63) || gt.R != gt.S) return 0;
+  if (!((gt.R == 3 && gt.pad == 1) || (gt.R == 1 && gt.pad == 0))) return 0;
+  S2Geom sg{};
+  sg.H = H;
+  sg.W = W;
+  sg.pre[0] = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int ph = c >> 1, pw = c & 1;
+    // taps reaching parity ph: r == (ph + pad) mod 2; virtual tap r' = 0.. reads r = trb - 2 r'
+    int rv = 0, trb = -1;
+    for (int r = gt.R - 1; r >= 0; --r)
+      if (((ph + gt.pad - r) & 1) == 0) {
+        if (trb < 0) trb = r;
+        ++rv;
+      }
+    int sv = 0, tsb = -1;
+    for (int s = gt.S - 1; s >= 0; --s)
+      if (((pw + gt.pad - s) & 1) == 0) {
+        if (tsb < 0) tsb = s;
+        ++sv;
+      }
+    // the first virtual tap reads dy pixel i + (ph + pad - trb) / 2: zero offset for the
+    // supported shapes (3x3 pad 1, 1x1 pad 0), so the class gather is stride 1, pad 0
+    if ((rv && ph + gt.pad - trb != 0) || (sv && pw + gt.pad - tsb != 0)) return 0;
+    const int hc = (H - ph + 1) / 2, wc = (W - pw + 1) / 2;
+    ConvGeom g{};
+    g.SH = gt.SH;
+    g.SW = gt.SW;
+    g.SC = gt.SC;
+    g.RP = hc;
+    g.RQ = wc;
+    g.R = rv > 0 ? rv : 1;
+    g.S = sv > 0 ? sv : 1;
+    g.stride = 1;
+    g.pad = 0;
+    g.Kc = (rv * sv) * (gt.SC >> 3);    // 0: no tap reaches the class -> zeros
+    g.Ncols = gt.Ncols;
+    g.M = N * hc * wc;
+    g.zero = zero_page();
+    g.ldb = gt.R * gt.S * gt.SC;
+    g.trb = trb < 0 ? 0 : trb;
+    g.tsb = tsb < 0 ? 0 : tsb;
+    g.tS = gt.S;
+    sg.g[c] = g;
+    sg.hc[c] = hc;
+    sg.wc[c] = wc;
+    sg.pre[c + 1] = sg.pre[c] + ((g.M + bm - 1) / bm) * ((g.Ncols + bn - 1) / bn);
+  }
+  EpiParams e = e_in;
+  e.slab = nullptr;                     // one K slice per tile
+#define MA_CASE(BM_, BN_)                    \
+  if (bm == BM_ && bn == BN_) {              \
+    s2_cfg<BM_, BN_>(dy, wt, sg, e, st);     \
+    return 1;                                \
+  }
+  MA_CASE(128, 128)
+  MA_CASE(128, 64)
+  MA_CASE(64, 128)
+  MA_CASE(64, 64)
+  MA_CASE(256, 64)
+#undef MA_CASE
+  return 0;
 }
 
 int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g_in, const EpiParams& e,

@@ -10,6 +10,7 @@ to straddle a 32-image stat group; ``pick_tiles`` enforces that.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -460,9 +461,30 @@ def _bw_args(bw, Mx, Cp):
             _ACT[bw.get('act')])
 
 
+DGRAD_S2 = os.environ.get('MERCURY_DGRAD_S2', '1') == '1'
+
+
+def dgrad_s2_ok(spec: ConvSpec):
+    """The stride-2 dgrad runs as four parity classes (csrc/igemm.hip dgrad_s2_launch): only
+    the taps that reach an input pixel are multiplied (3x3: 9/4 per pixel instead of 9)."""
+    return (DGRAD_S2 and spec.stride == 2 and spec.R == spec.S and spec.K % 64 == 0 and
+            ((spec.R == 3 and spec.pad == 1) or (spec.R == 1 and spec.pad == 0)))
+
+
+def dgrad_s2_plan(spec: ConvSpec):
+    """Tiles of the class dgrad: the classes hold a quarter of the rows each, so the tile
+    choice follows the total row count (one K slice per tile)."""
+    M = spec.N * spec.H * spec.W
+    N = spec.Cp
+    bn = 128 if N >= 128 else 64
+    bm = 128 if math.ceil(M / 128) * math.ceil(N / bn) >= 2 * CU else 64
+    return bm, bn, 1
+
+
 def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=False, bw=None):
-    """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2.  ``bw``: also reduce
-    the BN-backward sums of the (final, post-accumulate) dx in the epilogue."""
+    """dx[N*H*W][Cp] = dgrad(dy [M][K], wt [C][R][S][K]).  Stride 1 or 2 (stride 2 as parity
+    classes where dgrad_s2_ok; ``plan`` then sizes its tiles).  ``bw``: also reduce the
+    BN-backward sums of the (final, post-accumulate) dx in the epilogue."""
     if spec.stride not in (1, 2):
         raise ValueError('dgrad supports stride 1/2')
     if spec.K % 8:
@@ -471,8 +493,14 @@ def conv_dgrad(dy, wt, dx, spec: ConvSpec, slab=None, plan=None, accumulate=Fals
     _chk(dy, torch.bfloat16, 'dy', spec.M * spec.K)
     _chk(wt, torch.bfloat16, 'wt', Cp * spec.R * spec.S * spec.K)
     _chk(dx, torch.bfloat16, 'dx', spec.N * spec.H * spec.W * Cp)
-    bm, bn, splits = plan or dgrad_plan(spec)
     Mx = spec.N * spec.H * spec.W
+    if dgrad_s2_ok(spec):
+        bm, bn, _ = plan or dgrad_s2_plan(spec)
+        if lib().dgrad_s2(ptr(dy), ptr(wt), ptr(dx), Cp, int(accumulate), spec.P, spec.Q,
+                          spec.K, spec.R, spec.S, spec.stride, spec.pad, Cp, bm, bn, spec.H,
+                          spec.W, spec.N, stream_ptr(), *_bw_args(bw, Mx, Cp)):
+            return dx
+    bm, bn, splits = plan or dgrad_plan(spec)
     if splits > 1:
         slab = _slab(slab, slab_bytes(Mx, Cp, bm, bn, splits), dy.device)
     lib().igemm(ptr(dy), ptr(wt), ptr(dx), Cp, 0, 0, Cp, Mx, int(accumulate),
@@ -544,6 +572,11 @@ def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=Non
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
     _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
     _wg_range(spec)
+    if dgrad_s2_ok(spec):
+        # stride 2: the wgrad alone, then the dgrad as parity classes (two launches)
+        conv_wgrad(dy, x, dw, spec, plan=wplan, slab=wslab)
+        conv_dgrad(dy, wt, dx, spec, plan=dgrad_s2_plan(spec), accumulate=accumulate, bw=bw)
+        return dx, dw
     bm, bn, splits = dplan or dgrad_plan(spec)
     wbm, wbn, wsplits = (wplan or wgrad_plan(spec))[:3]
     Mx = spec.N * spec.H * spec.W

@@ -40,6 +40,8 @@ CONV_CASES = [
     (8, 8, 8, 256, 512, 3, 3, 2, 1),     # small M -> split-K
     (32, 4, 4, 512, 512, 3, 3, 1, 1),    # layer4 at batch 32
     (2, 16, 16, 96, 24, 1, 1, 1, 0),     # MobileNet-style odd channels
+    (2, 15, 15, 64, 128, 3, 3, 2, 1),    # odd input: uneven stride-2 dgrad parity classes
+    (2, 15, 13, 64, 64, 1, 1, 2, 0),     # odd 1x1 stride-2 (three classes get no tap)
 ]
 
 
