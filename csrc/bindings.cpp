@@ -89,6 +89,26 @@ PYBIND11_MODULE(_C, m) {
     if (ok) check_launch("dgrad_s2");
     return ok;
   });
+  m.def("conv_bwd_pair_s2", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int ldo, int accumulate,
+                               int SH, int SW, int SC, int R, int Sk, int stride, int pad,
+                               int Ncols, int bm, int bn, int H, int W, int N, uintptr_t bw_out,
+                               uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
+                               uintptr_t bw_stats2, uintptr_t bw_sums, float bw_inv_count,
+                               float bw_eps, int bw_act, uintptr_t x, uintptr_t dw, int C, int Pp,
+                               int Q, int K, int Creal, int wbm, int wbn, int wsplits,
+                               uintptr_t wslab, uintptr_t st) {
+    ConvGeom g{SH, SW, SC, H, W, R, Sk, stride, pad, R * Sk * SC / 8, Ncols, N * H * W};
+    EpiParams e{P<bf16>(dx), ldo, nullptr, nullptr, 0, N * H * W, accumulate, nullptr,
+                P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats),
+                P<const bf16>(bw_y2), P<const float>(bw_stats2), P<float>(bw_sums), bw_inv_count,
+                bw_eps, bw_act};
+    WgradGeom wg{N, H, W, C, Pp, Q, K, R, Sk, stride, pad, Creal, nullptr, P<float>(wslab)};
+    const int ok = conv_bwd_pair_s2_launch(P<const bf16>(dy), P<const bf16>(wt), g, e, bm, bn, H,
+                                           W, N, P<const bf16>(x), wg, P<float>(dw), wbm, wbn,
+                                           wsplits, S(st));
+    if (ok) check_launch("conv_bwd_pair_s2");
+    return ok;
+  });
   m.attr("SUMS_R") = SUMS_R;   // replicas of the BN-backward sums ([SUMS_R][3][C])
   // 1x1 conv as a persistent LDS-DMA GEMM (pgemm.hip); returns 0 if unsupported
   m.def("pgemm", [](uintptr_t a, uintptr_t b, uintptr_t out, uintptr_t stats, int M, int N, int K,

@@ -102,6 +102,12 @@ void wgrad_launch(const bf16* dy, const bf16* x, const WgradGeom& g, float* dw, 
 int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e, int bm,
                     int bn, int H, int W, int N, hipStream_t st);
 
+// the pair with the stride-2 class dgrad (dgrad tiles 64 x 64; returns 0 if not instantiated)
+int conv_bwd_pair_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
+                            int bm, int bn, int H, int W, int N, const bf16* x,
+                            const WgradGeom& wg, float* dw, int wbm, int wbn, int wsplits,
+                            hipStream_t st);
+
 // dgrad (TRANS igemm) + wgrad in ONE launch (returns 0 if the tile pair is not instantiated)
 int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, const EpiParams& e,
                          int bm, int bn, int splits, const bf16* x, const WgradGeom& wg, float* dw,

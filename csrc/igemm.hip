@@ -557,6 +557,37 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_kernel(const bf16* __restrict_
   }
 }
 
+// the same pair with a stride-2 dgrad as parity classes (S2Geom): blocks [0, nw) wgrad tiles,
+// the rest class-dgrad tiles
+template <int DBM, int DBN, int WBM, int WBN>
+__global__ __launch_bounds__(NT, 2) void bwd_pair_s2_kernel(const bf16* __restrict__ dy,
+                                                             const bf16* __restrict__ wt,
+                                                             S2Geom sg, EpiParams e,
+                                                             const bf16* __restrict__ x,
+                                                             WgradGeom wg, float* __restrict__ dw,
+                                                             int wper, int wgx, int wgy) {
+  constexpr int DB = Smem<DBM, DBN>::bytes(2), WB = wgb::WgSmem<WBM, WBN>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[DB > WB ? DB : WB];
+  const int nw = wgx * wgy;
+  const int b = blockIdx.x;
+  if (b < nw) {
+    wgb::wgrad_body<WBM, WBN>(dy, x, wg, dw, wper, (bf16*)smem, b % wgx, b / wgx, wgy);
+    return;
+  }
+  const int d = b - nw;
+  const int c = (d >= sg.pre[1]) + (d >= sg.pre[2]) + (d >= sg.pre[3]);
+  EpiParams ec = e;
+  ec.rm_hc = sg.hc[c];
+  ec.rm_wc = sg.wc[c];
+  ec.rm_h = sg.H;
+  ec.rm_w = sg.W;
+  ec.rm_ph = c >> 1;
+  ec.rm_pw = c & 1;
+  const ProParams none{};
+  igemm_nt_body<DBM, DBN, false, false, PAIR_PF<DBM, DBN>()>(
+      dy, wt, sg.g[c], ec, 1 << 20, smem, d - sg.pre[c], 0, sg.pre[c + 1] - sg.pre[c], 1, none);
+}
+
 template <int DBM, int DBN, int WBM, int WBN>
 void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
               const bf16* x, WgradGeom wg, float* dw, int wsplits, hipStream_t st) {
@@ -620,12 +651,12 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const E
 #undef MA_CASE
 }
 
-int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const EpiParams& e_in,
-                    int bm, int bn, int H, int W, int N, hipStream_t st) {
+// the four class geometries of a stride-2 dgrad (false: the conv does not qualify)
+static bool s2_geom(const ConvGeom& gt, int bm, int bn, int H, int W, int N, S2Geom& sg) {
   // gt: the TRANS geometry (SH, SW = dy spatial, SC = dy channels, R, S, stride, pad, Ncols = C)
-  if (gt.stride != 2 || (gt.SC & 63) || gt.R != gt.S) return 0;
-  if (!((gt.R == 3 && gt.pad == 1) || (gt.R == 1 && gt.pad == 0))) return 0;
-  S2Geom sg{};
+  if (gt.stride != 2 || (gt.SC & 63) || gt.R != gt.S) return false;
+  if (!((gt.R == 3 && gt.pad == 1) || (gt.R == 1 && gt.pad == 0))) return false;
+  sg = S2Geom{};
   sg.H = H;
   sg.W = W;
   sg.pre[0] = 0;
@@ -646,7 +677,7 @@ int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const Ep
       }
     // the first virtual tap reads dy pixel i + (ph + pad - trb) / 2: zero offset for the
     // supported shapes (3x3 pad 1, 1x1 pad 0), so the class gather is stride 1, pad 0
-    if ((rv && ph + gt.pad - trb != 0) || (sv && pw + gt.pad - tsb != 0)) return 0;
+    if ((rv && ph + gt.pad - trb != 0) || (sv && pw + gt.pad - tsb != 0)) return false;
     const int hc = (H - ph + 1) / 2, wc = (W - pw + 1) / 2;
     ConvGeom g{};
     g.SH = gt.SH;
@@ -671,6 +702,13 @@ int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const Ep
     sg.wc[c] = wc;
     sg.pre[c + 1] = sg.pre[c] + ((g.M + bm - 1) / bm) * ((g.Ncols + bn - 1) / bn);
   }
+  return true;
+}
+
+int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const EpiParams& e_in,
+                    int bm, int bn, int H, int W, int N, hipStream_t st) {
+  S2Geom sg;
+  if (!s2_geom(gt, bm, bn, H, W, N, sg)) return 0;
   EpiParams e = e_in;
   e.slab = nullptr;                     // one K slice per tile
 #define MA_CASE(BM_, BN_)                    \
@@ -684,6 +722,34 @@ int dgrad_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt, const Ep
   MA_CASE(64, 64)
   MA_CASE(256, 64)
 #undef MA_CASE
+  return 0;
+}
+
+int conv_bwd_pair_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt,
+                            const EpiParams& e_in, int bm, int bn, int H, int W, int N,
+                            const bf16* x, const WgradGeom& wg_in, float* dw, int wbm, int wbn,
+                            int wsplits, hipStream_t st) {
+  S2Geom sg;
+  if (!s2_geom(gt, bm, bn, H, W, N, sg)) return 0;
+  EpiParams e = e_in;
+  e.slab = nullptr;
+  WgradGeom wg = wg_in;
+  wg.zero = zero_page();
+#define MA_W(DBM_, DBN_, WBM_, WBN_)                                                        \
+  if (bm == DBM_ && bn == DBN_ && wbm == WBM_ && wbn == WBN_) {                            \
+    int wgx, wper, wgy;                                                                    \
+    wgb::wg_grid(wg, WBM_, WBN_, wsplits, wgx, wper, wgy);                                 \
+    if (wgx > wgb::WG_SEM_INTS) wg.slab = nullptr;                                         \
+    hipLaunchKernelGGL((bwd_pair_s2_kernel<DBM_, DBN_, WBM_, WBN_>),                        \
+                       dim3(sg.pre[4] + wgx * wgy), dim3(NT), 0, st, dy, wt, sg, e, x, wg, dw, \
+                       wper, wgx, wgy);                                                    \
+    return 1;                                                                              \
+  }
+  MA_W(64, 64, 64, 64)
+  MA_W(64, 64, 128, 128)
+  MA_W(64, 64, 64, 128)
+  MA_W(64, 64, 128, 64)
+#undef MA_W
   return 0;
 }
 

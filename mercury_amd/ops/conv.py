@@ -572,14 +572,21 @@ def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=Non
     _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * Cp)
     _chk(dw, torch.float32, 'dw', spec.K * spec.R * spec.S * spec.C)
     _wg_range(spec)
-    if dgrad_s2_ok(spec):
-        # stride 2: the wgrad alone, then the dgrad as parity classes (two launches)
-        conv_wgrad(dy, x, dw, spec, plan=wplan, slab=wslab)
-        conv_dgrad(dy, wt, dx, spec, plan=dgrad_s2_plan(spec), accumulate=accumulate, bw=bw)
-        return dx, dw
     bm, bn, splits = dplan or dgrad_plan(spec)
     wbm, wbn, wsplits = (wplan or wgrad_plan(spec))[:3]
     Mx = spec.N * spec.H * spec.W
+    if dgrad_s2_ok(spec):
+        # stride 2: the dgrad as parity classes; at the small train batch in the same launch as
+        # the wgrad (64 x 64 class tiles), else two launches with the class dgrad's own tiles
+        if spec.N <= 32 and lib().conv_bwd_pair_s2(
+                ptr(dy), ptr(wt), ptr(dx), Cp, int(accumulate), spec.P, spec.Q, spec.K, spec.R,
+                spec.S, spec.stride, spec.pad, Cp, 64, 64, spec.H, spec.W, spec.N,
+                *_bw_args(bw, Mx, Cp), ptr(x), ptr(dw), Cp, spec.P, spec.Q, spec.K, spec.C, wbm,
+                wbn, wsplits, _wslab_ptr(spec, (wbm, wbn, wsplits), wslab), stream_ptr()):
+            return dx, dw
+        conv_wgrad(dy, x, dw, spec, plan=(wbm, wbn, wsplits), slab=wslab)
+        conv_dgrad(dy, wt, dx, spec, plan=dgrad_s2_plan(spec), accumulate=accumulate, bw=bw)
+        return dx, dw
     if splits > 1:
         slab = _slab(slab, slab_bytes(Mx, Cp, bm, bn, splits), dy.device)
     ok = lib().conv_bwd_pair(
