@@ -152,6 +152,9 @@ def main():
     ap.add_argument('--sampler', default='alias', choices=('alias', 'cdf', 'groupwise'),
                     help="pool draw kernel, or 'groupwise': draws from the HBM importance table "
                          'over the current contiguous-slice group (Groupwise_Sampler)')
+    ap.add_argument('--replay-only', choices=('train', 'score'), default=None,
+                    help='profiling aid: after warm-up, replay only this step graph --steps '
+                         'times (no concurrent stream) and print its time per replay')
     ap.add_argument('--diag-steps', type=int, default=5,
                     help='untimed steps after the timed loop with device-phase events')
     args = ap.parse_args()
@@ -221,6 +224,20 @@ def main():
         return float(dt.item())
 
     eng = make(True)
+    if args.replay_only:
+        run(eng, 0, args.warmup)
+        g = eng.graphs
+        rep = (lambda: [x.replay() for x, _ in g['train']]) if args.replay_only == 'train' \
+            else (lambda: g['score'].replay())
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rep()
+        torch.cuda.synchronize()
+        print(json.dumps({'replay_only': args.replay_only, 'config': args.config,
+                          'ms_per_replay': round((time.perf_counter() - t0) * 1e3 / args.steps,
+                                                 4)}), flush=True)
+        return
     t_is = run(eng, args.steps, args.warmup)
     m = eng.read_meters()
     diag = diagnostics(eng, args.diag_steps, ws)

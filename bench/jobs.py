@@ -101,9 +101,14 @@ def job_trace(o, a):
     run(['rocprofv3', '--kernel-trace', '--stats', '--output-format', 'csv', '-d', tr, '-o',
          'run', '--', PY, 'bench.py', '--steps', '60', '--warmup', '10', '--no-overhead'] +
         shlex.split(a.args or ''), os.path.join(o, 'bench.log'), 300)
-    run([PY, 'bench/trace_timeline.py', tr, 'optimizer_fused', '40'],
+    marker = 'optimizer_fused'
+    if '--replay-only' in (a.args or ''):
+        marker = 'head_bwd' if 'train' in a.args else 'pool_build'
+    run([PY, 'bench/trace_timeline.py', tr, marker, '40'],
         os.path.join(o, 'timeline.txt'), 120)
     tail(os.path.join(o, 'timeline.txt'), 30)
+    if '--replay-only' in (a.args or ''):
+        return
     run([PY, 'bench/host_overhead.py'], os.path.join(o, 'host_overhead.log'), 240)
     tail(os.path.join(o, 'host_overhead.log'), 12)
 

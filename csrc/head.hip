@@ -10,6 +10,8 @@
 //
 // One workgroup per sample: the pooled feature vector and the logits stay in
 // LDS; dot products are wave64 reductions.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -329,12 +331,23 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadBwdArgs a) {
 void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
   HeadArgs a = a0;
   a.logits_ready = 0;
-  // wide heads: pool + fp32 tiled FC as their own launches (needs the pooled/logits workspaces)
-  if (a.pooled && a.logits && (long long)a.classes * a.C >= WIDE && a.C % 16 == 0) {
+  static const int path = [] {
+    const char* v = getenv("MERCURY_HEAD_PATH");   // (A/B: 0 auto, 1 per-sample, 2 pool + GEMM)
+    return v ? atoi(v) : 0;
+  }();
+  const bool wide = path == 2 || (path == 0 && (long long)a.classes * a.C >= WIDE);
+  // wide heads: pool + fp32 tiled FC as their own launches (needs the pooled/logits workspaces);
+  // the FC reduction is split over the channels so the launch fills the GPU (slices add into
+  // the zeroed logits)
+  if (wide && a.pooled && a.logits && a.C % 16 == 0) {
     hipLaunchKernelGGL(head_pool_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0, st,
                        a.act, a.pooled, a.B, a.HW, a.C);
+    const int tiles = ((a.B + LT - 1) / LT) * ((a.classes + LT - 1) / LT);
+    int z = 1;
+    while (tiles * z * 2 <= 256 && a.C / (z * 2) >= 4 * LK) z *= 2;
+    if (z > 1) (void)hipMemsetAsync(a.logits, 0, sizeof(float) * a.B * a.classes, st);
     hipLaunchKernelGGL((head_gemm_kernel<true, true, 0>),
-                       dim3((a.B + LT - 1) / LT, (a.classes + LT - 1) / LT), dim3(NT), 0, st,
+                       dim3((a.B + LT - 1) / LT, (a.classes + LT - 1) / LT, z), dim3(NT), 0, st,
                        a.pooled, a.C, a.w, a.C, a.b, (void*)a.logits, a.B, a.classes, a.C, 1, 1.f);
     a.logits_ready = 1;
   }
