@@ -545,6 +545,33 @@ PYBIND11_MODULE(_C, m) {
                         pad, S(st), bw_sums ? &bw : nullptr);
     check_launch("dwconv_dgrad");
   });
+  m.def("dwconv_wgrad_blocks", &dwconv_wgrad_blocks);
+  m.def("dwconv_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t dw, int N,
+                         int H, int W, int C, int Pp, int Q, int stride, int pad, uintptr_t slab,
+                         int reduce, uintptr_t st, uintptr_t bw_out, uintptr_t bw_y,
+                         uintptr_t bw_stats, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
+                         int bw_act) {
+    DwBw bw{P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats), P<float>(bw_sums),
+            bw_inv_count, bw_eps, bw_act};
+    dwconv_bwd_launch(P<const bf16>(dy), P<const bf16>(x), P<const float>(w), P<bf16>(dx),
+                      P<float>(dw), N, H, W, C, Pp, Q, stride, pad, P<float>(slab),
+                      bw_sums ? &bw : nullptr, reduce != 0, S(st));
+    check_launch("dwconv_bwd");
+  });
+  m.def("dwconv_wgrad_reduce_batch", [](std::vector<uintptr_t> slabs, std::vector<uintptr_t> dws,
+                                        std::vector<int> Cs, std::vector<int> nblks, uintptr_t st) {
+    const size_t n = slabs.size();
+    if (dws.size() != n || Cs.size() != n || nblks.size() != n)
+      throw std::invalid_argument("dwconv_wgrad_reduce_batch: list lengths differ");
+    std::vector<const float*> sp(n);
+    std::vector<float*> dp(n);
+    for (size_t i = 0; i < n; ++i) {
+      sp[i] = P<const float>(slabs[i]);
+      dp[i] = P<float>(dws[i]);
+    }
+    dwconv_wgrad_reduce_batch_launch(sp.data(), dp.data(), Cs.data(), nblks.data(), (int)n, S(st));
+    check_launch("dwconv_wgrad_reduce_batch");
+  });
   m.def("dwconv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int C,
                            int Pp, int Q, int stride, int pad, uintptr_t st, uintptr_t slab,
                            long long slab_floats) {

@@ -202,17 +202,17 @@ MA_DEV float dw_mask(float out, int act) {       // (bn.hip act_mask)
 // BW: the dgrad also reduces the BN-backward sums of the BN feeding this conv (what
 // bn_bwd_reduce would do in a separate pass over dx, out and y): dz = dx * act'(out),
 // sums += (dz, dz * xhat), block-reduced through padded LDS rows, one atomic pair per channel.
+// (body shared by the standalone launch and the dgrad + wgrad pair: block ``bid`` of ``nblk``)
 template <int S, bool BW>
-__global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const float* w, bf16* dx, int N,
-                                                      int H, int W, int C, int P, int Q, int pad,
-                                                      DwBw bw) {
-  extern __shared__ float part[];  // BW: [DT][ST_LD] per-thread (sum dz, sum dz * xhat)
+MA_DEV void dw_dgrad_body(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
+                          int P, int Q, int pad, const DwBw& bw, float* part, int bid, int nblk) {
+  // part (BW): [DT][ST_LD] per-thread (sum dz, sum dz * xhat)
   const int C8 = C >> 3, WS = (W + DWL - 1) / DWL;
   const int total = N * H * WS * C8;
-  const int gt = blockIdx.x * DT + threadIdx.x;
+  const int gt = bid * DT + threadIdx.x;
   // BW: a capped grid walks the strips (stride a multiple of C8: a thread keeps its channels),
   // so fewer blocks add their sums -- the per-channel atomics are what contends
-  const int T = gridDim.x * DT, stride = BW ? T - T % C8 : T;
+  const int T = nblk * DT, stride = BW ? T - T % C8 : T;
   const int lim = min(total, stride);
   float sdz[8], sx[8];
 #pragma unroll
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
       mine[8 + k] = sx[k];
     }
     __syncthreads();
-    const int g0 = blockIdx.x * DT;
+    const int g0 = bid * DT;
     const int nthr = min(DT, lim - g0), off = g0 % C8;
     for (int c = threadIdx.x; c < C; c += DT) {
       const int j0 = ((c >> 3) - off + C8) % C8;
@@ -325,12 +325,20 @@ __global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const floa
         v1 += part[j * ST_LD + 8 + (c & 7)];
       }
       if (v0 != 0.f || v1 != 0.f) {     // replica blockIdx % SUMS_R of [SUMS_R][3][C]
-        float* sums = bw.sums + (size_t)(blockIdx.x % SUMS_R) * 3 * C;
+        float* sums = bw.sums + (size_t)(bid % SUMS_R) * 3 * C;
         atomicAdd(sums + c, v0);
         atomicAdd(sums + C + c, v1);
       }
     }
   }
+}
+
+template <int S, bool BW>
+__global__ __launch_bounds__(DT) void dw_dgrad_kernel(const bf16* dy, const float* w, bf16* dx, int N,
+                                                      int H, int W, int C, int P, int Q, int pad,
+                                                      DwBw bw) {
+  extern __shared__ float part[];
+  dw_dgrad_body<S, BW>(dy, w, dx, N, H, W, C, P, Q, pad, bw, part, blockIdx.x, gridDim.x);
 }
 
 // One thread per (image, output row, 8 channels) walks the row's columns with the 3x3 input
@@ -344,14 +352,13 @@ constexpr int WG_LD = 73;   // floats per thread row (odd: conflict-free row wri
 // one memory round trip per column -- is QS x shorter and the grid QS x larger (the train-batch
 // layers otherwise launch 48-100 blocks whose threads each walk 32 dependent columns).
 template <int S>
-__global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
-                                                      int H, int W, int C, int P, int Q, int pad,
-                                                      int QS, float* slab) {
-  extern __shared__ float part[];  // [DT][WG_LD]
+MA_DEV void dw_wgrad_body(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
+                          int P, int Q, int pad, int QS, float* slab, float* part, int bid) {
+  // part: [DT][WG_LD]
   const int C8 = C >> 3;
   const int total = N * P * QS * C8;
   const int QL = (Q + QS - 1) / QS;
-  const int gt = blockIdx.x * DT + threadIdx.x;
+  const int gt = bid * DT + threadIdx.x;
   float acc[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -421,16 +428,66 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
     for (int k = 0; k < 8; ++k) mine[t * 8 + k] = acc[t][k];
   __syncthreads();
   // output (tap t, channel c): the threads of chunk c/8 are j0, j0 + C8, ... (gt = base + j)
-  const int nthr = min(DT, total - (int)blockIdx.x * DT);   // (c8 stays the fastest index)
-  const int off = (int)(((long long)blockIdx.x * DT) % C8);
+  const int nthr = min(DT, total - bid * DT);   // (c8 stays the fastest index)
+  const int off = (int)(((long long)bid * DT) % C8);
   for (int i = threadIdx.x; i < 9 * C; i += DT) {
     const int c = i % C, t = i / C;
     const int j0 = ((c >> 3) - off + C8) % C8;
     float v = 0.f;
     for (int j = j0; j < nthr; j += C8) v += part[j * WG_LD + t * 8 + (c & 7)];
     // slab: this block's partials, summed by dw_wgrad_reduce_kernel (no contended atomics)
-    if (slab) slab[(size_t)blockIdx.x * 9 * C + i] = v;
+    if (slab) slab[(size_t)bid * 9 * C + i] = v;
     else if (v != 0.f) atomicAdd(&dw[c * 9 + t], v);
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16* x, float* dw, int N,
+                                                      int H, int W, int C, int P, int Q, int pad,
+                                                      int QS, float* slab) {
+  extern __shared__ float part[];
+  dw_wgrad_body<S>(dy, x, dw, N, H, W, C, P, Q, pad, QS, slab, part, blockIdx.x);
+}
+
+// dgrad + wgrad of one depthwise conv in ONE launch (they read the same dy and are
+// independent): blocks [0, nwg) are wgrad column segments, the rest dgrad strips
+template <int S, bool BW>
+__global__ __launch_bounds__(DT) void dw_bwd_kernel(const bf16* dy, const bf16* x, const float* w,
+                                                    bf16* dx, float* dw, int N, int H, int W,
+                                                    int C, int P, int Q, int pad, int QS,
+                                                    float* slab, int nwg, DwBw bw) {
+  extern __shared__ float part[];
+  if ((int)blockIdx.x < nwg)
+    dw_wgrad_body<S>(dy, x, dw, N, H, W, C, P, Q, pad, QS, slab, part, blockIdx.x);
+  else
+    dw_dgrad_body<S, BW>(dy, w, dx, N, H, W, C, P, Q, pad, bw, part, blockIdx.x - nwg,
+                         gridDim.x - nwg);
+}
+
+// the partials reduce of several depthwise wgrads in one launch (blockIdx.z = layer): the
+// train step defers every layer's reduce to the end of the backward
+struct DwRedBatch {
+  const float* slab[DW_RED_MAX];
+  float* dw[DW_RED_MAX];
+  int C[DW_RED_MAX], nblk[DW_RED_MAX];
+};
+__global__ __launch_bounds__(DT) void dw_wgrad_reduce_batch_kernel(DwRedBatch b) {
+  const int l = blockIdx.z;
+  const int C = b.C[l], nblk = b.nblk[l];
+  if ((int)blockIdx.x * 64 >= 9 * C) return;          // whole block: this layer is narrower
+  __shared__ float red[4][64];
+  const int n9 = 9 * C;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int share = (nblk + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * share, b1 = min(nblk, b0 + share);
+  float v = 0.f;
+  if (i < n9)
+    for (int k = b0 + sub; k < b1; k += 4) v += b.slab[l][(size_t)k * n9 + i];
+  red[sub][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (sub == 0 && i < n9) {
+    const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    if (t != 0.f) atomicAdd(&b.dw[l][(i % C) * 9 + i / C], t);
   }
 }
 
@@ -501,11 +558,77 @@ void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H,
   }
 #undef DW_DG
 }
-size_t dwconv_wgrad_slab_floats(int N, int P, int Q, int C) {
+// wgrad column segments per row (QS) for the train-batch slab path
+static int dw_qs(int N, int P, int Q, int C) {
   const long long rows = (long long)N * P * (C / 8);
   int QS = 1;
   while (rows * QS < 256LL * 4 * 64 && (Q + 2 * QS - 1) / (2 * QS) >= 4) QS *= 2;
-  return (size_t)((rows * QS + DT - 1) / DT) * 9 * C;
+  return QS;
+}
+
+int dwconv_wgrad_blocks(int N, int P, int Q, int C) {
+  const long long total = (long long)N * P * (C / 8) * dw_qs(N, P, Q, C);
+  return (int)((total + DT - 1) / DT);
+}
+
+void dwconv_bwd_launch(const bf16* dy, const bf16* x, const float* w, bf16* dx, float* dw, int N,
+                       int H, int W, int C, int P, int Q, int stride, int pad, float* slab,
+                       const DwBw* bw, bool reduce, hipStream_t st) {
+  const int QS = dw_qs(N, P, Q, C);
+  const int nwg = dwconv_wgrad_blocks(N, P, Q, C);
+  const long long dtotal = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
+  long long ndg = (dtotal + DT - 1) / DT;
+  if (bw && ndg > 256) ndg = 256;
+  const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // >= the dgrad's [DT][ST_LD]
+  static const bool attr = [] {
+    const void* ks[] = {(const void*)dw_bwd_kernel<1, false>, (const void*)dw_bwd_kernel<1, true>,
+                        (const void*)dw_bwd_kernel<2, false>, (const void*)dw_bwd_kernel<2, true>};
+    for (const void* k : ks)
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  const DwBw none{};
+  const dim3 grid((unsigned)(nwg + ndg));
+#define DW_B(S_, BW_) hipLaunchKernelGGL((dw_bwd_kernel<S_, BW_>), grid, dim3(DT), shm, st, dy, x, w, dx, \
+                                         dw, N, H, W, C, P, Q, pad, QS, slab, nwg, bw ? *bw : none)
+  if (stride == 1) {
+    if (bw) DW_B(1, true);
+    else DW_B(1, false);
+  } else {
+    if (bw) DW_B(2, true);
+    else DW_B(2, false);
+  }
+#undef DW_B
+  if (reduce) {
+    const int shares = nwg >= 128 ? 8 : (nwg >= 32 ? 4 : 1);
+    hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((9 * C + 63) / 64, shares), dim3(DT), 0, st, slab,
+                       dw, C, nwg);
+  }
+}
+
+void dwconv_wgrad_reduce_batch_launch(const float* const* slabs, float* const* dws, const int* Cs,
+                                      const int* nblks, int n, hipStream_t st) {
+  for (int l0 = 0; l0 < n; l0 += DW_RED_MAX) {
+    DwRedBatch b{};
+    int cmax = 0, bmax = 0;
+    const int m = n - l0 < DW_RED_MAX ? n - l0 : DW_RED_MAX;
+    for (int j = 0; j < m; ++j) {
+      b.slab[j] = slabs[l0 + j];
+      b.dw[j] = dws[l0 + j];
+      b.C[j] = Cs[l0 + j];
+      b.nblk[j] = nblks[l0 + j];
+      cmax = b.C[j] > cmax ? b.C[j] : cmax;
+      bmax = b.nblk[j] > bmax ? b.nblk[j] : bmax;
+    }
+    const int shares = bmax >= 128 ? 8 : (bmax >= 32 ? 4 : 1);
+    hipLaunchKernelGGL(dw_wgrad_reduce_batch_kernel, dim3((9 * cmax + 63) / 64, shares, m),
+                       dim3(DT), 0, st, b);
+  }
+}
+
+size_t dwconv_wgrad_slab_floats(int N, int P, int Q, int C) {
+  return (size_t)dwconv_wgrad_blocks(N, P, Q, C) * 9 * C;
 }
 
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int P,

@@ -284,6 +284,16 @@ void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H,
                          const DwBw* bw = nullptr);
 // slab (optional, >= dwconv_wgrad_slab_floats): per-block partials + a reduce kernel
 size_t dwconv_wgrad_slab_floats(int N, int P, int Q, int C);
+// dgrad (+ fused BN-backward sums bw) and slab wgrad of a depthwise conv in one launch; the
+// partials reduce follows unless ``reduce`` is false (then dwconv_wgrad_reduce_batch_launch
+// sums this layer's slab later, e.g. once for every layer at the end of the backward)
+constexpr int DW_RED_MAX = 24;
+int dwconv_wgrad_blocks(int N, int P, int Q, int C);
+void dwconv_bwd_launch(const bf16* dy, const bf16* x, const float* w, bf16* dx, float* dw, int N,
+                       int H, int W, int C, int P, int Q, int stride, int pad, float* slab,
+                       const DwBw* bw, bool reduce, hipStream_t st);
+void dwconv_wgrad_reduce_batch_launch(const float* const* slabs, float* const* dws, const int* Cs,
+                                      const int* nblks, int n, hipStream_t st);
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
                          int P, int Q, int stride, int pad, hipStream_t st, float* slab = nullptr,
                          size_t slab_floats = 0);

@@ -60,6 +60,8 @@ class _Mode(object):
         self.slab = None
         self.G = 1 if not group_imgs else N // group_imgs
         self.prereduced = {}             # block index -> BN sums already reduced by a dgrad
+        self.dw_region = {}              # depthwise unit -> (slab offset, floats, wgrad blocks)
+        self.dw_pending = []             # deferred depthwise wgrad reduces of this backward
 
 
 class NativeEngine(object):
@@ -181,6 +183,8 @@ class NativeEngine(object):
         self.use_stem = os.environ.get('MERCURY_STEM', '1') == '1'
         # depthwise convs take their input's BN + activation in their chunk loads
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
+        # depthwise dgrad + wgrad in one launch, wgrad reduces batched at the end of the backward
+        self.dw_pair = os.environ.get('MERCURY_DW_PAIR', '1') == '1'
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
@@ -342,9 +346,12 @@ class NativeEngine(object):
                     sp.group_rows = group_imgs * sp.P * sp.Q
                 m.spec[u.name] = sp
                 if u.depthwise and train:
-                    # per-block weight-gradient partials (summed by a second kernel); its own
-                    # buffer: the split-K slab's head holds tile counters that must stay zero
-                    dw_slab = max(dw_slab, ops.dwconv_wgrad_slab_floats(N, sp.P, sp.Q, sp.C))
+                    # per-block weight-gradient partials (summed by a reduce kernel), a region
+                    # per layer so the reduces can be deferred and batched at the end of the
+                    # backward; its own buffer (the split-K slab's head holds tile counters)
+                    m.dw_region[u.name] = (dw_slab, ops.dwconv_wgrad_slab_floats(
+                        N, sp.P, sp.Q, sp.C), ops.dwconv_wgrad_blocks(N, sp.P, sp.Q, sp.C))
+                    dw_slab += m.dw_region[u.name][1]
                 if not u.depthwise:
                     # measured-best plans from the tuning cache (ops/tune.py) when present
                     # the scoring pass runs beside the latency-bound train chain: fewer, larger
@@ -732,12 +739,22 @@ class NativeEngine(object):
                      losses=m.losses, isw=isw, meters=meters,
                      score=self.score if mode == 'score' else 'loss')
 
+    def flush_dw_reduces(self, m):
+        """The deferred depthwise wgrad reduces of this backward, in one launch."""
+        ops.dwconv_wgrad_reduce_batch(m.dw_pending)
+        m.dw_pending = []
+
     def _wgrad(self, m, u, dy, x):
         sp = m.spec[u.name]
         gw = self._pview(u.w_seg, grad=True)
         if u.depthwise:
-            ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad,
-                             slab=m.dw_slab)
+            if m.dw_slab is not None:
+                off, n, _ = m.dw_region[u.name]
+                ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride,
+                                 sp.pad, slab=m.dw_slab[off:off + n])
+            else:
+                ops.dwconv_wgrad(dy, x, gw, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride,
+                                 sp.pad)
         else:
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 
@@ -754,13 +771,29 @@ class NativeEngine(object):
                          dplan=m.plan[u.name, 'dgrad'], wplan=m.plan[u.name, 'wgrad'],
                          slab=m.slab, accumulate=accumulate, bw=bw)
             return bw is not None
+        if u.depthwise and dx is not None and m.dw_slab is not None and self.dw_pair:
+            assert not accumulate
+            # the producer's BN-backward sums reduced in the depthwise dgrad (no bn_bwd reduce
+            # pass; one batch group in train mode, no shortcut BN)
+            if bw is not None and (not self.fuse_bn_bwd or bw.get('y2') is not None):
+                bw = None
+            # dgrad + wgrad in one launch; without DP the wgrad partials' reduce is deferred
+            # to one batched launch at the end of the backward (flush_dw_reduces) -- nothing
+            # reads a depthwise weight gradient before the optimizer
+            off, n, nblk = m.dw_region[u.name]
+            region = m.dw_slab[off:off + n]
+            gw = self._pview(u.w_seg, grad=True)
+            defer = not self.dp
+            ops.dwconv_bwd(dy, x, self._pview(u.w_seg), dx, gw, sp.N, sp.H, sp.W, sp.C, sp.P,
+                           sp.Q, sp.stride, sp.pad, region, bw=bw, reduce=not defer)
+            if defer:
+                m.dw_pending.append((region, gw, sp.C, nblk))
+            return bw is not None
         self._wgrad(m, u, dy, x)
         if u.depthwise:
             if dx is None:
                 return False
             assert not accumulate
-            # the producer's BN-backward sums reduced in the depthwise dgrad (no bn_bwd reduce
-            # pass; one batch group in train mode, no shortcut BN)
             if bw is not None and (not self.fuse_bn_bwd or bw.get('y2') is not None):
                 bw = None
             ops.dwconv_dgrad(dy, self._pview(u.w_seg), dx, sp.N, sp.H, sp.W, sp.C, sp.P,
@@ -798,6 +831,8 @@ class NativeEngine(object):
     def backward_block(self, m, bi):
         for _, f in self.backward_parts(m, bi):
             f()
+        if bi == 0:                      # the backward is complete: deferred reduces
+            self.flush_dw_reduces(m)
 
     def backward_parts(self, m, bi):
         """Block ``bi``'s backward as [(unit index, callable)] in execution order (last unit
@@ -1017,6 +1052,7 @@ class NativeEngine(object):
         segs = []
 
         def fwd_head():
+            tm.dw_pending = []
             ops.lib().step_begin(ops.ptr(self.ctrl), ops.stream_ptr(), ops.ptr(tm.stats_arena),
                                  tm.stats_arena.numel(), ops.ptr(tm.sums_arena),
                                  tm.sums_arena.numel())
@@ -1039,6 +1075,8 @@ class NativeEngine(object):
                     cur = []
         if cur:
             segs.append((cur, None))
+        if any(u.depthwise for u in self.units) and not self.dp:
+            segs[-1][0].append(lambda: self.flush_dw_reduces(tm))
         if self.check_order:
             # every train segment ticks o[2]; the comm stream checks it before reducing
             for fs, _ in segs:

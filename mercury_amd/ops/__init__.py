@@ -82,7 +82,8 @@ from .head import head_fwd, head_bwd, mlp_head_fwd, mlp_head_bwd  # noqa: E402
 from .importance import pool_build, is_sample, gather  # noqa: E402
 from .table import ImportanceTable  # noqa: E402
 from .optim import FlatOptimizer, optimizer_spec  # noqa: E402
-from .misc import (quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad, dwconv_wgrad_slab_floats,  # noqa: E402
+from .misc import (quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad, dwconv_wgrad, dwconv_wgrad_slab_floats,
+                   dwconv_bwd, dwconv_wgrad_reduce_batch, dwconv_wgrad_blocks,  # noqa: E402
                    nchw_to_nhwc8, tern_pack, tern_unpack)
 
 __all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'pgemm_fwd', 'pwconv_fwd', 'stem_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
@@ -90,4 +91,5 @@ __all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'pgemm_fwd', 'pwconv_fwd'
            'head_fwd', 'head_bwd', 'mlp_head_fwd', 'mlp_head_bwd', 'pool_build', 'is_sample', 'gather', 'ImportanceTable',
            'FlatOptimizer', 'optimizer_spec', 'quantize', 'tern_pack', 'tern_unpack', 'pool2d_fwd', 'maxpool2d_bwd',
            'dwconv_fwd', 'dwconv_dgrad', 'dwconv_wgrad', 'dwconv_wgrad_slab_floats',
+           'dwconv_bwd', 'dwconv_wgrad_reduce_batch', 'dwconv_wgrad_blocks',
            'nchw_to_nhwc8']

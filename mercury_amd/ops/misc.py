@@ -100,6 +100,42 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
     lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr(), *ba)
 
 
+def dwconv_bwd(dy, x, w, dx, dw, N, H, W, C, P, Q, stride, pad, slab, bw=None, reduce=True):
+    """Depthwise dgrad (+ fused BN-backward sums ``bw``, as dwconv_dgrad) and slab wgrad in
+    ONE launch.  ``slab`` (fp32, >= dwconv_wgrad_slab_floats): the wgrad blocks' partials;
+    ``reduce=False`` leaves them for dwconv_wgrad_reduce_batch (dw is then not yet updated)."""
+    _chk(slab, torch.float32, 'slab', dwconv_wgrad_slab_floats(N, P, Q, C))
+    ba = (0, 0, 0, 0, 0.0, 0.0, 0)
+    if bw is not None:
+        n_in = N * H * W * C
+        for k in ('out', 'y'):
+            _chk(bw[k], torch.bfloat16, 'bw.' + k, n_in)
+        _chk(bw['stats'], torch.float32, 'bw.stats', 2 * C)
+        _chk(bw['sums'], torch.float32, 'bw.sums', int(getattr(lib(), 'SUMS_R', 1)) * 3 * C)
+        if bw.get('y2') is not None:
+            raise ValueError('dwconv_bwd: no shortcut-BN reduce')
+        ba = (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw['sums']),
+              1.0 / (N * H * W), float(bw.get('eps', 1e-5)), _ACT[bw.get('act')])
+    lib().dwconv_bwd(ptr(dy), ptr(x), ptr(w), ptr(dx), ptr(dw), N, H, W, C, P, Q, stride, pad,
+                     ptr(slab), int(reduce), stream_ptr(), *ba)
+
+
+def dwconv_wgrad_reduce_batch(items):
+    """dw += the slab partials of several dwconv_bwd(reduce=False) launches in one kernel;
+    ``items``: [(slab, dw, C, nblk)] with nblk = dwconv_wgrad_blocks(N, P, Q, C)."""
+    if not items:
+        return
+    lib().dwconv_wgrad_reduce_batch([ptr(s) for s, _, _, _ in items],
+                                    [ptr(d) for _, d, _, _ in items],
+                                    [int(c) for _, _, c, _ in items],
+                                    [int(n) for _, _, _, n in items], stream_ptr())
+
+
+def dwconv_wgrad_blocks(N, P, Q, C):
+    """wgrad blocks (= slab partial rows) of the train-batch depthwise wgrad."""
+    return int(lib().dwconv_wgrad_blocks(N, P, Q, C))
+
+
 def dwconv_wgrad_slab_floats(N, P, Q, C):
     """fp32 workspace for ``dwconv_wgrad(slab=...)`` (per-block partials)."""
     return int(lib().dwconv_wgrad_slab_floats(N, P, Q, C))

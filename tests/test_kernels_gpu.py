@@ -1032,3 +1032,51 @@ def test_dwconv_dgrad_fused_bn_backward_reduce(case):
     scratch = torch.empty_like(y)
     ops.bn_bwd(dx, out, y, stats.reshape(-1), gamma, ref, scratch, M, C, act=act, eps=1e-5)
     close(ops.sums_total(sums, C)[:2], ops.sums_total(ref, C)[:2], 2e-3, 1e-2)
+
+
+@pytest.mark.parametrize('stride', [1, 2])
+@pytest.mark.parametrize('fused', [False, True])
+def test_dwconv_bwd_pair_matches_separate(stride, fused):
+    """dwconv_bwd (dgrad + slab wgrad in one launch, reduce immediate or deferred to the
+    batched reduce) == dwconv_dgrad + dwconv_wgrad, and the wgrad == torch."""
+    ops = _ops()
+    N, H, C = 8, 16, 96
+    P = (H + 2 - 3) // stride + 1
+    x = bf(torch.randn(N, C, H, H, device=DEV))
+    w = (torch.randn(C, 1, 3, 3, device=DEV) * 0.2)
+    gy = bf(torch.randn(N, C, P, P, device=DEV))
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=stride, padding=1, groups=C).backward(gy)
+    xn, gyn = ops.to_nhwc(x), ops.to_nhwc(gy)
+    wf = w.view(C, 9).contiguous()
+    Mx = N * H * H
+    bw = bw2 = None
+    if fused:
+        y = bf(torch.randn(Mx, C, device=DEV)).to(torch.bfloat16)
+        out = bf(torch.relu(torch.randn(Mx, C, device=DEV))).to(torch.bfloat16)
+        stats = torch.stack([y.float().sum(0), y.float().pow(2).sum(0)]).contiguous()
+        bw = dict(out=out, y=y, stats=stats, sums=torch.zeros(ops.sums_numel(C), device=DEV),
+                  act='relu')
+        bw2 = dict(bw, sums=torch.zeros(ops.sums_numel(C), device=DEV))
+    dx1 = torch.empty(Mx, C, dtype=torch.bfloat16, device=DEV)
+    dw1 = torch.zeros(C * 9, device=DEV)
+    slab = torch.zeros(ops.dwconv_wgrad_slab_floats(N, P, P, C), device=DEV)
+    ops.dwconv_dgrad(gyn, wf, dx1, N, H, H, C, P, P, stride, 1, bw=bw)
+    ops.dwconv_wgrad(gyn, xn, dw1, N, H, H, C, P, P, stride, 1, slab=slab)
+    for defer in (False, True):
+        dx2 = torch.empty_like(dx1)
+        dw2 = torch.zeros_like(dw1)
+        if bw2 is not None:
+            bw2['sums'].zero_()
+        ops.dwconv_bwd(gyn, xn, wf, dx2, dw2, N, H, H, C, P, P, stride, 1, slab, bw=bw2,
+                       reduce=not defer)
+        if defer:
+            nblk = ops.dwconv_wgrad_blocks(N, P, P, C)
+            ops.dwconv_wgrad_reduce_batch([(slab, dw2, C, nblk)])
+        assert torch.equal(dx1, dx2)
+        close(dw2, dw1, 1e-4, 1e-4)
+        if fused:
+            close(ops.sums_total(bw2['sums'], C), ops.sums_total(bw['sums'], C), 1e-4, 1e-3)
+    close(dw1.view(C, 3, 3), wr.grad.view(C, 3, 3), 2e-2, 2e-2)
+    close(ops.from_nhwc(dx1.view(N, H, H, C), C), xr.grad, 2e-2, 2e-2)
