@@ -147,6 +147,8 @@ def main():
                     help='DP all-reduce: own RCCL communicator on a comm stream, the direct-xGMI '
                          'two-shot over IPC-mapped peer buffers, or the torch ProcessGroup')
     ap.add_argument('--wire-bf16', action='store_true', help='bf16 gradients on the wire')
+    ap.add_argument('--bucket-mb', type=float, default=0,
+                    help='gradient bucket size in MiB (0: the engine default for the world size)')
     ap.add_argument('--compress', default='none', choices=('none', 'ternary'),
                     help='ternary-compressed gradient all-reduce (parallel/compress.py)')
     ap.add_argument('--sampler', default='alias', choices=('alias', 'cdf', 'groupwise'),
@@ -195,6 +197,7 @@ def main():
                            use_graphs=not args.no_graphs, image_hw=hw,
                            force_buckets=args.force_buckets, comm=args.comm,
                            wire_bf16=args.wire_bf16, sampler=args.sampler,
+                           bucket_bytes=int(args.bucket_mb * (1 << 20)) or None,
                            grad_compress=args.compress)
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
@@ -202,6 +205,15 @@ def main():
         return eng
 
     def run(eng, steps, warmup, scoring=True):
+        # (A/B: MERCURY_TRAIN_PRIO=1 issues the train stream's work -- the latency-bound
+        # critical path -- on a high-priority stream; the scoring stream keeps the default)
+        if os.environ.get('MERCURY_TRAIN_PRIO', '0') == '1':
+            lo, hi = torch.cuda.Stream.priority_range()
+            with torch.cuda.stream(torch.cuda.Stream(device, priority=hi)):
+                return run_on(eng, steps, warmup, scoring)
+        return run_on(eng, steps, warmup, scoring)
+
+    def run_on(eng, steps, warmup, scoring=True):
         eng.scoring = scoring
         eng.prime()
         eng.step()
