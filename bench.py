@@ -205,15 +205,6 @@ def main():
         return eng
 
     def run(eng, steps, warmup, scoring=True):
-        # (A/B: MERCURY_TRAIN_PRIO=1 issues the train stream's work -- the latency-bound
-        # critical path -- on a high-priority stream; the scoring stream keeps the default)
-        if os.environ.get('MERCURY_TRAIN_PRIO', '0') == '1':
-            lo, hi = torch.cuda.Stream.priority_range()
-            with torch.cuda.stream(torch.cuda.Stream(device, priority=hi)):
-                return run_on(eng, steps, warmup, scoring)
-        return run_on(eng, steps, warmup, scoring)
-
-    def run_on(eng, steps, warmup, scoring=True):
         eng.scoring = scoring
         eng.prime()
         eng.step()

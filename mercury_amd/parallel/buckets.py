@@ -26,7 +26,14 @@ import torch.distributed as dist
 
 
 def default_bucket_bytes(world_size):
-    return (4 << 20) if world_size <= 4 else (8 << 20)
+    """16 MiB buckets at every world size: each bucket costs the native step one more
+    host-replayed graph segment and one RCCL launch (~15 us at W=1, more per-message latency over
+    xGMI rings at W=8), and the scoring stream runs beside the whole backward, so a few large
+    buckets still overlap.  Measured forced-bucket ResNet-18 step at W=1 (profiles/r3/
+    bucket_size_sweep_w1.json): 4 MiB 1.514, 8 MiB 1.485, 16 MiB 1.469, 32 MiB 1.458 ms (no DP
+    1.358).  (32 MiB would leave ResNet-18 two buckets -- the first 34 MB -- too little overlap
+    at W=8.)"""
+    return 16 << 20
 
 
 class BucketedAllReduce(object):
