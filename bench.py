@@ -58,6 +58,23 @@ SAMPLER_DESC = {
 }
 
 
+def preset_data(pre):
+    """(image hw, x, y) of a preset: synthetic uint8 images, or float 'spectrograms' (a
+    class-dependent low-frequency pattern + noise) for the speech preset."""
+    import numpy as np
+    from mercury_amd.data.datasets import synthetic_arrays
+    ncls, hw, n = pre['classes'], pre['hw'], pre['n']
+    hw = hw if isinstance(hw, tuple) else (hw, hw)
+    if pre.get('chans', 3) == 3:
+        x_all, y_all = synthetic_arrays(n, ncls, shape=(hw[0], hw[1], 3), seed=8)
+    else:
+        rng = np.random.RandomState(8)
+        y_all = rng.randint(0, ncls, n).astype(np.int64)
+        proto = rng.randn(ncls, pre['chans'], hw[0], hw[1]).astype(np.float32)
+        x_all = (proto[y_all] + rng.randn(n, pre['chans'], hw[0], hw[1]).astype(np.float32) * 2)
+    return hw, x_all, y_all
+
+
 def diagnostics(eng, steps, ws):
     """Untimed steps AFTER the timed loop: device-phase times (HIP events on each stream),
     the DP communicator's view (ranks, bucket bytes, all-reduce device time, the part of it
@@ -176,15 +193,8 @@ def main():
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import build_model
 
-    ncls, hw, n = pre['classes'], pre['hw'], pre['n']
-    hw = hw if isinstance(hw, tuple) else (hw, hw)
-    if pre.get('chans', 3) == 3:
-        x_all, y_all = synthetic_arrays(n, ncls, shape=(hw[0], hw[1], 3), seed=8)
-    else:   # float "spectrograms": class-dependent low-frequency pattern + noise
-        rng = np.random.RandomState(8)
-        y_all = rng.randint(0, ncls, n).astype(np.int64)
-        proto = rng.randn(ncls, pre['chans'], hw[0], hw[1]).astype(np.float32)
-        x_all = (proto[y_all] + rng.randn(n, pre['chans'], hw[0], hw[1]).astype(np.float32) * 2)
+    ncls, n = pre['classes'], pre['n']
+    hw, x_all, y_all = preset_data(pre)
     np.random.seed(102)
     shards = dirichlet_partition(y_all, ws, 0.5, ncls) if ws > 1 else {0: np.arange(n)}
     idx = np.asarray(shards[rank])

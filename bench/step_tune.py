@@ -20,18 +20,20 @@ def main():
     ap.add_argument('--steps', type=int, default=40)
     ap.add_argument('--chunks', type=int, default=3)
     ap.add_argument('--threshold', type=float, default=0.004)
+    ap.add_argument('--config', default='resnet18-cifar10')
     args = ap.parse_args()
     os.environ['MERCURY_TUNE_CACHE'] = os.path.abspath(args.out) + '.none'   # start untuned
     import torch
-    from mercury_amd.data.datasets import synthetic_arrays
+    from bench import PRESETS, preset_data
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import build_model
     from mercury_amd.ops import step_tune
-    x, y = synthetic_arrays(50000, 10, seed=8)
+    pre = PRESETS[args.config]
+    hw, x, y = preset_data(pre)
     torch.manual_seed(1234)
-    net = build_model('resnet18', 10).cuda()
-    eng = NativeEngine(net, 'cuda', 32, 10, optimizer='adam', lr=0.001, seed=7,
-                       importance=True, world_size=1, use_graphs=True)
+    net = build_model(pre['model'], pre['classes']).cuda()
+    eng = NativeEngine(net, 'cuda', pre['batch'], 10, optimizer='adam', lr=0.001, seed=7,
+                       importance=True, world_size=1, use_graphs=True, image_hw=hw)
     eng.set_shard(x, y)
     eng.prime()
     eng.step()
