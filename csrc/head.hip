@@ -294,6 +294,38 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
   }
 }
 
+// Narrow heads with many classes (MobileNetV2 CIFAR-100: 100 x 1280): the per-sample kernel's
+// classes are a serial chain per wave (25 dot products of 1280 each); here block (b, j) pools
+// sample b (redundantly per class chunk -- a few KB) and computes HC_CHUNK classes, so the
+// chunks run as separate blocks; the loss / softmax kernel then runs on the ready logits.
+constexpr int HC_CHUNK = 16;
+__global__ __launch_bounds__(NT) void head_fc_chunk_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* pooled = sh;               // [C]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int k0 = blockIdx.y * HC_CHUNK;
+  const bf16* x = a.act + (size_t)b * a.HW * a.C;
+  const float invhw = 1.f / (float)a.HW;
+  for (int c = tid; c < a.C; c += NT) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
+    s *= invhw;
+    pooled[c] = s;
+    if (a.pooled && blockIdx.y == 0) a.pooled[(size_t)b * a.C + c] = s;
+  }
+  __syncthreads();
+  const int k1 = min(a.classes, k0 + HC_CHUNK);
+  for (int k = k0 + wv; k < k1; k += NT / 64) {
+    const float* wr = a.w + (size_t)k * a.C;
+    float d = 0.f;
+#pragma unroll 8
+    for (int c = lane; c < a.C; c += 64) d += wr[c] * pooled[c];
+    d = wave_sum(d);
+    if (lane == 0) a.logits[(size_t)b * a.classes + k] = d + (a.b ? a.b[k] : 0.f);
+  }
+}
+
 // grid = (channel blocks, B + classes): block row y < B writes sample y's activation
 // gradient (d pooled / HW broadcast over the spatial positions); row B + k reduces
 // dW[k][:] (and db[k]) over the batch.  Every thread's loop is short and unrolled so
@@ -349,6 +381,10 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
     hipLaunchKernelGGL((head_gemm_kernel<true, true, 0>),
                        dim3((a.B + LT - 1) / LT, (a.classes + LT - 1) / LT, z), dim3(NT), 0, st,
                        a.pooled, a.C, a.w, a.C, a.b, (void*)a.logits, a.B, a.classes, a.C, 1, 1.f);
+    a.logits_ready = 1;
+  } else if (path != 1 && a.logits && a.classes >= 4 * HC_CHUNK) {
+    hipLaunchKernelGGL(head_fc_chunk_kernel, dim3(a.B, (a.classes + HC_CHUNK - 1) / HC_CHUNK),
+                       dim3(NT), (size_t)a.C * sizeof(float), st, a);
     a.logits_ready = 1;
   }
   const size_t shm = (size_t)(a.C + a.classes + 16) * sizeof(float);
