@@ -21,6 +21,7 @@ def main():
     ap.add_argument('--chunks', type=int, default=3)
     ap.add_argument('--threshold', type=float, default=0.004)
     ap.add_argument('--config', default='resnet18-cifar10')
+    ap.add_argument('--kinds', default='fwd,bwd', help="coordinates to tune: 'fwd', 'bwd'")
     args = ap.parse_args()
     os.environ['MERCURY_TUNE_CACHE'] = os.path.abspath(args.out) + '.none'   # start untuned
     import torch
@@ -42,6 +43,7 @@ def main():
         eng.step()
     res, base, final = step_tune.tune_step(eng, steps=args.steps, chunks=args.chunks,
                                            threshold=args.threshold, budget_s=args.budget,
+                                           kinds=tuple(args.kinds.split(',')),
                                            log=lambda s: print(s, flush=True))
     with open(args.out, 'w') as f:
         json.dump(dict(sorted(res.items())), f, indent=0, sort_keys=True)

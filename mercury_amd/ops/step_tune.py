@@ -98,7 +98,7 @@ def _candidates(kind, sp, cur, max_split):
 
 
 def tune_step(eng, steps=40, chunks=3, threshold=0.004, max_split=4, budget_s=600.0,
-              log=print):
+              log=print, kinds=('fwd', 'bwd')):
     """Coordinate descent over the engine's conv plans, judged by step time.  Returns
     ({cache key: plan}, baseline ms, final ms).  ``eng`` must be primed and stepping."""
     t_start = time.perf_counter()
@@ -110,7 +110,7 @@ def tune_step(eng, steps=40, chunks=3, threshold=0.004, max_split=4, budget_s=60
 
     base = measure()
     best_t = base
-    coords = coordinates(eng)
+    coords = [c for c in coordinates(eng) if c[0] in kinds]
     # biggest work first: the scoring batch, then forward before backward
     coords.sort(key=lambda c: (-c[2][0][2].N, c[0] != 'fwd'))
     result = {}
