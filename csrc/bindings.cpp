@@ -142,13 +142,13 @@ PYBIND11_MODULE(_C, m) {
                         int Ncols, int M, int bm, int bn, int splits, uintptr_t st,
                         uintptr_t p_stats, uintptr_t p_rmean, uintptr_t p_rvar, uintptr_t p_gamma,
                         uintptr_t p_beta, uintptr_t p_keep, int p_group_rows, float p_inv_count,
-                        float p_eps, int p_act, int p_keep_tap) {
+                        float p_eps, int p_act, int p_keep_tap, uintptr_t p_res) {
     ConvGeom g{SH, SW, SC, RP, RQ, R, Sk, stride, pad, Kc, Ncols, M};
     EpiParams e{P<bf16>(out), ldo, P<const float>(bias), P<float>(stats), stats_ld, group_rows, 0,
                 P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
     ProParams pr{P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
                  P<const float>(p_gamma), P<const float>(p_beta), P<bf16>(p_keep), p_group_rows,
-                 p_inv_count, p_eps, p_act, p_keep_tap};
+                 p_inv_count, p_eps, p_act, p_keep_tap, P<const bf16>(p_res)};
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, false, S(st), &pr);
     check_launch("igemm_pro");
   });

@@ -77,6 +77,8 @@ struct ProParams {
   float eps;
   int act;              // 0 none, 1 relu, 2 relu6
   int keep_tap;         // r*S + s of the tap whose pixel is the output pixel itself
+  const bf16* res = nullptr;   // identity residual added before the activation, or null
+                               // (a = act(bn(y) + res): a block-final BN feeding the next block)
 };
 
 size_t igemm_slab_bytes(const ConvGeom& g, int bm, int bn, int splits);

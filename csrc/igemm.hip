@@ -250,6 +250,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
   float4 pst[8];
   int pz = 0;
   int pko[AR];
+  u32x4 prs[AR];       // residual chunks (pro.res)
   const float* pbase = nullptr;
   if constexpr (PRO) {
     const int grp = m0 / pro.group_rows;
@@ -289,6 +290,7 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
       if constexpr (PRO) {
         pz |= (ok ? 0 : 1) << i;
         pko[i] = keep && ok ? o : -1;
+        if (pro.res != nullptr) prs[i] = *(const u32x4*)(ok ? pro.res + o : zp);
       }
     }
 #pragma unroll
@@ -318,14 +320,16 @@ MA_DEV void igemm_nt_body(const bf16* __restrict__ src, const bf16* __restrict__
         sc[k] = gv[k] * rsqrtf(var + pro.eps);
         sh[k] = bv[k] - mean * sc[k];
       }
+      const bool hres = pro.res != nullptr;   // kernel-uniform
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bf16x8 y = __builtin_bit_cast(bf16x8, ra[i]);
+        const bf16x8 rv = __builtin_bit_cast(bf16x8, hres ? prs[i] : u32x4{0u, 0u, 0u, 0u});
         bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           // branch-free activation: clamp to the act's bounds (identity for none)
-          o[k] = f2bf(fminf(fmaxf(bf2f(y[k]) * sc[k] + sh[k], plo), phi));
+          o[k] = f2bf(fminf(fmaxf(bf2f(y[k]) * sc[k] + sh[k] + bf2f(rv[k]), plo), phi));
         }
         const u32x4 t = __builtin_bit_cast(u32x4, o);
         ra[i] = ((pz >> i) & 1) ? u32x4{0u, 0u, 0u, 0u} : t;

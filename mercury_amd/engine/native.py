@@ -183,6 +183,8 @@ class NativeEngine(object):
         self.use_stem = os.environ.get('MERCURY_STEM', '1') == '1'
         # depthwise convs take their input's BN + activation in their chunk loads
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
+        # block-final BN + identity residual inside the next block's igemm pointwise conv load
+        self.res_pro = self.fuse_bn_fwd and os.environ.get('MERCURY_RES_PRO', '1') == '1'
         # depthwise dgrad + wgrad in one launch, wgrad reduces batched at the end of the backward
         self.dw_pair = os.environ.get('MERCURY_DW_PAIR', '1') == '1'
 
@@ -552,6 +554,29 @@ class NativeEngine(object):
             d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
         return d
 
+    def _res_pro(self, m, u, act, out, nxt, res):
+        """Block-final BN + identity residual + activation folded into the register-staged
+        load of the next block's first (pointwise) conv on igemm: a = act(bn_u(y) + res), the
+        block output ``out`` written once through the prologue's keep (MobileNetV2's linear
+        bottleneck outputs feeding the next expand conv), instead of a bn_apply pass."""
+        if not self.res_pro or act not in ('relu', 'relu6', 'none') or nxt.depthwise:
+            return None
+        # (a pwconv / pgemm plan only runs with its own prologue kinds or plain; with this
+        # prologue the conv runs on igemm)
+        if any((nxt.name, k) in m.plan for k in ('stem', 'hconv')):
+            return None
+        sp = m.spec[nxt.name]
+        if sp.R != 1 or not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=True):
+            return None
+        su = m.spec[u.name]
+        d = dict(gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS, keep=out,
+                 res=res)
+        if m.train or m.group_imgs:
+            d.update(stats=m.stats[u.name], count=su.group_rows or su.M)
+        else:
+            d.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+        return d
+
     def _pool_bn(self, m, u, act):
         d = dict(gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS)
         if m.group_imgs:
@@ -669,6 +694,8 @@ class NativeEngine(object):
                     pgd = None
                     if nb is not None and not blk.pool and nb.units and ru is None:
                         pgd = self._pg_pro(m, u, blk.final_act, out, nb.units[0], res=res)
+                        if pgd is None and res is not None:
+                            pgd = self._res_pro(m, u, blk.final_act, out, nb.units[0], res)
                     if pgd is not None:
                         # the next block's first (pointwise) conv applies this BN (+ identity
                         # residual) + activation in its operand tiles and writes ``out``

@@ -225,12 +225,14 @@ def _pro_args(pro, spec):
     for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta'):
         _chk(pro.get(k), torch.float32, 'pro.' + k)
     _chk(pro.get('keep'), torch.bfloat16, 'pro.keep', spec.N * spec.H * spec.W * spec.Cp)
+    _chk(pro.get('res'), torch.bfloat16, 'pro.res', spec.N * spec.H * spec.W * spec.Cp)
     if pro.get('stats') is None and pro.get('rmean') is None:
         raise ValueError('pro needs stats or running statistics')
     grp = spec.group_rows if spec.group_rows else spec.M
     return (ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')), ptr(pro['gamma']),
             ptr(pro['beta']), ptr(pro.get('keep')), grp, 1.0 / float(pro.get('count', 1)),
-            float(pro.get('eps', 1e-5)), _ACT[pro.get('act')], (spec.R // 2) * spec.S + spec.S // 2)
+            float(pro.get('eps', 1e-5)), _ACT[pro.get('act')], (spec.R // 2) * spec.S + spec.S // 2,
+            ptr(pro.get('res')))
 
 
 def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=None,

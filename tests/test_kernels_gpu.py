@@ -805,6 +805,40 @@ def test_conv_fwd_bn_apply_prologue(case, mode):
         close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize('act', ['none', 'relu'])
+def test_conv_fwd_bn_residual_prologue(act):
+    """The block-final form of the prologue: conv(act(bn(y) + res)) with the residual added in
+    the operand load and the block output kept == bn_apply(res mode) then the plain conv."""
+    ops = _ops()
+    from mercury_amd.ops.conv import ConvSpec, fwd_plan, pro_ok, slab_bytes
+    N, H, C, K = 8, 16, 32, 96
+    g = torch.Generator(device='cpu').manual_seed(11)
+    yb = bf(torch.randn(N, C, H, H, generator=g) * 2 + 0.5).to(DEV)
+    rb = bf(torch.randn(N, C, H, H, generator=g)).to(DEV)
+    w = bf(torch.randn(K, C, 1, 1, generator=g) / math.sqrt(C)).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    yn, rn = ops.to_nhwc(yb), ops.to_nhwc(rb)
+    spec = ConvSpec(N, H, H, C, K, 1, 1, 1, 0)
+    stats = torch.stack([yb.sum((0, 2, 3)), yb.pow(2).sum((0, 2, 3))]).contiguous()
+    plan = fwd_plan(spec)
+    assert pro_ok(spec, plan, keep=True)
+    wk, _ = ops.pack_conv_weight(w)
+    slab = torch.zeros(max(1, slab_bytes(spec.M, K, *plan[:3]) // 4), device=DEV)
+    out = torch.empty(spec.M, K, dtype=torch.bfloat16, device=DEV)
+    keep = torch.full_like(yn, float('nan'))
+    pro = dict(gamma=gamma, beta=beta, act=act, eps=1e-5, keep=keep, res=rn,
+               stats=stats.reshape(-1), count=N * H * H)
+    ops.conv_fwd(yn, wk, out, spec, slab=slab, plan=plan, pro=pro)
+    an = torch.empty_like(yn)
+    ops.bn_apply(yn, stats.reshape(-1), gamma, beta, an, N * H * H, C, act=act, res=rn)
+    out2 = torch.empty_like(out)
+    ops.conv_fwd(an, wk, out2, spec, slab=slab, plan=plan)
+    close(out, out2, rtol=1e-2, atol=1e-2)
+    assert not torch.isnan(keep.float()).any()
+    close(keep.float(), an.float(), rtol=1e-2, atol=1e-2)
+
+
 def test_fused_bn_paths_propagate_nan_like_bn_hip():
     """act='none' (MobileNetV2's linear bottleneck): a NaN in the producer output must come out
     of the fused prologue as NaN, exactly where the standalone bn_apply + conv produces NaN,
