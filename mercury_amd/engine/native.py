@@ -555,17 +555,20 @@ class NativeEngine(object):
         return d
 
     def _res_pro(self, m, u, act, out, nxt, res):
-        """Block-final BN + identity residual + activation folded into the register-staged
-        load of the next block's first (pointwise) conv on igemm: a = act(bn_u(y) + res), the
-        block output ``out`` written once through the prologue's keep (MobileNetV2's linear
-        bottleneck outputs feeding the next expand conv), instead of a bn_apply pass."""
+        """Block-final BN (+ identity residual ``res``) + activation folded into the
+        register-staged load of the next block's first (pointwise) conv on igemm:
+        a = act(bn_u(y) [+ res]), the block output ``out`` written once through the prologue's
+        keep (MobileNetV2's linear-bottleneck outputs feeding the next expand conv), instead of
+        a bn_apply pass."""
         if not self.res_pro or act not in ('relu', 'relu6', 'none') or nxt.depthwise:
             return None
-        # (a pwconv / pgemm plan only runs with its own prologue kinds or plain; with this
-        # prologue the conv runs on igemm)
+        # (a pwconv plan only runs with its own prologue kind; with this prologue the conv runs
+        # on igemm -- not where the persistent GEMM would have run it plain, e.g. ResNet-50)
         if any((nxt.name, k) in m.plan for k in ('stem', 'hconv')):
             return None
         sp = m.spec[nxt.name]
+        if (nxt.name, 'pgemm') in m.plan and pgemm_plain_wins(sp):
+            return None
         if sp.R != 1 or not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=True):
             return None
         su = m.spec[u.name]
@@ -694,7 +697,7 @@ class NativeEngine(object):
                     pgd = None
                     if nb is not None and not blk.pool and nb.units and ru is None:
                         pgd = self._pg_pro(m, u, blk.final_act, out, nb.units[0], res=res)
-                        if pgd is None and res is not None:
+                        if pgd is None:
                             pgd = self._res_pro(m, u, blk.final_act, out, nb.units[0], res)
                     if pgd is not None:
                         # the next block's first (pointwise) conv applies this BN (+ identity
