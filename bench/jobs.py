@@ -103,7 +103,7 @@ def job_trace(o, a):
         shlex.split(a.args or ''), os.path.join(o, 'bench.log'), 300)
     marker = 'optimizer_fused'
     if '--replay-only' in (a.args or ''):
-        marker = 'head_bwd' if 'train' in a.args else 'pool_build'
+        marker = 'step_begin' if 'train' in a.args else 'pool_build'
     run([PY, 'bench/trace_timeline.py', tr, marker, '40'],
         os.path.join(o, 'timeline.txt'), 120)
     tail(os.path.join(o, 'timeline.txt'), 30)
