@@ -357,11 +357,17 @@ PYBIND11_MODULE(_C, m) {
     check_launch("mlp_head_bwd");
   });
   m.def("head_bwd", [](uintptr_t pooled, uintptr_t dlogits, uintptr_t w, uintptr_t dw, uintptr_t db,
-                       uintptr_t dact, int B, int HW, int C, int classes, uintptr_t st) {
+                       uintptr_t dact, int B, int HW, int C, int classes, uintptr_t st,
+                       uintptr_t bw_out, uintptr_t bw_y, uintptr_t bw_stats, uintptr_t bw_y2,
+                       uintptr_t bw_stats2, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
+                       int bw_act) {
     HeadBwdArgs a{P<const float>(pooled), P<const float>(dlogits), P<const float>(w), P<float>(dw),
-                  P<float>(db), P<bf16>(dact), B, HW, C, classes};
-    head_bwd_launch(a, S(st));
+                  P<float>(db), P<bf16>(dact), B, HW, C, classes, P<const bf16>(bw_out),
+                  P<const bf16>(bw_y), P<const float>(bw_stats), P<const bf16>(bw_y2),
+                  P<const float>(bw_stats2), P<float>(bw_sums), bw_inv_count, bw_eps, bw_act};
+    const int ok = head_bwd_launch(a, S(st));
     check_launch("head_bwd");
+    return ok;
   });
 
   m.def("pool_build", [](uintptr_t shard, uintptr_t labels, uintptr_t ctrl, uintptr_t pool,

@@ -299,6 +299,11 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
 // sample b (redundantly per class chunk -- a few KB) and computes HC_CHUNK classes, so the
 // chunks run as separate blocks; the loss / softmax kernel then runs on the ready logits.
 constexpr int HC_CHUNK = 16;
+
+MA_DEV void bn_act_bounds_h(int act, float& lo, float& hi) {   // (conv_epi.h bn_act_bounds)
+  lo = act == 0 ? -__builtin_huge_valf() : 0.f;
+  hi = act == 2 ? 6.f : __builtin_huge_valf();
+}
 __global__ __launch_bounds__(NT) void head_fc_chunk_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* pooled = sh;               // [C]
@@ -357,6 +362,35 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(HeadBwdArgs a) {
   const bf16 v = f2bf(s / (float)a.HW);
   bf16* dst = a.dact + (size_t)b * a.HW * a.C + c;
   for (int hw = 0; hw < a.HW; ++hw) dst[(size_t)hw * a.C] = v;
+  if (a.bw_sums != nullptr) {
+    // the final BN's backward sums over this sample's HW positions of channel c (the reduce
+    // pass bn_bwd would otherwise make): same arithmetic as the dgrad epilogue
+    float lo, hi;
+    bn_act_bounds_h(a.bw_act, lo, hi);
+    const bool pass = a.bw_act == 0;
+    const float m1 = a.bw_stats[c] * a.bw_inv_count;
+    const float r1 = rsqrtf(fmaxf(a.bw_stats[a.C + c] * a.bw_inv_count - m1 * m1, 0.f) + a.bw_eps);
+    float m2 = 0.f, r2 = 0.f;
+    if (a.bw_y2) {
+      m2 = a.bw_stats2[c] * a.bw_inv_count;
+      r2 = rsqrtf(fmaxf(a.bw_stats2[a.C + c] * a.bw_inv_count - m2 * m2, 0.f) + a.bw_eps);
+    }
+    const float g = bf2f(v);
+    const size_t base = (size_t)b * a.HW * a.C + c;
+    float sdz = 0.f, sx = 0.f, sx2 = 0.f;
+    for (int hw = 0; hw < a.HW; ++hw) {
+      const size_t o = base + (size_t)hw * a.C;
+      const float ov = bf2f(a.bw_out[o]);
+      const float dz = (pass || (ov > lo && ov < hi)) ? g : 0.f;
+      sdz += dz;
+      sx += dz * (bf2f(a.bw_y[o]) - m1) * r1;
+      if (a.bw_y2) sx2 += dz * (bf2f(a.bw_y2[o]) - m2) * r2;
+    }
+    float* sums = a.bw_sums + (size_t)(b % SUMS_R) * 3 * a.C;
+    atomicAdd(sums + c, sdz);
+    atomicAdd(sums + a.C + c, sx);
+    if (a.bw_y2) atomicAdd(sums + 2 * a.C + c, sx2);
+  }
 }
 }  // namespace
 
@@ -437,7 +471,7 @@ void head_loss_launch(const HeadArgs& a0, hipStream_t st) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3(a.B), dim3(NT), shm, st, a);
 }
 
-void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
+int head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
   if ((long long)a.classes * a.C >= WIDE && a.classes % 4 == 0 && a.C % 4 == 0) {
     // wide head: dact = (dlogits . W) / HW broadcast over HW, dW = dlogits^T . pooled, db
     hipLaunchKernelGGL((head_gemm_kernel<true, false, 1>),
@@ -450,8 +484,9 @@ void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st) {
                        a.classes, a.C, a.B, 1, 1.f);
     hipLaunchKernelGGL(head_db_kernel, dim3((a.classes + NT - 1) / NT), dim3(NT), 0, st,
                        a.dlogits, a.db, a.B, a.classes);
-    return;
+    return 0;
   }
   hipLaunchKernelGGL(head_bwd_kernel, dim3((a.C + NT - 1) / NT, a.B + a.classes), dim3(NT), 0, st,
                      a);
+  return a.bw_sums != nullptr;
 }

@@ -92,6 +92,17 @@ struct HeadBwdArgs {
   float* db;                     // [classes]
   bf16* dact;                    // [B][HW][C] grad of final activation
   int B, HW, C, classes;
+  // optional: also reduce the BN-backward sums of the final BN (+ shortcut BN) whose activation
+  // the head read -- as a dgrad epilogue does (EpiParams bw_*): dz = dact * act'(bw_out),
+  // sums[0] += dz, [1] += dz * xhat(bw_y), [2] += dz * xhat(bw_y2); [SUMS_R][3][C] replicas
+  const bf16* bw_out = nullptr;
+  const bf16* bw_y = nullptr;
+  const float* bw_stats = nullptr;
+  const bf16* bw_y2 = nullptr;
+  const float* bw_stats2 = nullptr;
+  float* bw_sums = nullptr;
+  float bw_inv_count = 0.f, bw_eps = 0.f;
+  int bw_act = 0;
 };
 void mlp_head_fwd_launch(const bf16* x, const bf16* w1, const float* b1, const float* w2,
                          const float* b2, float* h1, float* logits, int B, int F, int H1, int K,
@@ -99,7 +110,8 @@ void mlp_head_fwd_launch(const bf16* x, const bf16* w1, const float* b1, const f
 void mlp_head_bwd_launch(const float* dlogits, const float* h1, const bf16* x, const bf16* w1,
                          const float* w2, float* dh1, float* dw1, float* db1, float* dw2,
                          float* db2, bf16* dx, int B, int F, int H1, int K, hipStream_t st);
-void head_bwd_launch(const HeadBwdArgs& a, hipStream_t st);
+// returns 1 when the BN-backward sums (a.bw_sums) were reduced (the per-sample path)
+int head_bwd_launch(const HeadBwdArgs& a, hipStream_t st);
 
 // ------------------------------------------------------------------ importance sampling
 struct PoolBuildArgs {

@@ -185,6 +185,8 @@ class NativeEngine(object):
         self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
         # block-final BN + identity residual inside the next block's igemm pointwise conv load
         self.res_pro = self.fuse_bn_fwd and os.environ.get('MERCURY_RES_PRO', '1') == '1'
+        # the classifier head's backward reduces the final BN's backward sums
+        self.head_bw = os.environ.get('MERCURY_HEAD_BW', '1') == '1'
         # depthwise dgrad + wgrad in one launch, wgrad reduces batched at the end of the backward
         self.dw_pair = os.environ.get('MERCURY_DW_PAIR', '1') == '1'
 
@@ -1092,9 +1094,18 @@ class NativeEngine(object):
             if self.lw.head_pool == 'mlp2':
                 self._mlp_head_bwd(tm, tm.buf[last, 'dout'])
                 return
-            ops.head_bwd(tm.pooled, tm.dlogits, self._pview(self.lw.fc_w),
-                         self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True),
-                         tm.buf[last, 'dout'], self.B, tm.final_hw, tm.final_C, self.classes)
+            # the head's backward also reduces the final BN's backward sums (no bn_bwd reduce
+            # pass at the top of the last block) where its per-sample path runs
+            lb = self.lw.blocks[last]
+            bw = None
+            if self.head_bw and self.fuse_bn_bwd and not lb.pool:
+                bw = self._bw(tm, lb.units[-1], tm.buf[last, 'out'], lb.final_act,
+                              unit2=lb.shortcut)
+            if ops.head_bwd(tm.pooled, tm.dlogits, self._pview(self.lw.fc_w),
+                            self._pview(self.lw.fc_w, True), self._pview(self.lw.fc_b, True),
+                            tm.buf[last, 'dout'], self.B, tm.final_hw, tm.final_C,
+                            self.classes, bw=bw):
+                tm.prereduced[last] = True
         cuts = self.bucket_plan()
         cur = [fwd_head]
         for bi in range(len(self.lw.blocks) - 1, -1, -1):

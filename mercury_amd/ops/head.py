@@ -23,10 +23,14 @@ def head_fwd(act, w, b, label, B, HW, C, classes, mode, pooled=None, logits=None
                    stream_ptr(), SCORE[score])
 
 
-def head_bwd(pooled, dlogits, w, dw, db, dact, B, HW, C, classes):
+def head_bwd(pooled, dlogits, w, dw, db, dact, B, HW, C, classes, bw=None):
+    """Classifier-head backward.  ``bw`` (as conv_dgrad's): also reduce the BN-backward sums of
+    the final BN whose activation the head read; returns True when it did (the per-sample
+    path -- the wide GEMM path does not, and the caller then runs bn_bwd's reduce)."""
+    from .conv import _bw_args
     _chk(dact, torch.bfloat16, 'dact', B * HW * C)
-    lib().head_bwd(ptr(pooled), ptr(dlogits), ptr(w), ptr(dw), ptr(db), ptr(dact), B, HW, C,
-                   classes, stream_ptr())
+    return bool(lib().head_bwd(ptr(pooled), ptr(dlogits), ptr(w), ptr(dw), ptr(db), ptr(dact),
+                               B, HW, C, classes, stream_ptr(), *_bw_args(bw, B * HW, C)))
 
 
 def mlp_head_fwd(x, w1, b1, w2, b2, h1, logits, label, B, F, H1, classes, mode, isw=None,

@@ -1114,3 +1114,42 @@ def test_dwconv_bwd_pair_matches_separate(stride, fused):
             close(ops.sums_total(bw2['sums'], C), ops.sums_total(bw['sums'], C), 1e-4, 1e-3)
     close(dw1.view(C, 3, 3), wr.grad.view(C, 3, 3), 2e-2, 2e-2)
     close(ops.from_nhwc(dx1.view(N, H, H, C), C), xr.grad, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize('two', [False, True])
+def test_head_bwd_fused_bn_backward_reduce(two):
+    """head_bwd(bw=...) reduces the final BN's backward sums from the activation gradient it
+    writes (dz = dact * relu'(out)) -- vs torch fp32 on the produced dact."""
+    ops = _ops()
+    B, HW, C, K = 16, 16, 64, 10
+    g = torch.Generator(device='cpu').manual_seed(5)
+    pooled = torch.randn(B, C, generator=g).to(DEV)
+    dlogits = torch.randn(B, K, generator=g).to(DEV) * 0.1
+    w = torch.randn(K, C, generator=g).to(DEV) * 0.1
+    dw = torch.zeros(K * C, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    dact = torch.empty(B * HW * C, dtype=torch.bfloat16, device=DEV)
+    Mx = B * HW
+    y = bf(torch.randn(Mx, C, generator=g).to(DEV) * 2 + 0.5).to(torch.bfloat16)
+    y2 = bf(torch.randn(Mx, C, generator=g).to(DEV)).to(torch.bfloat16)
+    out = bf(torch.relu(torch.randn(Mx, C, generator=g).to(DEV))).to(torch.bfloat16)
+    stats = torch.stack([y.float().sum(0), y.float().pow(2).sum(0)]).contiguous()
+    stats2 = torch.stack([y2.float().sum(0), y2.float().pow(2).sum(0)]).contiguous()
+    sums = torch.zeros(ops.sums_numel(C), device=DEV)
+    bw = dict(out=out, y=y, stats=stats, sums=sums, act='relu', eps=1e-5)
+    if two:
+        bw.update(y2=y2, stats2=stats2)
+    assert ops.head_bwd(pooled, dlogits, w, dw, db, dact, B, HW, C, K, bw=bw)
+    d = dact.float().view(Mx, C)
+    close(d.view(B, HW, C)[:, 0], (dlogits @ w) / HW, 1e-2, 1e-3)
+    dz = d * (out.float() > 0)
+
+    def xhat(t, s):
+        mu = s[0] / Mx
+        var = (s[1] / Mx - mu * mu).clamp_min(0)
+        return (t.float() - mu) / torch.sqrt(var + 1e-5)
+    tot = ops.sums_total(sums, C)
+    close(tot[0], dz.sum(0), 1e-3, 1e-2)
+    close(tot[1], (dz * xhat(y, stats)).sum(0), 1e-3, 1e-2)
+    if two:
+        close(tot[2], (dz * xhat(y2, stats2)).sum(0), 1e-3, 1e-2)
