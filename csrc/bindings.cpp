@@ -16,6 +16,7 @@
 
 int igemm_read_stamps(unsigned long long* host, int n);
 int hconv_read_stamps(unsigned long long* host, int n);
+void hconv_configure(int grid, int waves);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
@@ -211,12 +212,19 @@ PYBIND11_MODULE(_C, m) {
     comm_ring_allreduce(c, buf, count, work, avg, st);
     check_launch("comm_ring_allreduce");
   });
-  m.def("xgmi_pack", [](uintptr_t src, uintptr_t xbuf, long long n, int bf, uintptr_t st) {
+  // the exchange kernels address a buffer through a buffer resource: 32-bit byte offsets
+  auto xgmi_range = [](long long n, int bf, const char* who) {
+    if (n < 0 || n * (bf ? 2 : 4) >= (1LL << 31))
+      throw std::invalid_argument(std::string(who) + ": exchange must be < 2 GiB (32-bit offsets)");
+  };
+  m.def("xgmi_pack", [xgmi_range](uintptr_t src, uintptr_t xbuf, long long n, int bf, uintptr_t st) {
+    xgmi_range(n, bf, "xgmi_pack");
     xgmi_pack(P<const float>(src), P<void>(xbuf), n, bf, S(st));
     check_launch("xgmi_pack");
   });
-  m.def("xgmi_reduce_scatter", [](const std::vector<uintptr_t>& peers, int rank, long long n,
-                                  int bf, float scale, uintptr_t st) {
+  m.def("xgmi_reduce_scatter", [xgmi_range](const std::vector<uintptr_t>& peers, int rank,
+                                            long long n, int bf, float scale, uintptr_t st) {
+    xgmi_range(n, bf, "xgmi_reduce_scatter");
     if (peers.empty() || (int)peers.size() > xgmi_max_ranks() || n % 4)
       throw std::invalid_argument("xgmi_reduce_scatter: 1..8 peers, n % 4 == 0");
     std::vector<const void*> p(peers.size());
@@ -224,8 +232,9 @@ PYBIND11_MODULE(_C, m) {
     xgmi_reduce_scatter(p.data(), (int)p.size(), rank, n, bf, scale, S(st));
     check_launch("xgmi_reduce_scatter");
   });
-  m.def("xgmi_all_gather", [](const std::vector<uintptr_t>& peers, long long n, int bf,
-                              uintptr_t dst, uintptr_t st) {
+  m.def("xgmi_all_gather", [xgmi_range](const std::vector<uintptr_t>& peers, long long n, int bf,
+                                        uintptr_t dst, uintptr_t st) {
+    xgmi_range(n, bf, "xgmi_all_gather");
     if (peers.empty() || (int)peers.size() > xgmi_max_ranks() || n % 4)
       throw std::invalid_argument("xgmi_all_gather: 1..8 peers, n % 4 == 0");
     std::vector<const void*> p(peers.size());
@@ -253,6 +262,7 @@ PYBIND11_MODULE(_C, m) {
     if (!igemm_read_stamps(v.data(), n)) v.clear();
     return v;
   });
+  m.def("hconv_configure", &hconv_configure);   // persistent halo grid (0: half the CUs), waves
   m.def("hconv_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!hconv_read_stamps(v.data(), n)) v.clear();

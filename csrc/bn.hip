@@ -360,6 +360,8 @@ void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
   // code evaluate every activation form and select)
   const bool two = a.y2 != nullptr;
   if (a.act < 0 || a.act > 2) throw std::runtime_error("bn_bwd: act must be 0-2");
+  // both kernels fold the sums through static LDS arrays of [3][2048] floats
+  if (a.C > 2048) throw std::runtime_error("bn_bwd: at most 2048 channels");
   const dim3 g1(grid_for(chunks, a.C / 8, 4, 256)), g2(grid_for(chunks, a.C / 8, 4, 2048));
 #define BN_BWD_CASE(A, T)                                                                 \
   if (a.act == A && two == T) {                                                           \

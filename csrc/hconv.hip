@@ -33,8 +33,6 @@
 // chunk c ^ (row & 7)).  MFMA v_mfma_f32_16x16x32_bf16 with swapped operands (lane l: output
 // pixel l&15, four consecutive channels), so the shared epilogue of conv_epi.h applies as is:
 // ghost-BN statistics, split-K (over 64-channel slices) reduced in-launch by the last slice.
-#include <cstdlib>
-
 #include "conv_epi.h"
 
 namespace {
@@ -1014,6 +1012,9 @@ int launch_persist_w(const bf16* src, const bf16* wt, const HconvGeom& g, const 
 }
 
 // WM4 / WM8: wave rows of the 4- and 8-wave blocks (MERCURY_HCONV_PERSIST_WAVES picks, 0 = none)
+int g_persist_grid = 0;      // 0: half the CUs
+int g_persist_waves = 8;     // 8 or 4
+
 template <int BM, int BN, int WM4, int WM8>
 int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                    const HconvPro& pro, hipStream_t st) {
@@ -1028,18 +1029,14 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   // blocks: half the CUs by default -- the scoring convs run beside the training stream, and a
   // grid on every CU (143 KB of LDS each) locks the training kernels out for its whole length.
   // Measured, ResNet-18 step (bench.py, same box): 256 blocks 1.653 ms, 192 1.590, 160 1.550,
-  // 128 1.525, 96 1.720, 64 2.037; per-tile kernels 1.607.  MERCURY_HCONV_PERSIST_GRID overrides.
-  static int gmax = -1, waves = -1;
-  if (gmax < 0) {
-    const char* ev = getenv("MERCURY_HCONV_PERSIST_GRID");
-    gmax = ev ? atoi(ev) : cus / 2;
-    if (gmax <= 0 || gmax > cus) gmax = cus;
-    // 8 waves (two per SIMD: one wave's waits, barriers and DMA issue overlap the other's
-    // MFMAs) where the tile has an 8-wave layout; measured 1.513 vs 1.521 and 1.534 vs 1.549
-    // ms/step (two same-box A/Bs), layer2 alone 33.4 vs 35.4 us
-    const char* wv = getenv("MERCURY_HCONV_PERSIST_WAVES");
-    waves = wv ? atoi(wv) : 8;
-  }
+  // 128 1.525, 96 1.720, 64 2.037; per-tile kernels 1.607.  hconv_configure() overrides (the
+  // engine's EngineOptions.hconv_persist_grid / _waves).
+  // 8 waves (two per SIMD: one wave's waits, barriers and DMA issue overlap the other's MFMAs)
+  // where the tile has an 8-wave layout; measured 1.513 vs 1.521 and 1.534 vs 1.549 ms/step
+  // (two same-box A/Bs), layer2 alone 33.4 vs 35.4 us
+  int gmax = g_persist_grid > 0 ? g_persist_grid : cus / 2;
+  if (gmax > cus) gmax = cus;
+  const int waves = g_persist_waves;
   const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
   const int grid = ntiles < gmax ? ntiles : gmax;
   if constexpr (WM8 > 0) {
@@ -1088,6 +1085,11 @@ int hconv_read_stamps(unsigned long long* host, int n) {
   (void)n;
   return 0;
 #endif
+}
+
+void hconv_configure(int grid, int waves) {
+  g_persist_grid = grid > 0 ? grid : 0;
+  g_persist_waves = waves == 4 ? 4 : 8;
 }
 
 int hconv_lds_bytes(const HconvGeom& g, int bm, int bn, int splits_gt1) {

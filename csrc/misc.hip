@@ -200,8 +200,9 @@ __global__ __launch_bounds__(NT) void tern_pack_kernel(const float* x, long long
                                                        uint32_t* words) {
   const long long j = (long long)blockIdx.x * NT + threadIdx.x;   // word index
   // graph-replayed steps: the Philox stream comes from the device step counter (a captured
-  // host counter would replay the same stream every step), 256 buckets per step
-  if (dctr) counter = ((uint64_t)dctr[0] << 8) + counter;
+  // host counter would replay the same stream every step): the step in the low word, the bucket
+  // index in the high word -- no two (step, bucket) pairs share a stream for < 2^32 buckets
+  if (dctr) counter = ((uint64_t)(uint32_t)counter << 32) | (uint64_t)(uint32_t)dctr[0];
   const long long nw = (n + 15) / 16;
   const float m = *amax;
   if (j == 0) words[0] = __float_as_uint(m);

@@ -110,3 +110,86 @@ class Config:
     def to_dict(self):
         return dataclasses.asdict(self)
 
+
+@dataclass
+class EngineOptions:
+    """Kernel-path switches of the native engine (``engine/native.py``).
+
+    The defaults are the measured-best paths; every field names the same-box A/B that keeps
+    it (``profiles/``).  Set them in code (``NativeEngine(..., opts=EngineOptions(...))``) or,
+    for A/B runs of an unmodified tree, with ONE environment variable parsed by ``from_env``:
+
+        MERCURY_ENGINE_OPTS="hconv=score,pgemm=0,hconv_plans=32,16,128,128=64,64,1"
+
+    (items separated by ',' where the next item starts with ``name=``)."""
+    # stride-1 3x3 convs on the halo-tile kernel: '1' both batch modes, 'score' / 'train' one,
+    # '0' igemm everywhere (profiles/r2/ab_hconv_modes.json, ab_train_persist.json)
+    hconv: str = '1'
+    # persistent halo-kernel plans ('0' per-tile plans only; profiles/r2/ab_hconv_persistent.json)
+    hconv_persist: bool = True
+    # persistent halo-kernel grid (0: half the CUs -- the scoring convs run beside the train
+    # stream; 256 blocks 1.653, 128 1.525 ms/step, profiles/r2/ab_hconv_persistent.json)
+    hconv_persist_grid: int = 0
+    # waves per persistent halo block (8: 1.513 vs 1.521 ms/step over 4)
+    hconv_persist_waves: int = 8
+    # per-shape halo plan overrides for sweeps: "N,H,C,K=bm,bn,splits;..." ('none' = igemm)
+    hconv_plans: str = ''
+    # 1x1 convs on the persistent LDS-DMA pointwise GEMM (profiles/r3/pgemm_cmp_v2.jsonl)
+    pgemm: bool = True
+    # narrow-input expansion 1x1 convs on the panel-resident kernel (pwconv_engine_ab.json)
+    pwconv: bool = True
+    # first conv on the dense-k stem kernel (stem_bench_v2.jsonl)
+    stem: bool = True
+    # intra-block BN + activation folded into the consuming conv's operand load
+    fuse_bn_fwd: bool = True
+    # block-final BN + identity residual in the next block's pointwise conv load (ab_res_pro.json)
+    res_pro: bool = True
+    # depthwise convs take their input's BN + activation in their loads (MobileNetV2)
+    dw_pro: bool = True
+    # depthwise dgrad + wgrad in one launch, wgrad reduces batched (ab_dw_pair.json)
+    dw_pair: bool = True
+    # the classifier head's backward reduces the final BN's backward sums (ab_head_bw.json)
+    head_bw: bool = True
+    # stride-2 dgrad as four parity classes (ab_dgrad_s2.json)
+    dgrad_s2: bool = True
+    # one-launch optimizer that also writes the bf16 weight copies (bench_fused_opt_r2h.json)
+    fused_opt: bool = True
+    # bucket all-reduces captured inside the train graph (dp_capture_ab.json: off)
+    capture_comm: bool = False
+    # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
+    score_min_blocks: int = 128
+    # debug mode: print each phase as it completes
+    debug_log: bool = False
+    # REJECTED paths kept for re-measurement (off): the input BN (+ residual / shortcut BN) in
+    # the per-tile halo conv's staging ('1' / 'score' / 'train'; profiles/r2/ab_fuse_bn_halo.json:
+    # off 1.602, score 1.634, train 1.724 ms/step) and the scoring pass's intra-block BN inside
+    # the persistent halo conv (profiles/r2/ab_persist_bn.json: 1.528 off vs 1.551 on)
+    fuse_bn_halo: str = '0'
+    persist_bn: bool = False
+
+    @classmethod
+    def from_env(cls, base=None):
+        import os
+        import re
+        o = dataclasses.replace(base) if base is not None else cls()
+        spec = os.environ.get('MERCURY_ENGINE_OPTS', '').strip()
+        if not spec:
+            return o
+        types = {f.name: f.type for f in dataclasses.fields(cls)}
+        for item in re.split(r',(?=[a-z_]+=)', spec):
+            if '=' not in item:
+                raise ValueError('MERCURY_ENGINE_OPTS: %r is not name=value' % item)
+            k, v = item.split('=', 1)
+            k = k.strip()
+            if k not in types:
+                raise ValueError('MERCURY_ENGINE_OPTS: unknown option %r (EngineOptions)' % k)
+            t = types[k]
+            if t in ('bool', bool):
+                val = v.strip().lower() in ('1', 'true', 'yes', 'on')
+            elif t in ('int', int):
+                val = int(v)
+            else:
+                val = v.strip()
+            setattr(o, k, val)
+        return o
+

@@ -23,7 +23,6 @@ a step costs a handful of host calls.  All buffers are allocated up front.
 from __future__ import annotations
 
 import math
-import os
 import time
 
 import numpy as np
@@ -72,8 +71,11 @@ class NativeEngine(object):
                  importance=True, world_size=1, bucket_bytes=None, use_graphs=True,
                  sampler='alias', exchange_scores=False, global_table=True, score='loss',
                  global_ema=False, autotune=None, force_buckets=False, comm='auto',
-                 wire_bf16=False, debug=False, check_order=False, grad_compress=None):
+                 wire_bf16=False, debug=False, check_order=False, grad_compress=None,
+                 opts=None):
         ops.lib()
+        from ..config import EngineOptions
+        self.opts = opts if opts is not None else EngineOptions.from_env()
         if autotune is not None:
             tune.enable(autotune)
         self.net = net
@@ -115,8 +117,7 @@ class NativeEngine(object):
         # (forced buckets, same box, profiles/r3/dp_capture_ab.json) the captured RCCL graph ran
         # 1.948 ms/step vs 1.598 for the segmented replays (non-DP 1.429) -- RCCL's captured
         # collectives cost more than the host-issued ones.  MERCURY_CAPTURE_COMM=1 turns it on.
-        self.capture_comm = self.s_comm is not None and \
-            os.environ.get('MERCURY_CAPTURE_COMM', '0') == '1'
+        self.capture_comm = self.s_comm is not None and self.opts.capture_comm
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         if grad_compress not in (None, 'none', 'ternary'):
             raise ValueError("grad_compress must be None, 'none' or 'ternary'")
@@ -148,47 +149,22 @@ class NativeEngine(object):
         self.fuse_bn_bwd = True          # BN-backward reduce in the dgrad epilogue
         self.roctx = False               # per-phase roctx ranges around the step's host calls
         self.pair_bwd = True             # dgrad + wgrad of a conv in one launch
-        # intra-block BN-apply folded into the next conv's operand load (no bn_apply pass)
-        self.fuse_bn_fwd = os.environ.get('MERCURY_FUSE_BN_FWD', '1') == '1'
-        # input BatchNorm (+ residual / shortcut BN) folded into the halo conv's staging, on the
-        # shapes where that measured faster than a bn_apply pass + the conv ALONE
-        # (ops/hconv.fused_plan).  ('1' both batch modes, 'score' / 'train' one, '0' off.)
-        # Off by default: in the two-stream step it lost (same-box A/B, profiles/r2/
-        # ab_fuse_bn_halo.json: off 1.602, score 1.634, train 1.724 ms/step) -- its blocks take
-        # one wave per SIMD and up to 150 KB of LDS, so the other stream's kernels cannot share
-        # their CUs; the bn_apply passes it removes are cheap to co-schedule
-        self.fuse_bn_halo = os.environ.get('MERCURY_FUSE_BN_HALO', '0')
-        # stride-1 3x3 forward convs on the halo-tile kernel (csrc/hconv.hip) where measured faster
-        # ('1' both batch modes, 'score' / 'train' one of them, '0' off).  With the per-tile
-        # kernel only the scoring pass gained (profiles/r2/ab_hconv_modes.json: off 1.614,
-        # score 1.605, train 1.615, both 1.640 ms/step -- its one-wave-per-SIMD blocks crowd the
-        # concurrent train kernels out); with the persistent 8-wave kernel on the train shapes
-        # too, both passes win: 1.536 (score) vs 1.521 ms (both), profiles/r2/ab_train_persist.json
-        self.use_hconv = os.environ.get('MERCURY_HCONV', '1')
-        # the scoring pass's intra-block BN + ReLU inside the persistent halo conv's staging.
-        # Off by default: same-box A/B (profiles/r2/ab_persist_bn.json) 1.528 off vs 1.551 ms
-        # on -- the in-LDS transform costs the persistent blocks more than the 8 bn_apply passes
-        # it removes cost the step
-        self.persist_bn = os.environ.get('MERCURY_PERSIST_BN', '0') == '1'
-        # 1x1 convs on the persistent LDS-DMA pointwise GEMM (csrc/pgemm.hip): plain where it
-        # measured faster than igemm (>= 128 output channels, profiles/r3/pgemm_cmp_v2.jsonl),
-        # and wherever it takes its input's BN + activation (+ identity residual) in LDS --
-        # intra-block BNs and the block-final BN of the previous block, which then never make a
-        # separate bn_apply pass (the consumer's N-tile-0 tiles write the activation once where
-        # the residual / backward need it).  MERCURY_PGEMM=0: igemm + bn_apply passes.
-        self.use_pgemm = os.environ.get('MERCURY_PGEMM', '1') == '1'
-        # narrow-input 1x1 convs with the input BN on the panel-resident kernel (pwconv.hip)
-        self.use_pwconv = os.environ.get('MERCURY_PWCONV', '1') == '1'
-        # the first conv (<= 4 input channels) on the dense-k stem kernel (stem.hip)
-        self.use_stem = os.environ.get('MERCURY_STEM', '1') == '1'
-        # depthwise convs take their input's BN + activation in their chunk loads
-        self.dw_pro = os.environ.get('MERCURY_DW_PRO', '1') == '1'
-        # block-final BN + identity residual inside the next block's igemm pointwise conv load
-        self.res_pro = self.fuse_bn_fwd and os.environ.get('MERCURY_RES_PRO', '1') == '1'
-        # the classifier head's backward reduces the final BN's backward sums
-        self.head_bw = os.environ.get('MERCURY_HEAD_BW', '1') == '1'
-        # depthwise dgrad + wgrad in one launch, wgrad reduces batched at the end of the backward
-        self.dw_pair = os.environ.get('MERCURY_DW_PAIR', '1') == '1'
+        # kernel-path switches (config.EngineOptions: defaults = the measured-best paths, each
+        # with the A/B that keeps it)
+        o = self.opts
+        self.fuse_bn_fwd = o.fuse_bn_fwd
+        self.use_hconv = o.hconv
+        self.use_pgemm = o.pgemm
+        self.use_pwconv = o.pwconv
+        self.use_stem = o.stem
+        self.dw_pro = o.dw_pro
+        self.res_pro = o.fuse_bn_fwd and o.res_pro
+        self.head_bw = o.head_bw
+        self.dw_pair = o.dw_pair
+        self.fuse_bn_halo = o.fuse_bn_halo
+        self.persist_bn = o.persist_bn
+        hconv.configure(o)
+        ops.conv.DGRAD_S2 = o.dgrad_s2
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
@@ -214,7 +190,7 @@ class NativeEngine(object):
         # debug mode also serialises the streams, runs eagerly and syncs after every phase
         self.check_order = check_order or debug
         self.order = torch.zeros(16, dtype=torch.int32, device=self.device)
-        self.debug_log = os.environ.get('MERCURY_DEBUG_LOG', '0') == '1'
+        self.debug_log = self.opts.debug_log
         if self.comm_kind == 'xgmi':
             from ..parallel.xgmi import XgmiAllReduce
             cap = max(e - s_ for s_, e in self.bucket_plan().values())
@@ -276,7 +252,7 @@ class NativeEngine(object):
                          w_krsc=self.w1p, w_crsk=None)
             segs.append(d)
         self.opt = ops.FlatOptimizer(segs, self.lw.total, self.device, optimizer, lr, betas, eps,
-                                     wd, momentum)
+                                     wd, momentum, fused=self.opts.fused_opt)
         self.load_from_module()
 
     def _pview(self, seg, grad=False):
@@ -361,8 +337,7 @@ class NativeEngine(object):
                     # the scoring pass runs beside the latency-bound train chain: fewer, larger
                     # tiles leave the train kernels more room (measured, ResNet-18: 128-block
                     # target 1.656 vs 256-block 1.667 ms/step; split-K or 512 blocks slower)
-                    mb = int(os.environ.get('MERCURY_SCORE_MIN_BLOCKS', '128')) \
-                        if group_imgs else 0
+                    mb = self.opts.score_min_blocks if group_imgs else 0
                     m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(
                         sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
@@ -436,10 +411,7 @@ class NativeEngine(object):
                 h, w = P_, Q_
             m.buf[bi, 'hw'] = (h, w)
             H, W, C = h, w, K
-        # (timing probe builds with -DMERCURY_SPREAD_PROBE=F add 8 replicas of F floats past it)
-        spread = int(os.environ.get('MERCURY_SPREAD_PROBE_FLOATS', '0'))
-        m.stats_store = torch.zeros(max(nstats, 1) + 8 * spread, device=dev)
-        m.stats_arena = m.stats_store[:max(nstats, 1)]
+        m.stats_arena = torch.zeros(max(nstats, 1), device=dev)
         m.sums_arena = torch.zeros(max(nsums, 1), device=dev)
         for key, off in list(m.stats.items()):
             u = next(x for x in self.units if x.name == key)

@@ -10,7 +10,6 @@ to straddle a 32-image stat group; ``pick_tiles`` enforces that.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -463,7 +462,7 @@ def _bw_args(bw, Mx, Cp):
             _ACT[bw.get('act')])
 
 
-DGRAD_S2 = os.environ.get('MERCURY_DGRAD_S2', '1') == '1'
+DGRAD_S2 = True    # EngineOptions.dgrad_s2 (the engine sets it)
 
 
 def dgrad_s2_ok(spec: ConvSpec):

@@ -11,7 +11,6 @@ Reference: the conv/BN/ReLU stack of `pytorch_model.py:19-36,72-97`.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
@@ -71,10 +70,22 @@ def lds_bytes(g, bm, bn, splits):
     return max(main, red)
 
 
+# engine-selected settings (config.EngineOptions via ``configure``)
+_CFG = dict(persist=True, plans='', waves=8, grid=0)
+
+
+def configure(opts):
+    """Take the halo-kernel switches of an ``EngineOptions`` (the persistent kernel's grid and
+    wave count are also handed to the C++ launcher)."""
+    _CFG.update(persist=bool(opts.hconv_persist), plans=opts.hconv_plans or '',
+                waves=8 if opts.hconv_persist_waves == 8 else 4,
+                grid=int(opts.hconv_persist_grid))
+    lib().hconv_configure(_CFG['grid'], _CFG['waves'])
+
+
 def persist_waves():
-    """Waves per persistent block (csrc/hconv.hip launch_persist reads the same variable)."""
-    w = int(os.environ.get('MERCURY_HCONV_PERSIST_WAVES', '8'))
-    return 8 if w == 8 else 4
+    """Waves per persistent block (the C++ launcher uses the same value: ``configure``)."""
+    return _CFG['waves']
 
 
 def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
@@ -255,21 +266,10 @@ MEASURED_PERSIST = {
     (32, 8, 256, 256): (64, 64, 0),
 }
 MEASURED_PERSIST_S2 = {(320, 8, 256, 512): (64, 64, 0)}
-# slower than the per-tile / igemm plans in isolation, candidates beside the training stream
-# (MERCURY_HCONV_PERSIST=all)
-PERSIST_EXTRA = {(320, 4, 512, 512): (128, 64, 0), (320, 32, 64, 128): (64, 64, 0),
-                 (320, 16, 128, 256): (64, 64, 0)}
-
-
-def _persist_enabled():
-    return os.environ.get('MERCURY_HCONV_PERSIST', '1') != '0'
-
-
 def _plan_override(key):
-    """MERCURY_HCONV_PLANS="N,H,C,K=bm,bn,splits;..." (A/B runs): a plan for that shape, or
-    'none' for igemm.  Returns (found, plan)."""
-    ev = os.environ.get('MERCURY_HCONV_PLANS', '')
-    for item in filter(None, ev.split(';')):
+    """EngineOptions.hconv_plans = "N,H,C,K=bm,bn,splits;..." (A/B runs): a plan for that
+    shape, or 'none' for igemm.  Returns (found, plan)."""
+    for item in filter(None, _CFG['plans'].split(';')):
         k, v = item.split('=')
         if tuple(int(t) for t in k.split(',')) == key:
             return True, (None if v == 'none' else tuple(int(t) for t in v.split(',')))
@@ -278,7 +278,7 @@ def _plan_override(key):
 
 def engine_plan(spec: ConvSpec, bias=False):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured
-    persistent-kernel winners (MERCURY_HCONV_PERSIST=0 turns them off), measured per-tile
+    persistent-kernel winners (EngineOptions.hconv_persist=0 turns them off), measured per-tile
     winners, else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every
     measured shape)."""
     if not supported(spec):
@@ -293,14 +293,8 @@ def engine_plan(spec: ConvSpec, bias=False):
             return p
     # (the measured tables are keyed by the square CIFAR shapes)
     key = (spec.N, spec.H, spec.C, spec.K) if spec.H == spec.W else None
-    if _persist_enabled() and not bias and key is not None:
+    if _CFG['persist'] and not bias and key is not None:
         p = (MEASURED_PERSIST if spec.stride == 1 else MEASURED_PERSIST_S2).get(key)
-        mode = os.environ.get('MERCURY_HCONV_PERSIST', '1')
-        if p is None and (mode == 'all' or (mode == 'l4' and spec.stride == 1)):
-            p = PERSIST_EXTRA.get(key)
-        bm_env = int(os.environ.get('MERCURY_HCONV_PERSIST_BM', '0'))
-        if p is not None and bm_env:
-            p = (min(bm_env, p[0]), p[1], 0)
         if p is not None and persistent_ok(spec, p[0], p[1]):
             g = geometry_cached(spec, p[0], p[1])
             if g is not None and lds_bytes(g, *p) <= LDS_MAX:
@@ -319,7 +313,7 @@ def engine_plan(spec: ConvSpec, bias=False):
 
 def persist_bn_plan(spec: ConvSpec, group_imgs):
     """The persistent plan with the input's BN + activation in the halo staging (no residual),
-    or None.  Scoring pass only (MERCURY_PERSIST_BN, engine)."""
+    or None.  Scoring pass only (EngineOptions.persist_bn, engine)."""
     p = engine_plan(spec)
     if p is None or p[2] != 0:
         return None

@@ -9,7 +9,6 @@ is one launch; ``set_lr`` is a 4-byte host->device copy done outside graphs
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -62,7 +61,7 @@ def optimizer_spec(optimizer):
 class FlatOptimizer(object):
 
     def __init__(self, segments, total, device, algo='adam', lr=1e-3, betas=(0.9, 0.999),
-                 eps=1e-8, weight_decay=0.0, momentum=0.9):
+                 eps=1e-8, weight_decay=0.0, momentum=0.9, fused=True):
         self.device = torch.device(device)
         self.total = int(total)
         self.segments = segments
@@ -114,7 +113,7 @@ class FlatOptimizer(object):
         pre = [0]
         for _, n in ew:
             pre.append(pre[-1] + n // 4)
-        self.fused = os.environ.get('MERCURY_FUSED_OPT', '1') == '1'
+        self.fused = bool(fused)        # EngineOptions.fused_opt
         self.n_fjobs = len(fjobs)
         self.fjobs = torch.tensor(fjobs if fjobs else [(0, 0, 0, 0)], dtype=torch.int32,
                                   device=device).contiguous()

@@ -11,9 +11,9 @@ Bucket size is chosen for xGMI: an 8-GPU MI355X node is fully connected with
 7 links per GPU (~153 GB/s each).  RCCL splits a bucket into per-channel ring
 slices; for every link to carry a slice worth its latency the bucket should
 be >= 7 x ~512 KB, while fewer, larger buckets amortise the ~10-20 us launch
-latency of each collective.  ``default_bucket_bytes`` picks 4 MB below 4 GPUs
-and 8 MB above (ResNet-18: layer4 alone is 33.6 MB, so it is split in
-4-5 buckets and the first goes out while layer3 backward is still running).
+latency of each collective.  ``default_bucket_bytes`` documents the size model
+(see its docstring); the W = 8 choice is a model, not a measurement -- no
+multi-GPU node has run this code yet.
 
 ``average`` uses ``ReduceOp.AVG`` on RCCL (folds the 1/W into the collective,
 removing the reference's extra divide) and SUM + scale on gloo.  Optional

@@ -136,7 +136,7 @@ def test_native_rccl_buckets_world1():
     from mercury_amd.data.datasets import synthetic_arrays
     x, y = synthetic_arrays(3000, 10, seed=5)
     _init_nccl_w1()
-    os.environ['MERCURY_CAPTURE_COMM'] = '1'
+    os.environ['MERCURY_ENGINE_OPTS'] = 'capture_comm=1'
     try:
         base = _engine(x, y)
         runs = {'rccl': _engine(x, y, force_buckets=True, comm='rccl', check_order=True,
@@ -147,7 +147,7 @@ def test_native_rccl_buckets_world1():
                 'tern': _engine(x, y, force_buckets=True, comm='rccl', grad_compress='ternary')}
         e = runs['rccl']
         assert e.comm is not None and e.comm.size == 1 and len(e.bucket_plan()) > 1
-        # MERCURY_CAPTURE_COMM=1 (set by the test): the untimed DP step is ONE captured train
+        # capture_comm=1 (EngineOptions, set by the test): the untimed DP step is ONE captured train
         # graph with the all-reduces inside it
         for name in ('rccl', 'bf16', 'xgmi', 'tern'):
             assert 'train_dp' in runs[name].graphs, name
@@ -188,7 +188,7 @@ def test_native_rccl_buckets_world1():
         torch.cuda.synchronize()
         assert torch.equal(gg, ref)
     finally:
-        os.environ.pop('MERCURY_CAPTURE_COMM', None)
+        os.environ.pop('MERCURY_ENGINE_OPTS', None)
         dist.destroy_process_group()
 
 

@@ -87,7 +87,7 @@ def test_train_forward_backward_matches_torch(arch, hw):
 def test_scoring_ghost_bn_matches_ten_separate_forwards(persist_bn, monkeypatch):
     """(persist_bn: the intra-block BN + ReLU applied inside the persistent halo conv)"""
     from mercury_amd.models import ResNet18
-    monkeypatch.setenv('MERCURY_PERSIST_BN', persist_bn)
+    monkeypatch.setenv('MERCURY_ENGINE_OPTS', 'persist_bn=' + persist_bn)
     torch.manual_seed(1)
     net = ResNet18(10).to(DEV)
     eng = _engine(net)

@@ -54,3 +54,20 @@ def test_quantize_unbiased():
         assert set(torch.unique(q.abs()).tolist()) <= {0.0, float(a.abs().max())}
         acc += q
     assert (acc / 400 - a).abs().mean() < 0.1
+
+
+def test_engine_options_from_env(monkeypatch):
+    """EngineOptions: defaults, and the one A/B variable (values may contain ',' and '=')."""
+    from mercury_amd.config import EngineOptions
+    monkeypatch.delenv('MERCURY_ENGINE_OPTS', raising=False)
+    assert EngineOptions.from_env() == EngineOptions()
+    monkeypatch.setenv('MERCURY_ENGINE_OPTS',
+                       'hconv=score,pgemm=0,hconv_plans=32,16,128,128=64,64,1;32,8,256,256=none,'
+                       'hconv_persist_grid=96')
+    o = EngineOptions.from_env()
+    assert o.hconv == 'score' and o.pgemm is False and o.hconv_persist_grid == 96
+    assert o.hconv_plans == '32,16,128,128=64,64,1;32,8,256,256=none'
+    monkeypatch.setenv('MERCURY_ENGINE_OPTS', 'no_such_option=1')
+    import pytest
+    with pytest.raises(ValueError):
+        EngineOptions.from_env()
