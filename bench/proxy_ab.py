@@ -36,12 +36,23 @@ def patches(name):
     def skip_bn_bwd(eng):
         eng._bn_bwd = lambda *a, **k: None
 
+    def skip_comm(eng):
+        # DP machinery kept (segmented graphs, comm-stream event edges), collective skipped
+        class NoComm(object):
+            size = eng.comm.size
+
+            def allreduce(self, t, avg=True):
+                return t
+        eng.comm = NoComm()
+
     table = {
         'base': [],
         'score_bn': [skip_bn_apply(lambda m: not m.train)],
         'train_fwd_bn': [skip_bn_apply(lambda m: m.train)],
         'train_bwd_bn': [skip_bn_bwd],
         'all_bn': [skip_bn_apply(lambda m: True), skip_bn_bwd],
+        'dp': [],                      # (--dp: every variant runs forced buckets)
+        'dp_nocomm': [skip_comm],
     }
     return table[name]
 
@@ -53,6 +64,10 @@ def main():
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--variants', default='base,score_bn,train_fwd_bn,train_bwd_bn,all_bn')
+    ap.add_argument('--dp', default='',
+                    help="comma list of variants run with forced DP buckets (RCCL, W = 1)")
+    ap.add_argument('--opts', default='',
+                    help="'|'-separated EngineOptions specs, one per variant named opt<i>")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -67,11 +82,23 @@ def main():
     net = build_model(pre['model'], pre['classes']).to(dev)
     res = {}
     names = args.variants.split(',')
+    dp = set(filter(None, args.dp.split(',')))
+    optspecs = [o for o in args.opts.split('|') if o] if args.opts else []
+    names += ['opt%d' % i for i in range(len(optspecs))]
+    if dp:
+        from mercury_amd.parallel import dist as pdist
+        pdist.init_from_env(force=True)
+    from mercury_amd.config import EngineOptions
     for rnd in range(args.rounds):
         for name in names:
+            opts = None
+            if name.startswith('opt'):
+                os.environ['MERCURY_ENGINE_OPTS'] = optspecs[int(name[3:])]
+                opts = EngineOptions.from_env()
+                os.environ.pop('MERCURY_ENGINE_OPTS')
             eng = NativeEngine(net, dev, pre['batch'], 10, optimizer='adam', lr=0.001, seed=7,
-                               image_hw=hw)
-            for p in patches(name):
+                               image_hw=hw, force_buckets=name in dp, opts=opts)
+            for p in patches(name) if not name.startswith('opt') else []:
                 p(eng)
             eng.set_shard(x_all, y_all)
             eng.prime()

@@ -17,6 +17,8 @@
 int igemm_read_stamps(unsigned long long* host, int n);
 int hconv_read_stamps(unsigned long long* host, int n);
 void hconv_configure(int grid, int waves);
+int ubench_mfma(int shape, int lds, const bf16* src, int trips, int grid, float* out,
+                hipStream_t st);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
@@ -35,6 +37,9 @@ void xgmi_reduce_scatter(const void* const* peers, int W, int rank, long long n,
 void xgmi_all_gather(const void* const* peers, int W, long long n, int bf, float* dst,
                      hipStream_t st);
 int xgmi_max_ranks();
+void xgmi_barrier(const void* const* flag_areas, int W, int rank, unsigned* epoch,
+                  double timeout_s, int* err, hipStream_t st);
+int xgmi_flag_bytes();
 std::string xgmi_ipc_handle(uintptr_t ptr);
 uintptr_t xgmi_ipc_open(const std::string& handle);
 uintptr_t xgmi_malloc(long long bytes);
@@ -242,6 +247,17 @@ PYBIND11_MODULE(_C, m) {
     xgmi_all_gather(p.data(), (int)p.size(), n, bf, P<float>(dst), S(st));
     check_launch("xgmi_all_gather");
   });
+  m.def("xgmi_barrier", [](const std::vector<uintptr_t>& flag_areas, int rank, uintptr_t epoch,
+                           double timeout_s, uintptr_t err, uintptr_t st) {
+    if (flag_areas.empty() || (int)flag_areas.size() > xgmi_max_ranks() || rank < 0 ||
+        rank >= (int)flag_areas.size())
+      throw std::invalid_argument("xgmi_barrier: 1..8 flag areas, 0 <= rank < W");
+    std::vector<const void*> p(flag_areas.size());
+    for (size_t i = 0; i < flag_areas.size(); ++i) p[i] = P<const void>(flag_areas[i]);
+    xgmi_barrier(p.data(), (int)p.size(), rank, P<unsigned>(epoch), timeout_s, P<int>(err), S(st));
+    check_launch("xgmi_barrier");
+  });
+  m.def("xgmi_flag_bytes", &xgmi_flag_bytes);
   m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(xgmi_ipc_handle(p)); });
   m.def("xgmi_ipc_open", [](py::bytes h) { return xgmi_ipc_open(std::string(h)); });
   m.def("xgmi_ipc_close", &xgmi_ipc_close);
@@ -262,7 +278,13 @@ PYBIND11_MODULE(_C, m) {
     if (!igemm_read_stamps(v.data(), n)) v.clear();
     return v;
   });
-  m.def("hconv_configure", &hconv_configure);   // persistent halo grid (0: half the CUs), waves
+  m.def("hconv_configure", &hconv_configure);
+  m.def("ubench_mfma", [](int shape, int lds, uintptr_t src, int trips, int grid, uintptr_t out,
+                          uintptr_t st) {
+    if (!ubench_mfma(shape, lds, P<const bf16>(src), trips, grid, P<float>(out), S(st)))
+      throw std::invalid_argument("ubench_mfma: shape 16 / 32, lds 0 / 1");
+    check_launch("ubench_mfma");
+  });   // persistent halo grid (0: half the CUs), waves
   m.def("hconv_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!hconv_read_stamps(v.data(), n)) v.clear();

@@ -14,9 +14,11 @@
 //                    writes the full reduced vector into the local destination.
 //
 // Each rank moves 2 (W-1)/W n elements over xGMI -- the same as a ring -- but spread over
-// W-1 links instead of one.  The passes are separated by stream-ordered barriers (a one-
-// element RCCL all-reduce on the same stream, or a host barrier in tests), so the kernels
-// themselves need no cross-GPU flags.  Exchange-buffer traffic uses system-coherent (sc0|sc1)
+// W-1 links instead of one.  The passes are separated by stream-ordered barriers: a one-block
+// kernel that writes this rank's epoch into every peer's flag slot (system-scope atomic
+// stores into the IPC-mapped flag area) and polls its own flag area until every peer has
+// written the same epoch (bounded: a peer that never arrives sets an error word and the kernel
+// exits instead of spinning forever).  Host barriers remain for tests.  Exchange-buffer traffic uses system-coherent (sc0|sc1)
 // buffer loads and stores, so no reader depends on kernel-boundary cache maintenance.  ``wire_bf16``: the exchange buffers hold bf16 (half the
 // bytes over the links); sums are accumulated in fp32 and rounded once per pass.
 //
@@ -152,6 +154,39 @@ void xgmi_all_gather(const void* const* peers, int W, long long n, int bf, float
     hipLaunchKernelGGL(xgmi_ag_kernel<false>, grid, dim3(256), 0, st, p, W, n4, dst);
 }
 
+// ---------------------------------------------------------------- device-side barrier
+// Flag area: XMAX slots of 128 B (one line each) at the head of every rank's exchange
+// allocation; slot q of rank r's area is written ONLY by rank q.  The epoch is this rank's
+// count of barriers (all ranks run the same sequence, graph replays included), so a slot
+// holding epoch e means that peer has reached barrier e.
+constexpr int FLAG_STRIDE = 32;    // uint32 per slot (128 B)
+
+__global__ __launch_bounds__(64) void xgmi_barrier_kernel(Peers flags, unsigned* own, int W,
+                                                          int rank, unsigned* epoch,
+                                                          unsigned long long timeout, int* err) {
+  const int q = threadIdx.x;
+  const unsigned e = epoch[0] + 1u;
+  // everything this rank wrote into its exchange buffer before the barrier (earlier kernels of
+  // this stream, system-coherent stores) is visible system-wide before the signal
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (q < W && q != rank) {
+    unsigned* slot = (unsigned*)flags.p[q] + rank * FLAG_STRIDE;
+    __hip_atomic_store(slot, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* mine = own + q * FLAG_STRIDE;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      __builtin_amdgcn_s_sleep(4);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {   // 100 MHz ticks
+        atomicOr(err, 1 << q);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (q == 0) epoch[0] = e;
+}
+
 int xgmi_max_ranks() { return XMAX; }
 
 // IPC: export a device allocation / map a peer's (one process per GPU; HSA_ENABLE_IPC_MODE_LEGACY=0)
@@ -169,6 +204,17 @@ uintptr_t xgmi_ipc_open(const std::string& handle) {
   if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return 0;
   return reinterpret_cast<uintptr_t>(p);
 }
+
+void xgmi_barrier(const void* const* flag_areas, int W, int rank, unsigned* epoch,
+                  double timeout_s, int* err, hipStream_t st) {
+  Peers p{};
+  for (int q = 0; q < W && q < XMAX; ++q) p.p[q] = flag_areas[q];
+  const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);
+  hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, st, p, (unsigned*)flag_areas[rank],
+                     W, rank, epoch, ticks, err);
+}
+
+int xgmi_flag_bytes() { return XMAX * FLAG_STRIDE * 4; }
 
 uintptr_t xgmi_malloc(long long bytes) {
   void* p = nullptr;

@@ -781,13 +781,15 @@ class NativeEngine(object):
             # pass; one batch group in train mode, no shortcut BN)
             if bw is not None and (not self.fuse_bn_bwd or bw.get('y2') is not None):
                 bw = None
-            # dgrad + wgrad in one launch; without DP the wgrad partials' reduce is deferred
-            # to one batched launch at the end of the backward (flush_dw_reduces) -- nothing
-            # reads a depthwise weight gradient before the optimizer
+            # dgrad + wgrad in one launch; the wgrad partials' reduce is deferred to one batched
+            # launch (flush_dw_reduces) -- nothing reads a depthwise weight gradient before the
+            # optimizer or its bucket's all-reduce
             off, n, nblk = m.dw_region[u.name]
             region = m.dw_slab[off:off + n]
             gw = self._pview(u.w_seg, grad=True)
-            defer = not self.dp
+            # deferred to one batched launch: at the end of the backward, or (DP) before the
+            # bucket all-reduce that carries this weight gradient (train_segments)
+            defer = True
             ops.dwconv_bwd(dy, x, self._pview(u.w_seg), dx, gw, sp.N, sp.H, sp.W, sp.C, sp.P,
                            sp.Q, sp.stride, sp.pad, region, bw=bw, reduce=not defer)
             if defer:
@@ -1079,16 +1081,21 @@ class NativeEngine(object):
                             self.classes, bw=bw):
                 tm.prereduced[last] = True
         cuts = self.bucket_plan()
+        dw = any(u.depthwise for u in self.units)
         cur = [fwd_head]
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
             for i, f in self.backward_parts(tm, bi):
                 cur.append(f)
                 if (bi, i) in cuts:
+                    if dw:
+                        # the bucket's depthwise weight gradients are complete before it
+                        # all-reduces (a no-op when none is pending)
+                        cur.append(lambda: self.flush_dw_reduces(tm))
                     segs.append((cur, cuts[bi, i]))
                     cur = []
         if cur:
             segs.append((cur, None))
-        if any(u.depthwise for u in self.units) and not self.dp:
+        if dw:
             segs[-1][0].append(lambda: self.flush_dw_reduces(tm))
         if self.check_order:
             # every train segment ticks o[2]; the comm stream checks it before reducing
@@ -1321,9 +1328,12 @@ class NativeEngine(object):
                 self._order(slot=2, ref=3, mult=self._nseg, add=si + 1, ge=True, at=6)
             self.timer.bucket(i, 0, self.s_comm)
             if self.xgmi is not None:
-                # direct two-shot over xGMI (all peers' exchange buffers mapped by IPC); the
-                # bf16 wire option lives in its exchange buffers
-                self.xgmi.allreduce(g, avg=True)
+                # direct two-shot over xGMI (all peers' exchange buffers mapped by IPC, device
+                # flag barriers); consecutive buckets alternate the two exchange slots; the bf16
+                # wire option lives in the exchange buffers
+                self.xgmi.allreduce(g, avg=True, slot=i % 2)
+                if i == len(self.bucket_plan()) - 1:
+                    self.xgmi.end_step(i + 1)
             elif self.tern is not None:
                 # 2-bit stochastic ternary codes + one scale per rank, all-gathered (1/16 of
                 # the fp32 bytes), decoded to the same mean on every rank; Philox stream =

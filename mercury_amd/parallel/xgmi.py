@@ -6,18 +6,24 @@ step moves every byte over one of the 7 links).  ``XgmiAllReduce`` instead maps 
 exchange buffer into this process (``hipIpcGetMemHandle`` / ``hipIpcOpenMemHandle``) and
 reduces in two direct passes that pull from all peers at once:
 
-    pack            own gradients -> own exchange buffer (fp32, or bf16 with ``wire_bf16``)
-    barrier         every rank's buffer is filled
-    reduce-scatter  rank r sums chunk r over all W buffers (W-1 remote reads in parallel)
-                    and writes it back into its own buffer
+    pack            own gradients -> own exchange buffer slot (fp32, or bf16 with ``wire_bf16``)
+    barrier         every rank's slot is filled
+    reduce-scatter  rank r sums chunk r over all W slots (W-1 remote reads in parallel)
+                    and writes it back into its own slot
     barrier         every chunk is reduced
     all-gather      chunk p of peer p -> local gradients, for every p
-    barrier         no rank refills its buffer while a peer still reads it
 
-The barriers are stream-ordered (a one-element all-reduce on the framework's own RCCL
-communicator, on the same stream) so nothing waits on the host; tests on one GPU use host
-barriers and emulated peers (``emulated_allreduce``: W local buffers stand for W ranks).
-RCCL stays the engine default (``comm='rccl'``); ``comm='xgmi'`` selects this path.
+The barriers are device-side and stream-ordered (``barrier='device'``, the default): a one-block
+kernel stores this rank's barrier epoch into every peer's flag area (system-scope atomic stores
+through the IPC mapping) and polls its own area until every peer's epoch has arrived, with a
+time limit that raises ``XgmiTimeout`` on the next ``check()`` instead of spinning forever.
+Two buffer slots alternate between consecutive buckets, so no third barrier is needed before a
+slot is refilled: a rank refills slot s for bucket k + 2 only after passing bucket k + 1's
+second barrier, which every peer reaches only after its all-gather of bucket k.  A step with an
+odd bucket count ends with one trailing barrier (``end_step``) so the next step can start on
+slot 0.  ``barrier='rccl'`` (a one-element RCCL all-reduce) and ``'host'`` (tests) remain.
+Tests on one GPU also use emulated peers (``emulated_allreduce``: W local buffers stand for W
+ranks).  RCCL stays the engine default (``comm='rccl'``); ``comm='xgmi'`` selects this path.
 """
 from __future__ import annotations
 
@@ -29,11 +35,18 @@ from ..ops import lib, ptr, stream_ptr
 MAX_RANKS = 8
 
 
+class XgmiTimeout(RuntimeError):
+    pass
+
+
 class XgmiAllReduce(object):
 
-    def __init__(self, capacity, device, group=None, wire_bf16=False, barrier='rccl'):
+    def __init__(self, capacity, device, group=None, wire_bf16=False, barrier='device',
+                 timeout_s=30.0):
         if capacity % 4:
             capacity += 4 - capacity % 4
+        if barrier not in ('device', 'rccl', 'host'):
+            raise ValueError("barrier must be 'device', 'rccl' or 'host'")
         self.capacity = int(capacity)
         self.device = torch.device(device)
         self.group = group
@@ -44,7 +57,10 @@ class XgmiAllReduce(object):
             raise ValueError('xgmi all-reduce: at most %d ranks (one node)' % MAX_RANKS)
         self.bf16 = bool(wire_bf16)
         L = lib()
-        self.buf = L.xgmi_malloc(self.capacity * (2 if self.bf16 else 4))
+        # one allocation per rank: [flag area][slot 0][slot 1], all three IPC-mapped by peers
+        self.flag_bytes = int(L.xgmi_flag_bytes())
+        self.slot_bytes = (self.capacity * (2 if self.bf16 else 4) + 255) // 256 * 256
+        self.buf = L.xgmi_malloc(self.flag_bytes + 2 * self.slot_bytes)
         if not self.buf:
             raise RuntimeError('xgmi all-reduce: exchange buffer allocation failed')
         self._opened = []
@@ -69,24 +85,49 @@ class XgmiAllReduce(object):
         else:
             self.peers = [self.buf]
         self.barrier_kind = barrier
+        self.timeout_s = float(timeout_s)
         self._comm = None
         self._tick = torch.zeros(4, dtype=torch.float32, device=self.device)
+        # device barrier state: this rank's epoch and the timeout error word (bit q: peer q late)
+        self._epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
         if barrier == 'rccl' and self.size > 1:
             from .rccl import RcclComm
             self._comm = RcclComm.shared(group)
 
+    def slot_ptrs(self, slot):
+        return [p + self.flag_bytes + slot * self.slot_bytes for p in self.peers]
+
     def barrier(self):
-        """Every rank reaches this point of its stream (no host wait for 'rccl')."""
+        """Every rank reaches this point of its stream (no host wait for 'device' / 'rccl')."""
         if self.size == 1:
             return
-        if self.barrier_kind == 'rccl':
+        if self.barrier_kind == 'device':
+            lib().xgmi_barrier(self.peers, self.rank, ptr(self._epoch), self.timeout_s,
+                               ptr(self._err), stream_ptr())
+        elif self.barrier_kind == 'rccl':
             self._comm.allreduce(self._tick, avg=False)
         else:
             torch.cuda.current_stream(self.device).synchronize()
             dist.barrier(group=self.group)
 
-    def allreduce(self, t, avg=True):
-        """In-place all-reduce of a contiguous fp32 device tensor (numel % 4 == 0)."""
+    def check(self):
+        """Raise ``XgmiTimeout`` if a device barrier gave up on a peer (host sync)."""
+        e = int(self._err.item())
+        if e:
+            late = [q for q in range(self.size) if e >> q & 1]
+            raise XgmiTimeout('xgmi barrier: peers %s did not arrive within %.1f s'
+                              % (late, self.timeout_s))
+
+    def end_step(self, nbuckets):
+        """After a step's last bucket: an odd bucket count leaves slot 0 last used, so one
+        trailing barrier lets the next step's first bucket refill it."""
+        if nbuckets % 2:
+            self.barrier()
+
+    def allreduce(self, t, avg=True, slot=0):
+        """In-place all-reduce of a contiguous fp32 device tensor (numel % 4 == 0) through
+        exchange slot ``slot`` (alternate 0 / 1 between consecutive calls; see end_step)."""
         if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
             raise ValueError('xgmi all-reduce: contiguous fp32 device tensor expected')
         n = t.numel()
@@ -94,13 +135,12 @@ class XgmiAllReduce(object):
             raise ValueError('xgmi all-reduce: numel %d (capacity %d, multiple of 4)'
                              % (n, self.capacity))
         L, st, bf = lib(), stream_ptr(), int(self.bf16)
-        L.xgmi_pack(ptr(t), self.buf, n, bf, st)
+        bufs = self.slot_ptrs(slot)
+        L.xgmi_pack(ptr(t), bufs[self.rank], n, bf, st)
         self.barrier()
-        L.xgmi_reduce_scatter(self.peers, self.rank, n, bf,
-                              1.0 / self.size if avg else 1.0, st)
+        L.xgmi_reduce_scatter(bufs, self.rank, n, bf, 1.0 / self.size if avg else 1.0, st)
         self.barrier()
-        L.xgmi_all_gather(self.peers, n, bf, ptr(t), st)
-        self.barrier()
+        L.xgmi_all_gather(bufs, n, bf, ptr(t), st)
         return t
 
     def close(self):

@@ -3,8 +3,10 @@
 * emulated peers: W = 2..8 local buffers stand for the W ranks' IPC-mapped exchange buffers;
   every emulated rank's all-gather must equal the fp64 mean of all inputs (fp32 wire) or the
   sum of bf16-rounded inputs rounded once more (bf16 wire);
-* two processes on the same GPU exchange real IPC handles (host barriers over gloo) and run
-  the production ``XgmiAllReduce`` end to end;
+* two processes on the same GPU exchange real IPC handles and run the production
+  ``XgmiAllReduce`` end to end: with host barriers (gloo) and with the device-side flag barriers
+  (system-scope stores into the peer's IPC-mapped flag area), three all-reduces in a row
+  alternating the two exchange slots, then a trailing barrier (odd count);
 * the engine's ``comm='xgmi'`` path at world size 1 (forced buckets) trains like the default.
 """
 import pytest
@@ -35,7 +37,7 @@ def test_emulated_two_shot(W, bf16):
             assert torch.equal(o, outs[0])          # every rank ends with identical values
 
 
-def _ipc_rank(rank, ws, port, q, bf16):
+def _ipc_rank(rank, ws, port, q, bf16, barrier):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
@@ -45,15 +47,24 @@ def _ipc_rank(rank, ws, port, q, bf16):
         torch.cuda.set_device(0)
         from mercury_amd.parallel.xgmi import XgmiAllReduce
         try:
-            x = XgmiAllReduce(1 << 14, 'cuda', wire_bf16=bf16, barrier='host')
+            x = XgmiAllReduce(1 << 14, 'cuda', wire_bf16=bf16, barrier=barrier, timeout_s=20.0)
         except RuntimeError as e:
             q.put(('skip', str(e)))
             return
-        t = torch.full((1 << 14,), float(rank + 1), device='cuda')
-        t[::7] = -2.0 * (rank + 1)
-        x.allreduce(t, avg=True)
+        dist.barrier()
+        out = []
+        ts = []
+        for k in range(3):              # slots 0, 1, 0: slot reuse after the second barrier
+            t = torch.full((1 << 14,), float(rank + 1 + 10 * k), device='cuda')
+            t[::7] = -2.0 * (rank + 1) - k
+            x.allreduce(t, avg=True, slot=k % 2)
+            ts.append(t)
+        x.end_step(3)
         torch.cuda.synchronize()
-        q.put(('ok', float(t[1]), float(t[0]), float(t[2])))
+        x.check()
+        for t in ts:
+            out.append((float(t[1]), float(t[0]), float(t[2])))
+        q.put(('ok', out))
         dist.barrier()
         x.close()
     finally:
@@ -61,7 +72,8 @@ def _ipc_rank(rank, ws, port, q, bf16):
 
 
 @pytest.mark.parametrize('bf16', [False, True])
-def test_two_process_ipc_same_gpu(bf16):
+@pytest.mark.parametrize('barrier', ['host', 'device'])
+def test_two_process_ipc_same_gpu(bf16, barrier):
     import queue
     import time
     import torch.multiprocessing as mp
@@ -69,7 +81,8 @@ def test_two_process_ipc_same_gpu(bf16):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_ipc_rank, args=(r, 2, port, q, bf16)) for r in range(2)]
+    procs = [ctx.Process(target=_ipc_rank, args=(r, 2, port, q, bf16, barrier))
+             for r in range(2)]
     for p in procs:
         p.start()
     res, deadline = [], time.time() + 100
@@ -87,8 +100,10 @@ def test_two_process_ipc_same_gpu(bf16):
     if any(r[0] == 'skip' for r in res):
         pytest.skip('IPC unavailable on this box: ' + [r for r in res if r[0] == 'skip'][0][1])
     for r in res:
-        # mean of 1 and 2 = 1.5; mean of -2 and -4 = -3
-        assert r[1] == 1.5 and r[2] == -3.0 and r[3] == 1.5, r
+        for k, v in enumerate(r[1]):
+            # round k: mean of (1, 2) + 10 k and of (-2 - k, -4 - k)
+            a, b = 1.5 + 10 * k, -3.0 - k
+            assert v == (a, b, a), (k, v)
 
 
 def test_engine_xgmi_world1_matches_default():
