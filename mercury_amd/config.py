@@ -134,7 +134,7 @@ class EngineOptions:
     hconv_persist_waves: int = 8
     # stride-1 3x3 convs with 64 / 128 input channels on the weight-stationary persistent kernel
     # (csrc/wsconv.hip): '1' both batch modes, 'score' / 'train' one, '0' off
-    wsconv: str = 'score'
+    wsconv: str = '0'
     # its grid (0: half the CUs, like the persistent halo kernel beside the train stream)
     wsconv_grid: int = 0
     # per-shape halo plan overrides for sweeps: "N,H,C,K=bm,bn,splits;..." ('none' = igemm)
