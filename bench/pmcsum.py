@@ -28,6 +28,8 @@ def main():
         extra = []
         if v.get('SQ_BUSY_CYCLES'):
             extra.append('mfma_busy/busy(raw)=%.3f' % (v.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / v['SQ_BUSY_CYCLES']))
+        if v.get('SQ_INSTS_MFMA'):
+            extra.append('valu/mfma=%.2f' % (v.get('SQ_INSTS_VALU', 0) / v['SQ_INSTS_MFMA']))
         if v.get('SQ_INSTS_LDS'):
             extra.append('lds_conflict/lds_inst=%.3f' % (v.get('SQ_LDS_BANK_CONFLICT', 0) / v['SQ_INSTS_LDS']))
         print('%-70s n=%-5d %s' % (k, len(disp[k]), ' '.join(extra)))

@@ -49,3 +49,4 @@ void order_check_launch(int* o, int slot, int ref, int mult, int add, int ge, in
   hipLaunchKernelGGL(order_check_kernel, dim3(1), dim3(64), 0, st, o, slot, ref, mult, add, ge,
                      tick, at);
 }
+

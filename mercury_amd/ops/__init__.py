@@ -58,6 +58,30 @@ def stream_ptr():
     return torch.cuda.current_stream().cuda_stream
 
 
+_ROLE_STREAMS = {}
+
+
+def role_stream(device, role):
+    """The process-wide stream of ``role`` ('score', 'comm') on ``device``, shared by every
+    engine of the process.
+
+    HIP runs each stream on one of GPU_MAX_HW_QUEUES hardware queues PER PRIORITY and, past
+    that many streams, makes a new stream share the least-used queue of its priority; two
+    streams on one queue run back to back.  PyTorch hands out its pooled streams round-robin,
+    so an engine whose scoring stream landed on the train (default-priority) stream's queue ran
+    its step serially (1.37 -> 2.1-2.2 ms, bench/queue_probe.py, profiles/r4/queue_probe.json).
+    The role streams are therefore HIGH-priority pool streams -- a different queue pool from
+    the default-priority train stream -- taken once, consecutively (the pool assigns queues
+    round-robin, so score and comm get different queues), and cached.  (A CU-masked stream
+    gets an unpooled queue but measured serial too: 2.26 ms/step.)"""
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _ROLE_STREAMS:
+        d = torch.device('cuda', idx)
+        _ROLE_STREAMS[idx] = {r: torch.cuda.Stream(d, priority=-1) for r in ('score', 'comm')}
+    return _ROLE_STREAMS[idx][role]
+
+
 def ptr(t):
     return 0 if t is None else t.data_ptr()
 
