@@ -434,79 +434,87 @@ constexpr int PDW = 5;              // weight prefetch distance (steps)
 constexpr int PSLOT = PDW + 1;      // weight ring slots
 constexpr int PHP = 4;              // taps of a slice carrying the next slice's halo pieces
 
-// epilogue of one persistent tile: bf16 round, ghost-BN sums (DPP rows -> LDS -> one atomic
-// pair per column), LDS-staged coalesced 16-byte row stores.  VMEM instructions per wave:
-// BM*BN/(8*64*NW) stores + 2 atomics on the waves with 64 w < BN (STATS).
-template <int BM, int BN, int WM, int NW, bool STATS>
-MA_DEV void epi_persist(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)], char* es,
-                        const EpiParams& e, int m0, int n0) {
-  constexpr int NTP = 64 * NW;
-  constexpr int WN = NW / WM, TM = BM / (16 * WM), TN = BN / (16 * WN), LDT = BN + 8;
-  constexpr int CPR = BN / 8, ST = BM * CPR / NTP;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// Lean persistent epilogue (the default): the tile goes out as 8-byte buffer stores straight from
+// the accumulators (lane l: output pixel l & 15, four consecutive channels) -- no LDS staging and
+// no barrier -- and its ghost-BN sums are added to per-lane RUNNING sums.  The block walks a
+// contiguous, N-tile-major range of tiles, so consecutive tiles share (statistics group, channel
+// tile) and the cross-lane / cross-wave reduction and the global atomics (epi_flush) run once per
+// (group, channel tile) the block touches instead of once per tile.  PMC, ResNet-18 scoring pass:
+// the per-tile staged epilogue made the kernel 4.15 VALU per MFMA (profiles/r4/pmc).
+template <int BM, int BN, int WM, int NW>
+MA_DEV void epi_lean(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
+                     float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM / (16 * NW)][4],
+                     bool stats, const EpiParams& e, int m0, int n0) {
+  constexpr int WN = NW / WM, TM = BM / (16 * WM), TN = BN / (16 * WN);
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w / WN, wn = w % WN;
-  float* red = (float*)es;                          // [WM][2][BN] per-wave-row partials
-  bf16* tile = (bf16*)(es + 16 * BN * 4);           // [BM][LDT]
-  bar_lds();                                        // every wave's reads of the area are done
+  const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)e.out, 0, 0x7fffffff, 0x00020000);
+  // lane part of the byte offset (tile-invariant) + the tile origin as the scalar offset
+  const int voff = (((wm * (BM / WM) + (lane & 15)) * e.ldo) + wn * (BN / WN) + 4 * (lane >> 4)) * 2;
+  const int soff = (m0 * e.ldo + n0) * 2;
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int nl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      const int ml = wm * (BM / WM) + tm * 16 + (lane & 15);
+    for (int tn = 0; tn < TN; ++tn) {
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
-      *(bf16x4*)(tile + ml * LDT + nl) = o;
-      if constexpr (STATS) {
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, o), ro,
+                                            voff + (tm * 16 * e.ldo + tn * 16) * 2, soff, 0);
+      if (stats) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float f = bf2f(o[j]);
-          s[j] += f;
-          ss[j] += f * f;
+          rs[tn][j] += f;
+          rss[tn][j] = fmaf(f, f, rss[tn][j]);
         }
       }
     }
-    if constexpr (STATS) {
+}
+
+// the running sums of (group g, channel tile n0) -> e.stats: DPP row sums, one LDS slot per
+// (wave row, channel), one atomic pair per channel.  ``red``: 2 * WM * BN floats of LDS that no
+// wave reads or DMAs into until the next slice's first barrier.  Block-uniform call.
+template <int BM, int BN, int WM, int NW>
+MA_DEV void epi_flush(float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM / (16 * NW)][4],
+                      float* red, const EpiParams& e, int g, int n0) {
+  constexpr int WN = NW / WM, TN = BN / (16 * WN);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s[j] = row16_sum(s[j]);
-        ss[j] = row16_sum(ss[j]);
-      }
-      if ((lane & 15) == 0) {
-        float* r = red + wm * 2 * BN + nl;
-        *(f32x4*)r = f32x4{s[0], s[1], s[2], s[3]};
-        *(f32x4*)(r + BN) = f32x4{ss[0], ss[1], ss[2], ss[3]};
-      }
+  for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rs[tn][j] = row16_sum(rs[tn][j]);
+      rss[tn][j] = row16_sum(rss[tn][j]);
+    }
+  bar_lds();                                        // every wave's reads of the area are done
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      float* r = red + wm * 2 * BN + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+      *(f32x4*)r = f32x4{rs[tn][0], rs[tn][1], rs[tn][2], rs[tn][3]};
+      *(f32x4*)(r + BN) = f32x4{rss[tn][0], rss[tn][1], rss[tn][2], rss[tn][3]};
     }
   }
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rs[tn][j] = rss[tn][j] = 0.f;
   bar_lds();
-  if constexpr (STATS) {
-    if (tid < BN) {                                 // whole waves (BN = 64 or 128)
-      float a = 0.f, b = 0.f;
+  if (tid < BN) {
+    float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int q = 0; q < WM; ++q) {
-        a += red[q * 2 * BN + tid];
-        b += red[q * 2 * BN + BN + tid];
-      }
-      float* dst = MA_SPREAD(e.stats + (size_t)(m0 / e.group_rows) * 2 * e.stats_ld + n0 + tid);
-      atomicAdd(dst, a);
-      atomicAdd(dst + e.stats_ld, b);
+    for (int q = 0; q < WM; ++q) {
+      a += red[q * 2 * BN + tid];
+      b += red[q * 2 * BN + BN + tid];
     }
+    float* dst = MA_SPREAD(e.stats + (size_t)g * 2 * e.stats_ld + n0 + tid);
+    atomicAdd(dst, a);
+    atomicAdd(dst + e.stats_ld, b);
   }
-  // 16-byte buffer stores: the lane's byte offset is tile-invariant, the row step per
-  // iteration and the tile origin go into the scalar offset (no 64-bit address VALU)
-  const int ch = tid % CPR, r0 = tid / CPR;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)e.out, 0, 0x7fffffff, 0x00020000);
-  const int voff = (r0 * e.ldo + ch * 8) * 2;
-#pragma unroll
-  for (int it = 0; it < ST; ++it) {
-    const int rl = r0 + it * (NTP / CPR);
-    const bf16x8 v = *(const bf16x8*)(tile + rl * LDT + ch * 8);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff,
-                                           ((m0 + it * (NTP / CPR)) * e.ldo + n0) * 2, 0);
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // red read before any later DMA lands
 }
 
 // raw buffer resource over [base, base + bytes): an LDS-DMA whose offset is past the end
@@ -579,7 +587,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   static_assert(BI >= 1 && BN % PPX == 0, "whole weight pieces per wave");
   constexpr int SLOT = BN * 128;
   constexpr int R = 3, T = R * R;
-  constexpr int ST = BM * BN / (8 * NTP);
+  constexpr int ST = TM * TN;                       // epilogue stores per wave (epi_lean)
   constexpr int PHI = HRC / PHP;                    // halo pieces per wave on a carrying tap
   static_assert(PHP <= T - 3, "a slice's halo lands >= 2 steps before its first read");
   static_assert(HRC % PHP == 0 && HRC <= HRMAX, "halo piece capacity");
@@ -594,7 +602,11 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   const int PQ = g.P * g.Q;
   const int ntiles = (g.N * PQ / BM) * ntn;
   const int G = gridDim.x, b = blockIdx.x;
-  const int my = b < ntiles ? (ntiles - 1 - b) / G + 1 : 0;
+  // a contiguous range of tiles per block, N-tile-major (consecutive tiles share their channel
+  // tile and, mostly, their statistics group: epi_lean's running sums)
+  const int mtiles = g.N * PQ / BM;
+  const int t0 = (int)((long long)ntiles * b / G);
+  const int my = (int)((long long)ntiles * (b + 1) / G) - t0;
   if (my == 0) return;
   MA_STAMP(0);
 #ifdef MERCURY_STAMPS
@@ -643,10 +655,10 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   }
   unsigned hoff[HRC];                                // byte offsets of the current halo (OOB: pad)
   int hgrp = 0;                                      // ... and its statistics group (MODE 1)
-  const float rntn = 1.f / (float)ntn, rpq = 1.f / (float)PQ, rq = 1.f / (float)g.Q;
+  const float rmt = 1.f / (float)mtiles, rpq = 1.f / (float)PQ, rq = 1.f / (float)g.Q;
   auto tile_of = [&](int k, int& m0, int& n0) {
-    const int t = xcd_tile(k * G + b, ntiles);
-    const int mt = udiv24(t, ntn, rntn), nt = t - mt * ntn;
+    const int t = t0 + k;
+    const int nt = udiv24(t, mtiles, rmt), mt = t - nt * mtiles;
     m0 = mt * BM;
     n0 = nt * BN;
   };
@@ -768,6 +780,11 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rsum[TN][4], rsq[TN][4];                     // running ghost-BN sums (epi_lean)
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rsum[i][j] = rsq[i][j] = 0.f;
 
   // ---- slice cursors.  Slice sigma = (tile k, 64-channel slice cl); the block walks
   // NS = my * nsl of them.  Halo of slice sigma + D (D = NHB - 1) is prefetched during slice
@@ -864,7 +881,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
       mma(0, 0, NM / 2);
       MA_LAP(0, tl);
       if (go) {
-        wait_tap<T, BI, PHI, ST, STATS>(t, hd, hn, epi && t <= PDW - 2, ew);
+        wait_tap<T, BI, PHI, ST, STATS>(t, hd, hn, epi && t <= PDW - 2, false);
       }
       MA_LAP(1, tl);
       if constexpr (MODE == 1) {
@@ -920,7 +937,13 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
       MA_LAP(4, tl);
       if (t == T - 1 && last_sl) {
         // staged in this slice's halo buffer: fully read, refilled only from the next slice on
-        epi_persist<BM, BN, WM, NW, STATS>(acc, smem + buf * HBYTES, e, m0, n0);
+        epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0);
+        if (STATS) {
+          // flush when the next tile of this block starts another (group, channel tile)
+          const int gcur = m0 / e.group_rows;
+          if (!hn || n0n != n0 || m0n / e.group_rows != gcur)
+            epi_flush<BM, BN, WM, NW>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur, n0);
+        }
         MA_LAP(5, tl);
 #pragma unroll
         for (int i = 0; i < TM; ++i)

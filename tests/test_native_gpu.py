@@ -171,8 +171,8 @@ def test_uniform_baseline_keeps_running_stats_sane():
 
 def test_vgg_speech_native_matches_torch():
     """Speech VGG on the native engine: float (spectrogram-like) shard converted once to NHWC
-    bf16, conv+bias+BN+ReLU units with 2x2 max-pools, flatten -> fc1 -> fc2 head on
-    hipBLASLt; gradients vs PyTorch within the bf16 tolerance (conv biases: exactly zero under
+    bf16, conv+bias+BN+ReLU units with 2x2 max-pools, flatten -> fc1 -> fc2 head on the
+    native HIP head kernels (csrc/head.hip mlp_head_*); gradients vs PyTorch within the bf16 tolerance (conv biases: exactly zero under
     train-mode BN, torch returns float noise -- not compared)."""
     import copy
     from mercury_amd import ops

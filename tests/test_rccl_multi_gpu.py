@@ -3,7 +3,9 @@
 Collected for W in {2, 4, every device}: on the 8-GPU driver node that is W = 2, 4 and 8 (the
 whole node, the size the scaling bench runs at); on a one-GPU box every case skips.  Same checks
 as the gloo test of test_native_dp_gpu.py, over the engine's own RCCL communicator and comm
-stream: bucketed AVG all-reduce (captured inside the train graph), replicas bit-identical,
+stream: bucketed AVG all-reduce (each bucket issued on the comm stream right after the train-graph
+segment that finishes it; EngineOptions.capture_comm captures them into one graph), replicas
+bit-identical,
 score all-gather, global EMA; also the direct-xGMI two-shot (experimental) and the ternary wire.
 
 ``test_rccl_collectives_real_gpus`` drives every ``RcclComm`` entry point across the ranks --
