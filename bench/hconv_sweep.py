@@ -37,6 +37,10 @@ def main():
     ap.add_argument('--no-bn', action='store_true')
     ap.add_argument('--reps', type=int, default=12)
     ap.add_argument('--r50', action='store_true', help='ResNet-50/224 3x3 shapes')
+    ap.add_argument('--group', type=int, default=0,
+                    help='ghost-BN group in images (0: 32 above a batch of 32)')
+    ap.add_argument('--miopen', action='store_true',
+                    help='also time F.conv2d (MIOpen, bf16 channels_last) on the same shape')
     args = ap.parse_args()
     import torch
     from mercury_amd import ops
@@ -44,7 +48,9 @@ def main():
     from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes
     dev = 'cuda'
     N = args.batch
-    gimgs = 32 if N > 32 else 0
+    gimgs = args.group or (32 if N > 32 else 0)
+    if gimgs >= N:
+        gimgs = 0
     G = N // gimgs if gimgs else 1
     tot = dict(igemm=0.0, bn_apply=0.0, hconv=0.0, hconv_bn=0.0)
     for (C, K, Hh, R, st) in (R50_SHAPES if args.r50 else SHAPES):
@@ -79,12 +85,34 @@ def main():
         tb = gtime(lambda: ops.bn_apply(y, ystats, gamma, beta, a, N * Hh * Hh, C,
                                         group_rows=(gimgs or N) * Hh * Hh, act='relu'),
                    reps=args.reps)
+        tm = -1.0
+        if args.miopen:
+            import torch.nn.functional as F
+            xt = torch.randn(N, C, Hh, Hh, device=dev, dtype=torch.bfloat16).to(
+                memory_format=torch.channels_last)
+            wt = (torch.randn(K, C, R, R, device=dev) * 0.05).to(torch.bfloat16).to(
+                memory_format=torch.channels_last)
+            for _ in range(3):
+                F.conv2d(xt, wt, stride=st, padding=R // 2)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(args.reps):
+                F.conv2d(xt, wt, stride=st, padding=R // 2)
+            e1.record()
+            torch.cuda.synchronize()
+            tm = e0.elapsed_time(e1) * 1e3 / args.reps
+            del xt, wt
         res = {}
         for c in cands:
             res[c] = gtime(lambda: H.hconv_fwd(y, wk, out, sp, c, stats=stats, slab=slab),
                            reps=args.reps)
         if not res:
-            print(json.dumps(dict(shape=[N, C, K, Hh, R, st], igemm_us=round(ti, 2),
+            print(json.dumps(dict(shape=[N, C, K, Hh, R, st], igemm_plan=list(ip),
+                                  igemm_us=round(ti, 2),
+                                  igemm_tflops=round(sp.flops() / ti / 1e6, 1),
+                                  miopen_us=round(tm, 2),
+                                  miopen_tflops=round(sp.flops() / tm / 1e6, 1) if tm > 0 else None,
                                   bn_apply_us=round(tb, 2), hconv=None)), flush=True)
             continue
         best = min(res, key=res.get)
@@ -94,6 +122,7 @@ def main():
             lambda: H.hconv_fwd(y, wk, out, sp, best, stats=stats, slab=slab, pro=pro),
             reps=args.reps)
         row = dict(shape=[N, C, K, Hh, R, st], igemm_plan=list(ip), igemm_us=round(ti, 2),
+                   miopen_us=round(tm, 2),
                    igemm_tflops=round(sp.flops() / ti / 1e6, 1), bn_apply_us=round(tb, 2),
                    hconv_heur=list(hp) if hp else None,
                    hconv_heur_us=round(res.get(tuple(hp), -1), 2) if hp else None,

@@ -34,8 +34,20 @@ def main():
     ap.add_argument('--streams', type=int, default=12)
     ap.add_argument('--priorities', default='0,-1')
     ap.add_argument('--cycles', type=int, default=20_000_000)
+    ap.add_argument('--dist', action='store_true',
+                    help='initialise a one-rank nccl (RCCL) process group first, as the DP path does')
     a = ap.parse_args()
     torch.cuda.init()
+    if a.dist:
+        import os
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from mercury_amd.parallel import dist as pdist
+        pdist.init_from_env(force=True)
+        import torch.distributed as tdist
+        t = torch.ones(4, device='cuda')
+        tdist.all_reduce(t)
+        torch.cuda.synchronize()
     print('priority_range', torch.cuda.Stream.priority_range(), flush=True)
     torch.cuda._sleep(a.cycles)
     torch.cuda.synchronize()

@@ -12,6 +12,13 @@
 // 32x32x16: 4 k-quarters x 4 MFMAs) = 524,288 FLOP per wave per trip for both shapes.  LDS=1
 // re-reads the A/B fragments from LDS every trip (ds_read_b128 at XOR-swizzled chunks; the
 // LDS image holds random data), LDS=0 keeps them in registers.  bench/mfma_shape_bench.py times the launches.
+//
+// The accumulators are pinned to AGPRs after every k step (empty asm "+a"): unpinned, hipcc
+// chose MFMA destinations that differ from their accumulator inputs and restored the loop-carried
+// mapping with 112-120 v_accvgpr_read/write per trip of the 16x16x32 loop (none in the 32x32x16
+// loop), which made the first version of this benchmark rank the 16x16x32 shape 1.3-1.65x slower
+// for that reason alone.  With the pin, the LDS=1 loops of both shapes are MFMA + ds_read only;
+// the LDS=0 16x16x32 loop still carries the copies (hipcc, loop-invariant operands) -- read LDS=1.
 #include "common.h"
 
 namespace {
@@ -55,12 +62,17 @@ __global__ __launch_bounds__(256, 1) void mfma_loop_kernel(const bf16* __restric
           }
       }
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));   // see header
+      }
     }
     float s = 0.f;
 #pragma unroll
@@ -104,6 +116,10 @@ __global__ __launch_bounds__(256, 1) void mfma_loop_kernel(const bf16* __restric
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kq][i], fb[kq][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+a"(acc[i][j]));
     }
     float s = 0.f;
 #pragma unroll
