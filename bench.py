@@ -18,10 +18,12 @@ real dataset.  Weights are random-init ResNet-18 (11,173,962 params).
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
+import os
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:   # before torch loads HIP: see
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'                # mercury_amd/__init__.py
 
 import argparse
 import json
-import os
 import sys
 import time
 

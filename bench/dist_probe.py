@@ -7,9 +7,11 @@ host time per ``step()`` call (no sync), which separates a host-bound step from 
 
     python bench/dist_probe.py [--steps 200]
 """
+import os
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:   # before torch loads HIP: see
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'                # mercury_amd/__init__.py
 import argparse
 import json
-import os
 import sys
 import time
 

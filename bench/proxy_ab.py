@@ -9,10 +9,12 @@ timing only -- never a result) and the variants are timed in interleaved rounds 
 Prints one JSON line: {variant: [ms/step per round]}.
 """
 from __future__ import annotations
+import os
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:   # before torch loads HIP: see
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'                # mercury_amd/__init__.py
 
 import argparse
 import json
-import os
 import sys
 import time
 

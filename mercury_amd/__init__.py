@@ -7,11 +7,27 @@ ResNet/MobileNet conv/BN stack (MFMA implicit GEMM), RCCL over xGMI for data
 parallelism, HIP graphs for the step.  The public train-loop API mirrors the
 reference ``pytorch_collab.py`` (see ``mercury_amd.trainer.Trainer``).
 """
-import torch  # noqa: F401  (load torch's HIP runtime before our extension)
+import os
 
-from .config import Config
-from .trainer import Trainer
-from . import models, data, importance, parallel, utils
+# HIP runs every stream on one of GPU_MAX_HW_QUEUES hardware queues PER PRIORITY (4 by default)
+# and makes a stream created past that count SHARE the least-used queue; two streams on one queue
+# run back to back.  The engine's step needs its train, scoring and comm streams to overlap, and
+# RCCL and PyTorch's stream pools create streams of their own, so with 4 queues the comm stream
+# of a DP engine landed on a queue with other work and the step ran serially (ResNet-18 forced
+# DP at W=1: 2.25-2.29 ms with 4 or 8 queues, 1.477 with 16, in the process order a DP program
+# uses; bench/dist_probe.py, profiles/r4/ab_hw_queues.json).  Set it before the HIP runtime
+# starts (before `import torch` to be safe): it takes effect only when mercury_amd is imported first
+# (bench.py, collab.py and tests/conftest.py set it first thing; a DP program of your own should
+# export GPU_MAX_HW_QUEUES=16).  Raised, not defaulted: the MI355X boxes export the HIP default
+# (4) explicitly, which a setdefault would keep (profiles/r4/ab_hw_queues.json).
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'
+
+import torch  # noqa: F401,E402  (load torch's HIP runtime before our extension)
+
+from .config import Config  # noqa: E402
+from .trainer import Trainer  # noqa: E402
+from . import models, data, importance, parallel, utils  # noqa: E402
 
 __version__ = '0.1.0'
 

@@ -12,9 +12,11 @@ and keeps its own shard (the reference builds all loaders in the parent and
 forks them).  ``my_run`` keeps the reference signature.
 """
 from __future__ import annotations
+import os
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:   # before torch loads HIP: see
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'                # mercury_amd/__init__.py
 
 import argparse
-import os
 
 import numpy as np
 import torch

@@ -1,4 +1,6 @@
 import os
+if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:   # before torch loads HIP: see
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'                # mercury_amd/__init__.py
 import sys
 
 import pytest

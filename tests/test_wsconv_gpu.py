@@ -72,16 +72,22 @@ def test_wsconv_matches_torch(case):
 
 
 def test_wsconv_engine_plans():
-    """The engine puts ResNet-18's stride-1 64 / 128-channel scoring convs on wsconv by default
-    and the scoring forward still matches ten separate torch forwards (covered end to end by
-    test_native_gpu.test_scoring_ghost_bn_matches_ten_separate_forwards)."""
+    """EngineOptions.wsconv='score' puts ResNet-18's stride-1 64 / 128-channel scoring convs on
+    wsconv (off by default: the scoring-pass A/B measured 1.395 vs 1.3675 ms/step,
+    profiles/r4/ab_wsconv.json), and the default engine has none."""
+    from mercury_amd.config import EngineOptions
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import ResNet18
     import numpy as np
-    torch.manual_seed(0)
-    eng = NativeEngine(ResNet18(10).to(DEV), DEV, 32, 10)
     rng = np.random.RandomState(0)
-    eng.set_shard(rng.randint(0, 256, (640, 32, 32, 3), dtype=np.uint8), rng.randint(0, 10, 640))
+    x = rng.randint(0, 256, (640, 32, 32, 3), dtype=np.uint8)
+    y = rng.randint(0, 10, 640)
+    torch.manual_seed(0)
+    eng = NativeEngine(ResNet18(10).to(DEV), DEV, 32, 10, opts=EngineOptions(wsconv='score'))
+    eng.set_shard(x, y)
     ws = [k[0] for k in eng.score_mode.plan if k[1] == 'wsconv']
     assert len(ws) == 7, ws          # layer1: 4 convs, layer2: 3 stride-1 convs
     assert not any(k[1] == 'wsconv' for k in eng.train_mode.plan)
+    eng0 = NativeEngine(ResNet18(10).to(DEV), DEV, 32, 10, opts=EngineOptions())
+    eng0.set_shard(x, y)
+    assert not any(k[1] == 'wsconv' for k in eng0.score_mode.plan)
