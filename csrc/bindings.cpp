@@ -15,6 +15,15 @@
 #include "kernels.h"
 
 int igemm_read_stamps(unsigned long long* host, int n);
+int conv_bwd_pair_sc_launch(const bf16* dyA, const bf16* wtA, const ConvGeom& gA_in,
+                            const EpiParams& eA_in, int bm, int bn, int splits, const bf16* xA,
+                            const WgradGeom& wgA_in, float* dwA, int wbm, int wbn, int wsplits,
+                            const bf16* dyB, const bf16* wtB, const ConvGeom& gtB,
+                            const EpiParams& eB_in, int HB, int WB, int NB, const bf16* xB,
+                            const WgradGeom& wgB_in, float* dwB, int wsplitsB, hipStream_t st);
+int igemm_dual_launch(const bf16* srcA, const bf16* wtA, const ConvGeom& gA, const EpiParams& eA,
+                      int splitsA, const bf16* srcB, const bf16* wtB, const ConvGeom& gB,
+                      const EpiParams& eB, int splitsB, int bm, int bn, hipStream_t st);
 int hconv_read_stamps(unsigned long long* host, int n);
 void hconv_configure(int grid, int waves);
 int wsconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
@@ -80,6 +89,28 @@ PYBIND11_MODULE(_C, m) {
                 P<float>(bw_sums), bw_inv_count, bw_eps, bw_act};
     igemm_launch(P<const bf16>(src), P<const bf16>(wt), g, e, bm, bn, splits, trans, S(st));
     check_launch("igemm");
+  });
+  // two independent forward convs (plain input, same tile) in one launch; each conv is
+  // (src, wt, out, ldo, stats, stats_ld, group_rows, slab, SH, SW, SC, RP, RQ, R, S, stride, pad,
+  //  Kc, Ncols, M, splits) as int64 values; returns 0 if there is no instantiation
+  m.def("igemm_dual", [](std::vector<int64_t> a, std::vector<int64_t> b, int bm, int bn,
+                         uintptr_t st) {
+    if (a.size() != 21 || b.size() != 21) throw std::invalid_argument("igemm_dual: 21 values each");
+    auto geo = [](const std::vector<int64_t>& v) {
+      return ConvGeom{(int)v[8], (int)v[9], (int)v[10], (int)v[11], (int)v[12], (int)v[13],
+                      (int)v[14], (int)v[15], (int)v[16], (int)v[17], (int)v[18], (int)v[19]};
+    };
+    auto epi = [](const std::vector<int64_t>& v) {
+      return EpiParams{P<bf16>((uintptr_t)v[2]), (int)v[3], nullptr, P<float>((uintptr_t)v[4]),
+                       (int)v[5], (int)v[6], 0, P<float>((uintptr_t)v[7]), nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
+    };
+    const int ok = igemm_dual_launch(P<const bf16>((uintptr_t)a[0]), P<const bf16>((uintptr_t)a[1]),
+                                     geo(a), epi(a), (int)a[20], P<const bf16>((uintptr_t)b[0]),
+                                     P<const bf16>((uintptr_t)b[1]), geo(b), epi(b), (int)b[20], bm,
+                                     bn, S(st));
+    if (ok) check_launch("igemm_dual");
+    return ok;
   });
   // stride-2 dgrad by parity classes (one launch); returns 0 if the conv does not qualify
   m.def("dgrad_s2", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int ldo, int accumulate, int SH,
@@ -204,6 +235,45 @@ PYBIND11_MODULE(_C, m) {
     const int ok = conv_bwd_pair_launch(P<const bf16>(dy), P<const bf16>(wt), g, e, bm, bn, splits,
                                         P<const bf16>(x), wg, P<float>(dw), wbm, wbn, wsplits, S(st));
     if (ok) check_launch("conv_bwd_pair");
+    return ok;
+  });
+  // a block's last-conv pair (conv_bwd_pair's arguments, without the stream) and its shortcut's
+  // stride-2 pair (conv_bwd_pair_s2's, 64 x 64 tiles) in one launch; returns 0 if unsupported
+  m.def("conv_bwd_pair_sc", [](py::tuple a, py::tuple b, uintptr_t st) {
+    if (a.size() != 44 || b.size() != 38) throw std::invalid_argument("conv_bwd_pair_sc: arity");
+    auto U = [](const py::tuple& t, int i) { return t[i].cast<uintptr_t>(); };
+    auto I = [](const py::tuple& t, int i) { return t[i].cast<int>(); };
+    auto F = [](const py::tuple& t, int i) { return t[i].cast<float>(); };
+    // A: dy wt dx ldo accumulate slab SH SW SC RP RQ R Sk stride pad Kc Ncols M bm bn splits
+    //    bw_out bw_y bw_stats bw_y2 bw_stats2 bw_sums bw_inv_count bw_eps bw_act x dw N H W C Pp
+    //    Q K Creal wbm wbn wsplits wslab
+    ConvGeom gA{I(a, 6), I(a, 7), I(a, 8), I(a, 9), I(a, 10), I(a, 11), I(a, 12), I(a, 13),
+                I(a, 14), I(a, 15), I(a, 16), I(a, 17)};
+    EpiParams eA{P<bf16>(U(a, 2)), I(a, 3), nullptr, nullptr, 0, I(a, 17), I(a, 4),
+                 P<float>(U(a, 5)), P<const bf16>(U(a, 21)), P<const bf16>(U(a, 22)),
+                 P<const float>(U(a, 23)), P<const bf16>(U(a, 24)), P<const float>(U(a, 25)),
+                 P<float>(U(a, 26)), F(a, 27), F(a, 28), I(a, 29)};
+    WgradGeom wgA{I(a, 32), I(a, 33), I(a, 34), I(a, 35), I(a, 36), I(a, 37), I(a, 38), I(a, 11),
+                  I(a, 12), I(a, 13), I(a, 14), I(a, 39), nullptr, P<float>(U(a, 43))};
+    // B: dy wt dx ldo accumulate SH SW SC R Sk stride pad Ncols bm bn H W N bw_out bw_y bw_stats
+    //    bw_y2 bw_stats2 bw_sums bw_inv_count bw_eps bw_act x dw C Pp Q K Creal wbm wbn wsplits
+    //    wslab
+    const int HB = I(b, 15), WB = I(b, 16), NB = I(b, 17);
+    ConvGeom gB{I(b, 5), I(b, 6), I(b, 7), HB, WB, I(b, 8), I(b, 9), I(b, 10), I(b, 11),
+                I(b, 8) * I(b, 9) * I(b, 7) / 8, I(b, 12), NB * HB * WB};
+    EpiParams eB{P<bf16>(U(b, 2)), I(b, 3), nullptr, nullptr, 0, NB * HB * WB, I(b, 4), nullptr,
+                 P<const bf16>(U(b, 18)), P<const bf16>(U(b, 19)), P<const float>(U(b, 20)),
+                 P<const bf16>(U(b, 21)), P<const float>(U(b, 22)), P<float>(U(b, 23)), F(b, 24),
+                 F(b, 25), I(b, 26)};
+    WgradGeom wgB{NB, HB, WB, I(b, 29), I(b, 30), I(b, 31), I(b, 32), I(b, 8), I(b, 9), I(b, 10),
+                  I(b, 11), I(b, 33), nullptr, P<float>(U(b, 37))};
+    if (I(b, 13) != 64 || I(b, 14) != 64 || I(b, 34) != 64 || I(b, 35) != 64) return 0;
+    const int ok = conv_bwd_pair_sc_launch(
+        P<const bf16>(U(a, 0)), P<const bf16>(U(a, 1)), gA, eA, I(a, 18), I(a, 19), I(a, 20),
+        P<const bf16>(U(a, 30)), wgA, P<float>(U(a, 31)), I(a, 40), I(a, 41), I(a, 42),
+        P<const bf16>(U(b, 0)), P<const bf16>(U(b, 1)), gB, eB, HB, WB, NB,
+        P<const bf16>(U(b, 27)), wgB, P<float>(U(b, 28)), I(b, 36), S(st));
+    if (ok) check_launch("conv_bwd_pair_sc");
     return ok;
   });
   m.def("comm_unique_id", []() { return py::bytes(comm_unique_id()); });

@@ -485,6 +485,46 @@ void launch_cfg(const bf16* src, const bf16* wt, const ConvGeom& g, EpiParams e,
   launch_main<BM, BN, TRANS>(src, wt, g, e, per, dim3(gx, gy), st);
 }
 
+// ---------------------------------------------------------------- two forward convs, one launch
+// A downsampling block's first conv (3x3, stride 2) and its 1x1 shortcut conv read the same
+// input and are independent: at the train batch each alone fills a fraction of the chip (the
+// shortcut 7-8 us on its own), so one launch runs both -- blocks [0, A.gx * A.gy) are the first
+// conv's (tile, K split), the rest the shortcut's.  Same tile shape for both (one template);
+// each problem keeps its own epilogue (statistics, split-K slab).
+struct IgProb {
+  const bf16* src;
+  const bf16* wt;
+  ConvGeom g;
+  EpiParams e;
+  int per, gx, gy;
+};
+
+template <int BM, int BN, int PF>
+__global__ __launch_bounds__(NT, (nt_occ<BM, BN>())) void igemm_dual_kernel(IgProb A, IgProb B) {
+  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::bytes(2)];
+  const ProParams none{};
+  int b = blockIdx.x;
+  const bool first = b < A.gx * A.gy;              // block-uniform
+  if (!first) b -= A.gx * A.gy;
+  const IgProb& p = first ? A : B;
+  const int bx0 = b % p.gx, by = b / p.gx;
+  const int bx = p.gy == 1 ? xcd_tile(bx0, p.gx) : bx0;
+  igemm_nt_body<BM, BN, false, false, PF>(p.src, p.wt, p.g, p.e, p.per, smem, bx, by, p.gx, p.gy,
+                                          none);
+}
+
+template <int BM, int BN>
+void dual_cfg(IgProb A, IgProb B, hipStream_t st) {
+  const int grid = A.gx * A.gy + B.gx * B.gy;
+  if constexpr (PAIR_PF<BM, BN>() == 2) {
+    if (grid <= 512) {   // the latency-bound rule of launch_main
+      hipLaunchKernelGGL((igemm_dual_kernel<BM, BN, 2>), dim3(grid), dim3(NT), 0, st, A, B);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((igemm_dual_kernel<BM, BN, 1>), dim3(grid), dim3(NT), 0, st, A, B);
+}
+
 // ---------------------------------------------------------------- stride-2 dgrad classes
 // A stride-2 dgrad as a TRANS gather evaluates all R*S taps for every input pixel although only
 // the taps whose parity matches the pixel's reach it (3x3 pad 1: 1, 2, 2 or 4 of 9; 1x1: 1 or
@@ -592,6 +632,74 @@ __global__ __launch_bounds__(NT, 2) void bwd_pair_s2_kernel(const bf16* __restri
       dy, wt, sg.g[c], ec, 1 << 20, smem, d - sg.pre[c], 0, sg.pre[c + 1] - sg.pre[c], 1, none);
 }
 
+// A downsampling block's shortcut backward (1x1 stride 2: class dgrad + wgrad) and the block's
+// last conv's backward (3x3 stride 1: dgrad + wgrad) both start from the block-final BN's
+// backward and are independent: one launch runs the two pairs -- blocks [0, nA) the stride-1
+// pair's wgrad then dgrad tiles, the rest the shortcut's wgrad then parity-class dgrad tiles
+// (64 x 64 class tiles, 64 x 64 wgrad tiles: the train-batch shortcut plans).
+struct PairProb {
+  const bf16* dy;
+  const bf16* wt;
+  ConvGeom g;
+  EpiParams e;
+  int dper, dgx, dgy;
+  const bf16* x;
+  WgradGeom wg;
+  float* dw;
+  int wper, wgx, wgy;
+};
+struct S2PairProb {
+  const bf16* dy;
+  const bf16* wt;
+  S2Geom sg;
+  EpiParams e;
+  const bf16* x;
+  WgradGeom wg;
+  float* dw;
+  int wper, wgx, wgy;
+};
+
+template <int DBM, int DBN, int WBM, int WBN>
+__global__ __launch_bounds__(NT, 2) void bwd_pair_sc_kernel(PairProb A, S2PairProb B) {
+  constexpr int DB = Smem<DBM, DBN>::bytes(2), WB = wgb::WgSmem<WBM, WBN>::BYTES;
+  constexpr int SB = Smem<64, 64>::bytes(2), SWB = wgb::WgSmem<64, 64>::BYTES;
+  constexpr int M1 = DB > WB ? DB : WB, M2 = SB > SWB ? SB : SWB;
+  __shared__ __attribute__((aligned(16))) char smem[M1 > M2 ? M1 : M2];
+  const ProParams none{};
+  int b = blockIdx.x;
+  const int nwA = A.wgx * A.wgy, nA = nwA + A.dgx * A.dgy;
+  if (b < nA) {                                         // block-uniform
+    if (b < nwA) {
+      wgb::wgrad_body<WBM, WBN>(A.dy, A.x, A.wg, A.dw, A.wper, (bf16*)smem, b % A.wgx, b / A.wgx,
+                                A.wgy);
+    } else {
+      const int d = b - nwA;
+      igemm_nt_body<DBM, DBN, true, false, PAIR_PF<DBM, DBN>()>(A.dy, A.wt, A.g, A.e, A.dper, smem,
+                                                                 d % A.dgx, d / A.dgx, A.dgx,
+                                                                 A.dgy, none);
+    }
+    return;
+  }
+  b -= nA;
+  const int nwB = B.wgx * B.wgy;
+  if (b < nwB) {
+    wgb::wgrad_body<64, 64>(B.dy, B.x, B.wg, B.dw, B.wper, (bf16*)smem, b % B.wgx, b / B.wgx, B.wgy);
+    return;
+  }
+  const int d = b - nwB;
+  const int c = (d >= B.sg.pre[1]) + (d >= B.sg.pre[2]) + (d >= B.sg.pre[3]);
+  EpiParams ec = B.e;
+  ec.rm_hc = B.sg.hc[c];
+  ec.rm_wc = B.sg.wc[c];
+  ec.rm_h = B.sg.H;
+  ec.rm_w = B.sg.W;
+  ec.rm_ph = c >> 1;
+  ec.rm_pw = c & 1;
+  igemm_nt_body<64, 64, false, false, PAIR_PF<64, 64>()>(B.dy, B.wt, B.sg.g[c], ec, 1 << 20, smem,
+                                                         d - B.sg.pre[c], 0,
+                                                         B.sg.pre[c + 1] - B.sg.pre[c], 1, none);
+}
+
 template <int DBM, int DBN, int WBM, int WBN>
 void pair_cfg(const bf16* dy, const bf16* wt, const ConvGeom& g, EpiParams e, int splits,
               const bf16* x, WgradGeom wg, float* dw, int wsplits, hipStream_t st) {
@@ -653,6 +761,30 @@ void igemm_launch(const bf16* src, const bf16* wt, const ConvGeom& g_in, const E
   MA_CASE(256, 64)
   MA_CASE(256, 128)
 #undef MA_CASE
+}
+
+// both forward, plain input, the same tile (bm, bn); returns 0 when there is no instantiation
+int igemm_dual_launch(const bf16* srcA, const bf16* wtA, const ConvGeom& gA, const EpiParams& eA,
+                      int splitsA, const bf16* srcB, const bf16* wtB, const ConvGeom& gB,
+                      const EpiParams& eB, int splitsB, int bm, int bn, hipStream_t st) {
+  IgProb A{srcA, wtA, gA, eA, 0, 0, 0}, B{srcB, wtB, gB, eB, 0, 0, 0};
+  A.g.zero = B.g.zero = zero_page();
+  ig_grid(A.g, bm, bn, splitsA, A.gx, A.per, A.gy);
+  ig_grid(B.g, bm, bn, splitsB, B.gx, B.per, B.gy);
+  if (A.gy == 1) A.e.slab = nullptr;
+  if (B.gy == 1) B.e.slab = nullptr;
+  if (A.gy > 1 && B.gy > 1 && A.e.slab == B.e.slab) return 0;   // one slab per split problem
+#define MA_CASE(BM_, BN_)                 \
+  if (bm == BM_ && bn == BN_) {           \
+    dual_cfg<BM_, BN_>(A, B, st);         \
+    return 1;                             \
+  }
+  MA_CASE(64, 128)
+  MA_CASE(128, 128)
+  MA_CASE(128, 64)
+  MA_CASE(64, 64)
+#undef MA_CASE
+  return 0;
 }
 
 // the four class geometries of a stride-2 dgrad (false: the conv does not qualify)
@@ -754,6 +886,55 @@ int conv_bwd_pair_s2_launch(const bf16* dy, const bf16* wt, const ConvGeom& gt,
   MA_W(64, 64, 64, 128)
   MA_W(64, 64, 128, 64)
 #undef MA_W
+  return 0;
+}
+
+// the stride-1 pair (conv_bwd_pair_launch's arguments) and the shortcut's stride-2 pair
+// (conv_bwd_pair_s2_launch's, 64 x 64 tiles) in one launch; 0: no instantiation / not a pair
+int conv_bwd_pair_sc_launch(const bf16* dyA, const bf16* wtA, const ConvGeom& gA_in,
+                            const EpiParams& eA_in, int bm, int bn, int splits, const bf16* xA,
+                            const WgradGeom& wgA_in, float* dwA, int wbm, int wbn,
+                            int wsplits, const bf16* dyB, const bf16* wtB, const ConvGeom& gtB,
+                            const EpiParams& eB_in, int HB, int WB, int NB, const bf16* xB,
+                            const WgradGeom& wgB_in, float* dwB, int wsplitsB,
+                            hipStream_t st) {
+  PairProb A;
+  A.dy = dyA;
+  A.wt = wtA;
+  A.g = gA_in;
+  A.g.zero = zero_page();
+  A.e = eA_in;
+  A.x = xA;
+  A.wg = wgA_in;
+  A.wg.zero = A.g.zero;
+  A.dw = dwA;
+  ig_grid(A.g, bm, bn, splits, A.dgx, A.dper, A.dgy);
+  if (A.dgy == 1) A.e.slab = nullptr;
+  wgb::wg_grid(A.wg, wbm, wbn, wsplits, A.wgx, A.wper, A.wgy);
+  if (A.wgx > wgb::WG_SEM_INTS) A.wg.slab = nullptr;
+  S2PairProb B;
+  if (!s2_geom(gtB, 64, 64, HB, WB, NB, B.sg)) return 0;
+  B.dy = dyB;
+  B.wt = wtB;
+  B.e = eB_in;
+  B.e.slab = nullptr;
+  B.x = xB;
+  B.wg = wgB_in;
+  B.wg.zero = A.g.zero;
+  B.dw = dwB;
+  wgb::wg_grid(B.wg, 64, 64, wsplitsB, B.wgx, B.wper, B.wgy);
+  if (B.wgx > wgb::WG_SEM_INTS) B.wg.slab = nullptr;
+  if (A.wg.slab != nullptr && A.wg.slab == B.wg.slab) return 0;
+  const int grid = A.wgx * A.wgy + A.dgx * A.dgy + B.wgx * B.wgy + B.sg.pre[4];
+#define MA_SC(DBM_, DBN_, WBM_, WBN_)                                                       \
+  if (bm == DBM_ && bn == DBN_ && wbm == WBM_ && wbn == WBN_) {                             \
+    hipLaunchKernelGGL((bwd_pair_sc_kernel<DBM_, DBN_, WBM_, WBN_>), dim3(grid), dim3(NT), 0, st, \
+                       A, B);                                                                \
+    return 1;                                                                                \
+  }
+  MA_SC(64, 64, 64, 64)
+  MA_SC(64, 64, 128, 128)
+#undef MA_SC
   return 0;
 }
 

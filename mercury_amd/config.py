@@ -145,6 +145,12 @@ class EngineOptions:
     pwconv: bool = True
     # first conv on the dense-k stem kernel (stem_bench_v2.jsonl)
     stem: bool = True
+    # a downsampling block's first conv and its shortcut conv in one launch (profiles/r4/
+    # ab_dual_fwd.json)
+    dual_fwd: bool = True
+    # the shortcut's backward pair in one launch with the block's last conv's pair (profiles/r4/
+    # ab_dual_bwd.json)
+    dual_bwd: bool = False
     # intra-block BN + activation folded into the consuming conv's operand load
     fuse_bn_fwd: bool = True
     # block-final BN + identity residual in the next block's pointwise conv load (ab_res_pro.json)

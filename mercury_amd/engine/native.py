@@ -480,6 +480,39 @@ class NativeEngine(object):
                          plan=m.plan[u.name, 'fwd'],
                          bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
 
+    def _igemm_only(self, m, u):
+        """True when _conv_fwd(m, u, ..., pro=None) runs u on the plain igemm kernel."""
+        if u.depthwise or u.b_seg is not None:
+            return False
+        if any((u.name, k) in m.plan for k in ('stem', 'wsconv', 'hconv')):
+            return False
+        return not ((u.name, 'pgemm') in m.plan and pgemm_plain_wins(m.spec[u.name]))
+
+    def _dual_fwd(self, m, u, sc, x, stats_on):
+        """A downsampling block's first conv and its shortcut conv (both read the block input x)
+        in ONE launch (ops.conv_fwd_dual); False when the pair does not qualify."""
+        if not self.opts.dual_fwd or not (self._igemm_only(m, u) and self._igemm_only(m, sc)):
+            return False
+        pa, pb = m.plan[u.name, 'fwd'], m.plan[sc.name, 'fwd']
+        if tuple(pa[:2]) != tuple(pb[:2]):
+            return False
+        slab_b = m.slab
+        if pa[2] > 1 and pb[2] > 1:
+            # the shortcut's split-K partials and tile counters get a slab of their own
+            slab_b = m.buf.get((sc.name, 'slab'))
+            if slab_b is None:
+                if torch.cuda.is_current_stream_capturing():
+                    return False
+                sp = m.spec[sc.name]
+                slab_b = m.buf[sc.name, 'slab'] = torch.zeros(
+                    (slab_bytes(sp.M, sp.K, *pb[:3]) + 3) // 4, dtype=torch.float32,
+                    device=self.device)
+        a = dict(x=x, w=self.w_krsc[u.name], out=m.buf[u.name, 'y'], spec=m.spec[u.name],
+                 stats=m.stats[u.name] if stats_on else None, slab=m.slab, plan=pa)
+        b = dict(x=x, w=self.w_krsc[sc.name], out=m.buf[sc.name, 'y'], spec=m.spec[sc.name],
+                 stats=m.stats[sc.name] if stats_on else None, slab=slab_b, plan=pb)
+        return ops.conv_fwd_dual(a, b)
+
     def _pro_for(self, m, u, nxt):
         """BN-apply of ``u`` folded into the load of its consumer ``nxt`` (csrc/igemm.h
         ProParams), or None when that conv/plan cannot take it.  Train mode also keeps the
@@ -636,12 +669,16 @@ class NativeEngine(object):
             inp = x
             nu = len(blk.units)
             pro = None
+            sc_done = False      # the shortcut conv already ran (with the first conv, one launch)
             for i, u in enumerate(blk.units):
                 y = m.buf[u.name, 'y']
                 st = m.stats[u.name] if stats_on else None
                 if pgp is not None:
                     self._conv_fwd(m, u, pgp['y'], y, st, pro=pgp['pro'])
                     pgp = None
+                elif (i == 0 and pend is None and blk.shortcut is not None and
+                        self._dual_fwd(m, u, blk.shortcut, inp, stats_on)):
+                    sc_done = True
                 elif pend is not None:
                     # BN (+ residual / shortcut BN) + act of the input applied while staging;
                     # ``keep`` materialises x (block input) for the residual, shortcut and
@@ -671,8 +708,9 @@ class NativeEngine(object):
                     res, ru = None, None
                     if blk.shortcut is not None:
                         sc = blk.shortcut
-                        self._conv_fwd(m, sc, x, m.buf[sc.name, 'y'],
-                                       m.stats[sc.name] if stats_on else None)
+                        if not sc_done:
+                            self._conv_fwd(m, sc, x, m.buf[sc.name, 'y'],
+                                           m.stats[sc.name] if stats_on else None)
                         res, ru = m.buf[sc.name, 'y'], sc
                     elif blk.identity:
                         res = x
@@ -822,6 +860,35 @@ class NativeEngine(object):
             return bw is not None
         return False
 
+    def _bwd_sc_ok(self, m, u, sc):
+        """Can the shortcut ``sc``'s backward share one launch with ``u``'s (ops.conv_bwd_sc)?"""
+        if not self.opts.dual_bwd or not self.pair_bwd or u.depthwise or sc.depthwise:
+            return False
+        su, ss = m.spec[u.name], m.spec[sc.name]
+        if su.stride != 1 or su.K % 8 or ss.K % 8 or not ops.conv.dgrad_s2_ok(ss) or ss.N > 32:
+            return False
+        return (tuple(m.plan[u.name, 'dgrad'][:2]) == (64, 64) and
+                tuple(m.plan[u.name, 'wgrad'][:2]) in ((64, 64), (128, 128)) and
+                tuple(m.plan[sc.name, 'wgrad'][:2]) == (64, 64))
+
+    def _conv_bwd_sc(self, m, u, dy, x, dx, bw, sc, xs, dxs):
+        """``u``'s dgrad + wgrad (dx, fused BN-backward sums ``bw``) and the shortcut ``sc``'s
+        (input ``xs``, writes ``dxs``) in one launch; two launches when the pair does not fit.
+        Returns whether ``bw`` was reduced (as _conv_bwd)."""
+        sp = m.spec[u.name]
+        if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
+            bw = None
+        a = dict(dy=dy, wt=self.w_crsk[u.name], dx=dx, x=x, dw=self._pview(u.w_seg, grad=True),
+                 spec=sp, dplan=m.plan[u.name, 'dgrad'], wplan=m.plan[u.name, 'wgrad'],
+                 slab=m.slab, accumulate=False, bw=bw)
+        b = dict(dy=m.buf[sc.name, 'dy'], wt=self.w_crsk[sc.name], dx=dxs, x=xs,
+                 dw=self._pview(sc.w_seg, grad=True), spec=m.spec[sc.name],
+                 wplan=m.plan[sc.name, 'wgrad'], accumulate=False)
+        if ops.conv.conv_bwd_sc(a, b):
+            return bw is not None
+        self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], xs, dxs, accumulate=False)
+        return self._conv_bwd(m, u, dy, x, dx, accumulate=False, bw=bw)
+
     def _bw(self, m, u, out, act, unit2=None):
         """Fused-reduce descriptor for the BN of ``u`` (+ shortcut BN ``unit2``) whose activation
         output is ``out`` -- consumed by conv_dgrad(bw=...)."""
@@ -860,6 +927,11 @@ class NativeEngine(object):
         last = units[-1]
         sc = blk.shortcut
 
+        # the shortcut's backward runs in ONE launch with the last conv's (both start from the
+        # block-final BN's backward; EngineOptions.dual_bwd)
+        merge = (sc is not None and dx is not None and len(units) > 1 and
+                 self._bwd_sc_ok(m, last, sc))
+
         def top():
             dout = m.buf[bi, 'dout']
             out = m.buf[bi, 'out']
@@ -872,7 +944,7 @@ class NativeEngine(object):
             pre = m.prereduced.pop(bi, False) and not blk.pool
             self._bn_bwd(m, last, dout, out, blk.final_act, m.buf[last.name, 'dy'], unit2=sc,
                          dy2=m.buf[sc.name, 'dy'] if sc else None, dz=dz, reduce=not pre)
-            if sc is not None:
+            if sc is not None and not merge:
                 self._conv_bwd(m, sc, m.buf[sc.name, 'dy'], x, dx, accumulate=False)
 
         def unit(i):
@@ -882,8 +954,11 @@ class NativeEngine(object):
             if i > 0:
                 prev = units[i - 1]
                 da = m.buf[prev.name, 'da']
-                fused = self._conv_bwd(m, u, d, inp, da, accumulate=False,
-                                       bw=self._bw(m, prev, m.buf[prev.name, 'a'], prev.act))
+                bw = self._bw(m, prev, m.buf[prev.name, 'a'], prev.act)
+                if merge and u is last:
+                    fused = self._conv_bwd_sc(m, u, d, inp, da, bw, sc, x, dx)
+                else:
+                    fused = self._conv_bwd(m, u, d, inp, da, accumulate=False, bw=bw)
                 self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
                              m.buf[prev.name, 'dy'], reduce=not fused)
             else:

@@ -99,7 +99,7 @@ def _chk(t, dtype, name, numel=None):
         raise ValueError('%s too small: %d < %d' % (name, t.numel(), numel))
 
 
-from .conv import (ConvSpec, conv_fwd, conv_dgrad, conv_wgrad, conv_bwd, pick_tiles, pack_conv_weight,  # noqa: E402
+from .conv import (ConvSpec, conv_fwd, conv_fwd_dual, conv_dgrad, conv_wgrad, conv_bwd, pick_tiles, pack_conv_weight,  # noqa: E402
                    to_nhwc, from_nhwc, pgemm_fwd, pwconv_fwd, stem_fwd)
 from .bn import bn_apply, bn_bwd, BnRunTable, sums_numel, sums_total  # noqa: E402
 from .head import head_fwd, head_bwd, mlp_head_fwd, mlp_head_bwd  # noqa: E402
@@ -110,7 +110,7 @@ from .misc import (quantize, pool2d_fwd, maxpool2d_bwd, dwconv_fwd, dwconv_dgrad
                    dwconv_bwd, dwconv_wgrad_reduce_batch, dwconv_wgrad_blocks,  # noqa: E402
                    nchw_to_nhwc8, tern_pack, tern_unpack)
 
-__all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'pgemm_fwd', 'pwconv_fwd', 'stem_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
+__all__ = ['lib', 'available', 'ConvSpec', 'conv_fwd', 'conv_fwd_dual', 'pgemm_fwd', 'pwconv_fwd', 'stem_fwd', 'conv_dgrad', 'conv_wgrad', 'conv_bwd', 'pick_tiles',
            'pack_conv_weight', 'to_nhwc', 'from_nhwc', 'bn_apply', 'bn_bwd', 'BnRunTable', 'sums_numel', 'sums_total',
            'head_fwd', 'head_bwd', 'mlp_head_fwd', 'mlp_head_bwd', 'pool_build', 'is_sample', 'gather', 'ImportanceTable',
            'FlatOptimizer', 'optimizer_spec', 'quantize', 'tern_pack', 'tern_unpack', 'pool2d_fwd', 'maxpool2d_bwd',

@@ -265,6 +265,35 @@ def conv_fwd(x, w, out, spec: ConvSpec, stats=None, bias=None, slab=None, plan=N
     return out
 
 
+def _dual_args(x, w, out, spec: ConvSpec, stats, slab, plan):
+    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * spec.Cp)
+    _chk(w, torch.bfloat16, 'w', spec.K * spec.R * spec.S * spec.Cp)
+    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
+    _chk(stats, torch.float32, 'stats')
+    bm, bn, splits = plan[:3]
+    if splits > 1:
+        slab = _slab(slab, slab_bytes(spec.M, spec.K, bm, bn, splits), x.device)
+    grp = spec.group_rows if spec.group_rows else spec.M
+    return [ptr(x), ptr(w), ptr(out), spec.K, ptr(stats), spec.K, grp,
+            ptr(slab) if splits > 1 else 0, spec.H, spec.W, spec.Cp, spec.P, spec.Q, spec.R,
+            spec.S, spec.stride, spec.pad, spec.R * spec.S * spec.Cp // 8, spec.K, spec.M, splits]
+
+
+def conv_fwd_dual(a, b):
+    """Two independent forward convs (plain input, no bias) in ONE launch (csrc/igemm.hip
+    igemm_dual_kernel): ``a`` and ``b`` are dicts x=, w=, out=, spec=, stats=, slab=, plan=
+    with the same (bm, bn) tile and distinct slabs when both split K.  Returns False (nothing
+    launched) when the pair has no instantiation; the caller then runs conv_fwd twice."""
+    pa, pb = a['plan'], b['plan']
+    if tuple(pa[:2]) != tuple(pb[:2]):
+        return False
+    if pa[2] > 1 and pb[2] > 1 and a.get('slab') is b.get('slab'):
+        return False
+    va = _dual_args(a['x'], a['w'], a['out'], a['spec'], a.get('stats'), a.get('slab'), pa)
+    vb = _dual_args(b['x'], b['w'], b['out'], b['spec'], b.get('stats'), b.get('slab'), pb)
+    return bool(lib().igemm_dual(va, vb, pa[0], pa[1], stream_ptr()))
+
+
 PGEMM_BM = 256
 
 
@@ -601,6 +630,45 @@ def conv_bwd(dy, wt, dx, x, dw, spec: ConvSpec, dplan=None, wplan=None, slab=Non
         conv_dgrad(dy, wt, dx, spec, slab=slab, plan=(bm, bn, splits), accumulate=accumulate,
                    bw=bw)
     return dx, dw
+
+
+def conv_bwd_sc(a, b):
+    """A block's last-conv backward pair (stride 1: dgrad + wgrad) and its 1x1 stride-2
+    shortcut's pair (parity-class dgrad + wgrad) in ONE launch (csrc/igemm.hip
+    bwd_pair_sc_kernel).  ``a``: dict(dy, wt, dx, x, dw, spec, dplan, wplan, slab, accumulate,
+    bw) as conv_bwd takes; ``b``: the shortcut's dict(dy, wt, dx, x, dw, spec, wplan,
+    accumulate).  Returns False (nothing launched) when the pair is outside the kernel's
+    instantiations; the caller then runs conv_bwd twice."""
+    sa, sb = a['spec'], b['spec']
+    if sa.stride != 1 or sa.K % 8 or not dgrad_s2_ok(sb) or sb.N > 32:
+        return False
+    bm, bn, splits = a.get('dplan') or dgrad_plan(sa)
+    wbm, wbn, wsplits = (a.get('wplan') or wgrad_plan(sa))[:3]
+    sbm, sbn, ssplits = (b.get('wplan') or wgrad_plan(sb))[:3]
+    if (sbm, sbn) != (64, 64):
+        return False
+    for d, sp in ((a, sa), (b, sb)):
+        _chk(d['dy'], torch.bfloat16, 'dy', sp.M * sp.K)
+        _chk(d['wt'], torch.bfloat16, 'wt', sp.Cp * sp.R * sp.S * sp.K)
+        _chk(d['dx'], torch.bfloat16, 'dx', sp.N * sp.H * sp.W * sp.Cp)
+        _chk(d['x'], torch.bfloat16, 'x', sp.N * sp.H * sp.W * sp.Cp)
+        _chk(d['dw'], torch.float32, 'dw', sp.K * sp.R * sp.S * sp.C)
+        _wg_range(sp)
+    Mx = sa.N * sa.H * sa.W
+    slab = a.get('slab')
+    if splits > 1:
+        slab = _slab(slab, slab_bytes(Mx, sa.Cp, bm, bn, splits), a['dy'].device)
+    ta = (ptr(a['dy']), ptr(a['wt']), ptr(a['dx']), sa.Cp, int(a.get('accumulate', False)),
+          ptr(slab) if splits > 1 else 0, sa.P, sa.Q, sa.K, sa.H, sa.W, sa.R, sa.S, sa.stride,
+          sa.pad, sa.R * sa.S * sa.K // 8, sa.Cp, Mx, bm, bn, splits,
+          *_bw_args(a.get('bw'), Mx, sa.Cp), ptr(a['x']), ptr(a['dw']), sa.N, sa.H, sa.W, sa.Cp,
+          sa.P, sa.Q, sa.K, sa.C, wbm, wbn, wsplits, 0)
+    Mb = sb.N * sb.H * sb.W
+    tb = (ptr(b['dy']), ptr(b['wt']), ptr(b['dx']), sb.Cp, int(b.get('accumulate', False)),
+          sb.P, sb.Q, sb.K, sb.R, sb.S, sb.stride, sb.pad, sb.Cp, 64, 64, sb.H, sb.W, sb.N,
+          *_bw_args(None, Mb, sb.Cp), ptr(b['x']), ptr(b['dw']), sb.Cp, sb.P, sb.Q, sb.K, sb.C,
+          sbm, sbn, ssplits, 0)
+    return bool(lib().conv_bwd_pair_sc(ta, tb, stream_ptr()))
 
 
 # ----------------------------------------------------------------------- layout helpers

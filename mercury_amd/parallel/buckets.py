@@ -26,13 +26,26 @@ import torch.distributed as dist
 
 
 def default_bucket_bytes(world_size):
-    """16 MiB buckets at every world size: each bucket costs the native step one more
-    host-replayed graph segment and one RCCL launch (~15 us at W=1, more per-message latency over
-    xGMI rings at W=8), and the scoring stream runs beside the whole backward, so a few large
-    buckets still overlap.  Measured forced-bucket ResNet-18 step at W=1 (profiles/r3/
-    bucket_size_sweep_w1.json): 4 MiB 1.514, 8 MiB 1.485, 16 MiB 1.469, 32 MiB 1.458 ms (no DP
-    1.358).  (32 MiB would leave ResNet-18 two buckets -- the first 34 MB -- too little overlap
-    at W=8.)"""
+    """16 MiB buckets at every world size, from this cost model:
+
+    * a bucket of S bytes all-reduced by RCCL's rings at W ranks moves 2(W-1)/W * S bytes per
+      GPU; on a fully connected 8-GPU MI355X node that traffic is spread over 7 xGMI links
+      (153 GB/s each, spec), so T(S) = alpha + 2(W-1)/W * S / B_eff, with B_eff the achieved
+      per-GPU bus bandwidth (NOT measured here: no multi-GPU node has run this code yet);
+    * every bucket also costs the step a fixed amount: one more graph segment of the train
+      graph plus the comm-stream event edges, measured at W = 1 as +0.065 ms for 3 buckets
+      (~33 us per extra segment, dp_nocomm in profiles/r4/ab_hw_queues.json), plus RCCL's
+      per-collective latency alpha (~10-20 us, assumed);
+    * the backward produces ResNet-18's 44.7 MB of gradients over ~0.5 ms of train-stream time,
+      so everything but the last bucket is hidden if T(S) stays under the backward time left
+      after that bucket closes; the last bucket (stem + layer1, closed when the backward ends)
+      is exposed.
+    With B_eff ~ 300 GB/s (an assumption) at W = 8: the bandwidth term is 78 MB / 300 GB/s =
+    0.26 ms per step in all; 16 MiB gives ResNet-18 3 buckets (18.9 / 17.1 / 8.7 MB): ~0.1 ms
+    of fixed costs and ~70 us exposed for the last one, where 4 MiB buckets (7) would pay ~0.23
+    ms of fixed costs and 64 MiB (1) would expose the whole 0.26 ms.  The W = 1 forced-bucket
+    sweep (profiles/r3/bucket_size_sweep_w1.json: 4 MiB 1.514, 8 MiB 1.485, 16 MiB 1.469, 32
+    MiB 1.458 ms) measures only the fixed costs and agrees with the n * 33 us term."""
     return 16 << 20
 
 
