@@ -561,14 +561,9 @@ int pgemm_launch(const PgemmArgs& g_in, int bn, int grid, hipStream_t st, const 
     if (pro.mode == 2 && !pro.res) return 0;
   }
   const int ntiles = ((g.M + PG_BM - 1) / PG_BM) * ((g.N + bn - 1) / bn);
-  // default grid: one block per CU; MERCURY_PGEMM_GRID caps it (the two-stream step can leave
+  // default grid: one block per CU (the caller's ``grid`` caps it: the two-stream step can leave
   // CUs to the other stream, whose kernels cannot share a CU with a 130-160 KB LDS block)
-  static int gcap = -1;
-  if (gcap < 0) {
-    const char* ev = getenv("MERCURY_PGEMM_GRID");
-    gcap = ev ? atoi(ev) : 0;
-  }
-  if (grid <= 0) grid = gcap > 0 ? gcap : pg_cus();
+  if (grid <= 0) grid = pg_cus();
   if (grid > ntiles) grid = ntiles;
   if (pro.mode) {
     const int n = pro.G * g.K;

@@ -148,6 +148,8 @@ class EngineOptions:
     # a downsampling block's first conv and its shortcut conv in one launch (profiles/r4/
     # ab_dual_fwd.json)
     dual_fwd: bool = True
+    # priority of the scoring / comm streams (ops.role_stream): -1 high, 0 default
+    role_prio: int = -1
     # the shortcut's backward pair in one launch with the block's last conv's pair (profiles/r4/
     # ab_dual_bwd.json)
     dual_bwd: bool = False
@@ -159,6 +161,9 @@ class EngineOptions:
     dw_pro: bool = True
     # depthwise dgrad + wgrad in one launch, wgrad reduces batched (ab_dw_pair.json)
     dw_pair: bool = True
+    # the depthwise conv's output-BN backward applied in that conv's backward dy loads, no
+    # bn_bwd_apply pass (profiles/r4/ab_dw_bn_pro.json)
+    dw_bn_pro: bool = False
     # the classifier head's backward reduces the final BN's backward sums (ab_head_bw.json)
     head_bw: bool = True
     # stride-2 dgrad as four parity classes (ab_dgrad_s2.json)
@@ -167,6 +172,10 @@ class EngineOptions:
     fused_opt: bool = True
     # bucket all-reduces captured inside the train graph (dp_capture_ab.json: off)
     capture_comm: bool = False
+    # ONE train graph with an external event-record node after each bucket's backward segment;
+    # the host issues each bucket's all-reduce on the comm stream behind that event (no graph
+    # segments, no graph-internal comm streams; profiles/r4/ab_comm_events.json)
+    comm_events: bool = False
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes

@@ -107,16 +107,17 @@ class NativeEngine(object):
             if comm in ('rccl', 'xgmi'):
                 from ..parallel.rccl import RcclComm
                 self.comm = RcclComm.shared()
-                self.s_comm = ops.role_stream(self.device, 'comm')
+                self.s_comm = ops.role_stream(self.device, 'comm', self.opts.role_prio)
             elif comm != 'pg':
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
         # the bucket all-reduces captured INSIDE the train graph (event fork onto the comm stream
-        # after each bucket's backward segment, one join before the tail), so a DP step replays
-        # the same three graphs as a one-GPU step.  OFF by default: measured on MI355X at W = 1
-        # (forced buckets, same box, profiles/r3/dp_capture_ab.json) the captured RCCL graph ran
-        # 1.948 ms/step vs 1.598 for the segmented replays (non-DP 1.429) -- RCCL's captured
-        # collectives cost more than the host-issued ones.  MERCURY_CAPTURE_COMM=1 turns it on.
+        # after each bucket's backward segment, one join before the tail).  OFF: at W = 1 (forced
+        # buckets) it ran 2.48-3.91 ms/step vs 1.47 segmented; the trace shows the captured
+        # fork/join replayed on several graph-internal streams, the train chain's kernels spread
+        # over three hardware queues waiting on each other (profiles/r4/
+        # timeline_forced_dp_captured_traced.txt).  EngineOptions.comm_events is the one-graph
+        # alternative without graph-internal streams.
         self.capture_comm = self.s_comm is not None and self.opts.capture_comm
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         if grad_compress not in (None, 'none', 'ternary'):
@@ -143,7 +144,7 @@ class NativeEngine(object):
         # profiles/ab_experiments_r1c.json)
         # the scoring and comm streams each own a hardware queue (ops.role_stream): a pooled
         # stream that lands on the train stream's queue serialises the step (1.37 -> 2.1 ms)
-        self.s_score = ops.role_stream(self.device, 'score')
+        self.s_score = ops.role_stream(self.device, 'score', self.opts.role_prio)
         self.graphs = None
         self.shard = None
         self.primed = False              # a scored pool / drawn batch is pending
@@ -809,11 +810,21 @@ class NativeEngine(object):
         else:
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 
-    def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None):
+    def _dw_pro_ok(self, m, u):
+        """Does depthwise unit ``u``'s backward take its output BN's backward in its dy loads?"""
+        return (self.opts.dw_bn_pro and u.depthwise and self.dw_pair and m.dw_slab is not None and
+                u.act in ('relu', 'relu6', 'none') and u.K == u.C and u.K * 3 * 4 <= 32 * 1024)
+
+    def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None, bwpro=None):
         """Weight gradient, then the data gradient.  ``bw``: the dgrad epilogue also reduces
         the BN-backward sums of the unit feeding ``dx`` (returns True when it did, so the
         caller skips bn_bwd's reduce pass)."""
         sp = m.spec[u.name]
+        if bwpro is not None and not (u.depthwise and dx is not None and m.dw_slab is not None and
+                                      self.dw_pair):
+            # only the depthwise pair launch applies it: materialise dy the usual way instead
+            self._bn_bwd(m, u, bwpro['dout'], bwpro['out'], u.act, dy, reduce=False)
+            bwpro = None
         if (dx is not None and not u.depthwise and self.pair_bwd and sp.K % 8 == 0):
             if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
                 bw = None
@@ -837,8 +848,9 @@ class NativeEngine(object):
             # deferred to one batched launch: at the end of the backward, or (DP) before the
             # bucket all-reduce that carries this weight gradient (train_segments)
             defer = True
-            ops.dwconv_bwd(dy, x, self._pview(u.w_seg), dx, gw, sp.N, sp.H, sp.W, sp.C, sp.P,
-                           sp.Q, sp.stride, sp.pad, region, bw=bw, reduce=not defer)
+            ops.dwconv_bwd(None if bwpro is not None else dy, x, self._pview(u.w_seg), dx, gw,
+                           sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad, region, bw=bw,
+                           reduce=not defer, pro=bwpro)
             if defer:
                 m.dw_pending.append((region, gw, sp.C, nblk))
             return bw is not None
@@ -927,6 +939,7 @@ class NativeEngine(object):
         last = units[-1]
         sc = blk.shortcut
 
+        bwpro = {}   # unit name -> its output BN's backward, applied by its own backward (DwPro)
         # the shortcut's backward runs in ONE launch with the last conv's (both start from the
         # block-final BN's backward; EngineOptions.dual_bwd)
         merge = (sc is not None and dx is not None and len(units) > 1 and
@@ -958,9 +971,19 @@ class NativeEngine(object):
                 if merge and u is last:
                     fused = self._conv_bwd_sc(m, u, d, inp, da, bw, sc, x, dx)
                 else:
-                    fused = self._conv_bwd(m, u, d, inp, da, accumulate=False, bw=bw)
-                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
-                             m.buf[prev.name, 'dy'], reduce=not fused)
+                    fused = self._conv_bwd(m, u, d, inp, da, accumulate=False, bw=bw,
+                                           bwpro=bwpro.pop(u.name, None))
+                if fused and self._dw_pro_ok(m, prev):
+                    # prev is a depthwise conv: its backward applies this BN's backward to the
+                    # gradient as it loads it (DwPro) -- no bn_bwd_apply pass, no dy tensor
+                    bwpro[prev.name] = dict(
+                        dout=da, out=m.buf[prev.name, 'a'], y=m.buf[prev.name, 'y'],
+                        stats=m.stats[prev.name], gamma=self._gamma(prev),
+                        sums=m.buf[prev.name, 'sums'], dgamma=self._gamma(prev, True),
+                        dbeta=self._beta(prev, True), act=prev.act, eps=BN_EPS)
+                else:
+                    self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
+                                 m.buf[prev.name, 'dy'], reduce=not fused)
             else:
                 acc = blk.identity or sc is not None
                 bw = None
@@ -972,7 +995,7 @@ class NativeEngine(object):
                         bw = self._bw(m, pb.units[-1], m.buf[bi - 1, 'out'], pb.final_act,
                                       unit2=pb.shortcut)
                 fused = self._conv_bwd(m, u, d, inp, dx if u.need_dgrad else None,
-                                       accumulate=acc, bw=bw)
+                                       accumulate=acc, bw=bw, bwpro=bwpro.pop(u.name, None))
                 if fused:
                     m.prereduced[bi - 1] = True
 
@@ -1288,6 +1311,22 @@ class NativeEngine(object):
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
         if self.dp and self.capture_comm:
             self.graphs['train_dp'] = self._capture(self._train_dp_body, cap)
+        elif self.s_comm is not None and self.opts.comm_events and len(segs) > 1:
+            # one train graph; an EXTERNAL event record node marks each bucket's gradients
+            # final, so the host-issued all-reduce on the comm stream waits on that node of
+            # this replay (the segmented replays cost ~33 us per extra segment at W = 1)
+            self._bucket_evs = [torch.cuda.Event(external=True) for _, b in segs
+                                if b is not None]
+
+            def body():
+                k = 0
+                for fs, b in segs:
+                    for f in fs:
+                        f()
+                    if b is not None:
+                        self._bucket_evs[k].record()
+                        k += 1
+            self.graphs['train_ev'] = self._capture(body, cap)
         self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
@@ -1345,6 +1384,15 @@ class NativeEngine(object):
             # DP train phase incl. every bucket all-reduce and the comm join: one replay
             graphs['train_dp'].replay()
             segs = []
+        elif graphs and 'train_ev' in graphs and not T.on and not debug:
+            # one train replay; each bucket's all-reduce waits on its event node in it
+            graphs['train_ev'].replay()
+            for si, (_, bucket) in enumerate(segs):
+                if bucket is not None:
+                    works.append(self._reduce_bucket(s0, bucket, nb, si,
+                                                     ev=self._bucket_evs[nb]))
+                    nb += 1
+            segs = []
         for si, (g, bucket) in enumerate(segs):
             if graphs:
                 g.replay()
@@ -1392,8 +1440,9 @@ class NativeEngine(object):
         if rx:
             prof.pop()
 
-    def _reduce_bucket(self, s0, bucket, i, si):
-        """Issue bucket ``i``'s gradient all-reduce behind train segment ``si``."""
+    def _reduce_bucket(self, s0, bucket, i, si, ev=None):
+        """Issue bucket ``i``'s gradient all-reduce behind train segment ``si`` (or behind
+        ``ev``, that segment's event node in the one-graph train replay)."""
         s, e = bucket
         g = self.opt.g[s:e]
         if self.tern is not None:
@@ -1403,8 +1452,9 @@ class NativeEngine(object):
                 self.tern.allreduce(g, self._tern_ctr)
                 return None
             return [dist.all_reduce(g, op=self._avg_op, async_op=True), s, e, False]
-        ev = torch.cuda.Event()
-        ev.record(s0)
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(s0)
         self.s_comm.wait_event(ev)
         with torch.cuda.stream(self.s_comm):
             if self.check_order:

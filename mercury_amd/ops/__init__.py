@@ -61,7 +61,7 @@ def stream_ptr():
 _ROLE_STREAMS = {}
 
 
-def role_stream(device, role):
+def role_stream(device, role, priority=-1):
     """The process-wide stream of ``role`` ('score', 'comm') on ``device``, shared by every
     engine of the process.
 
@@ -73,13 +73,17 @@ def role_stream(device, role):
     The role streams are therefore HIGH-priority pool streams -- a different queue pool from
     the default-priority train stream -- taken once, consecutively (the pool assigns queues
     round-robin, so score and comm get different queues), and cached.  (A CU-masked stream
-    gets an unpooled queue but measured serial too: 2.26 ms/step.)"""
+    gets an unpooled queue but measured serial too: 2.26 ms/step.)  ``priority=0`` takes them from
+    the default-priority pool instead (EngineOptions.role_prio), relying on GPU_MAX_HW_QUEUES
+    being raised for distinct queues."""
     device = torch.device(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    if idx not in _ROLE_STREAMS:
+    key = (idx, int(priority))
+    if key not in _ROLE_STREAMS:
         d = torch.device('cuda', idx)
-        _ROLE_STREAMS[idx] = {r: torch.cuda.Stream(d, priority=-1) for r in ('score', 'comm')}
-    return _ROLE_STREAMS[idx][role]
+        _ROLE_STREAMS[key] = {r: torch.cuda.Stream(d, priority=int(priority))
+                              for r in ('score', 'comm')}
+    return _ROLE_STREAMS[key][role]
 
 
 def ptr(t):

@@ -77,3 +77,46 @@ def test_dual_forward_refuses_shared_split_slab():
     y2 = torch.empty(s2.M * 512, dtype=torch.bfloat16, device=DEV)
     assert not ops.conv_fwd_dual(dict(x=x, w=w1, out=y1, spec=s1, slab=slab, plan=(64, 128, 4)),
                                  dict(x=x, w=w2, out=y2, spec=s2, slab=slab, plan=(64, 128, 2)))
+
+
+@pytest.mark.parametrize('N,H,C,K', [(32, 32, 64, 128), (32, 16, 128, 256), (32, 8, 256, 512)])
+def test_shortcut_backward_merged_matches_separate(N, H, C, K):
+    """ops.conv.conv_bwd_sc: the block's last conv (3x3 stride 1, K -> K at H/2) backward pair
+    and the 1x1 stride-2 shortcut's (C -> K) in one launch vs the two conv_bwd launches."""
+    from mercury_amd import ops
+    from mercury_amd.ops.conv import ConvSpec, conv_bwd_sc, dgrad_plan, wgrad_plan, slab_bytes
+    torch.manual_seed(0)
+    h = H // 2
+    s2 = ConvSpec(N, h, h, K, K, 3, 3, 1, 1)          # last conv of the block
+    ss = ConvSpec(N, H, H, C, K, 1, 1, 2, 0)          # shortcut
+    dy2 = (torch.randn(s2.M, K, device=DEV) * 0.1).to(torch.bfloat16)
+    dys = (torch.randn(ss.M, K, device=DEV) * 0.1).to(torch.bfloat16)
+    x2 = torch.randn(N, h, h, K, device=DEV).to(torch.bfloat16)
+    xs = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    _, wt2 = ops.pack_conv_weight(torch.randn(K, K, 3, 3, device=DEV) * 0.05)
+    _, wts = ops.pack_conv_weight(torch.randn(K, C, 1, 1, device=DEV) * 0.1)
+    dp, wp = dgrad_plan(s2), wgrad_plan(s2)
+    if tuple(dp[:2]) != (64, 64):
+        dp = (64, 64, dp[2])
+    wps = wgrad_plan(ss)
+    if tuple(wps[:2]) != (64, 64):
+        wps = (64, 64, wps[2])
+    slab = torch.zeros(max(1, slab_bytes(N * h * h, K, *dp[:3]) // 4 + 1), device=DEV)
+    res = []
+    for merged in (False, True):
+        dx2 = torch.empty(N * h * h * K, dtype=torch.bfloat16, device=DEV)
+        dxs = torch.empty(N * H * H * C, dtype=torch.bfloat16, device=DEV)
+        dw2 = torch.zeros(K * 9 * K, device=DEV)
+        dws = torch.zeros(K * C, device=DEV)
+        if merged:
+            ok = conv_bwd_sc(dict(dy=dy2, wt=wt2, dx=dx2, x=x2, dw=dw2, spec=s2, dplan=dp, wplan=wp,
+                                  slab=slab),
+                             dict(dy=dys, wt=wts, dx=dxs, x=xs, dw=dws, spec=ss, wplan=wps))
+            assert ok
+        else:
+            ops.conv_bwd(dys, wts, dxs, xs, dws, ss, wplan=wps)
+            ops.conv_bwd(dy2, wt2, dx2, x2, dw2, s2, dplan=dp, wplan=wp, slab=slab)
+        torch.cuda.synchronize()
+        res.append((dx2, dxs, dw2, dws))
+    for a, b in zip(*res):
+        torch.testing.assert_close(b.float(), a.float(), rtol=1e-2, atol=1e-2)

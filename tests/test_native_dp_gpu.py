@@ -192,6 +192,38 @@ def test_native_rccl_buckets_world1():
         dist.destroy_process_group()
 
 
+def test_native_rccl_buckets_comm_events():
+    """EngineOptions.comm_events: ONE train graph with an external event-record node after each
+    bucket's backward segment, the host-issued all-reduces on the comm stream waiting on those
+    nodes.  The stream-order checker proves every all-reduce started after its segment ticked
+    in the same replay (a wait on a stale record would run it early), and training matches the
+    unbucketed engine."""
+    from mercury_amd.config import EngineOptions
+    from mercury_amd.data.datasets import synthetic_arrays
+    x, y = synthetic_arrays(3000, 10, seed=5)
+    _init_nccl_w1()
+    try:
+        base = _engine(x, y)
+        runs = {'rccl': _engine(x, y, force_buckets=True, comm='rccl', check_order=True,
+                                opts=EngineOptions(comm_events=True)),
+                'xgmi': _engine(x, y, force_buckets=True, comm='xgmi',
+                                opts=EngineOptions(comm_events=True))}
+        for r in runs.values():
+            assert 'train_ev' in r.graphs and len(r.bucket_plan()) > 1
+        for _ in range(8):
+            base.step()
+            for r in runs.values():
+                r.step()
+        torch.cuda.synchronize()
+        n, first = runs['rccl'].order_violations()
+        assert n == 0, first
+        for name, r in runs.items():
+            d = float((r.opt.p - base.opt.p).abs().max())
+            assert torch.isfinite(r.opt.p).all() and d < 5e-2, (name, d)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_order_checker_detects_missing_wait():
     """The race detector itself: a tail that runs before the scoring stream ticked is
     reported (slot 0), a correctly ordered one is not."""
