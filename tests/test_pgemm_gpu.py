@@ -49,17 +49,19 @@ def _pw_ok(C, st, resid=False):
     return st == 1 and C <= 128 and not resid
 
 
-@pytest.mark.parametrize('kern', ['pgemm', 'pwconv'])
-@pytest.mark.parametrize('case', CASES)
+def _kern_cases(cases, bn_at, pw_ok):
+    # only the (case, kernel) pairs that apply: pgemm where a tile width is given (bn != 0),
+    # pwconv on its stride-1 narrow-input shapes
+    return [(c, k) for c in cases for k in ('pgemm', 'pwconv')
+            if (k == 'pgemm' and c[bn_at] != 0) or (k == 'pwconv' and pw_ok(c))]
+
+
+@pytest.mark.parametrize('case,kern', _kern_cases(CASES, 7, lambda c: _pw_ok(c[3], c[5])))
 def test_pgemm_matches_torch(case, kern):
     from mercury_amd import ops
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, st, gimgs, bn, grid = case
-    if kern.startswith('pwconv') and not _pw_ok(C, st):
-        pytest.skip('not a pwconv shape')
-    if kern == 'pgemm' and bn == 0:
-        pytest.skip('pwconv-only case')
 
     def run(xn, wk, out, spec, stats=None):
         if kern.startswith('pwconv'):
@@ -107,8 +109,7 @@ PRO_CASES = [
 ]
 
 
-@pytest.mark.parametrize('kern', ['pgemm', 'pwconv'])
-@pytest.mark.parametrize('case', PRO_CASES)
+@pytest.mark.parametrize('case,kern', _kern_cases(PRO_CASES, 6, lambda c: _pw_ok(c[3], 1, c[8])))
 def test_pgemm_input_bn_prologue(case, kern):
     """pgemm(pro=...) == bn_apply (+ residual) pass followed by the plain conv, and == an fp32
     torch reference; the kept activation == bn_apply's output."""
@@ -116,10 +117,6 @@ def test_pgemm_input_bn_prologue(case, kern):
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
     N, H, W, C, K, gimgs, bn, act, resid, ev = case
-    if kern.startswith('pwconv') and not _pw_ok(C, 1, resid):
-        pytest.skip('not a pwconv shape')
-    if kern == 'pgemm' and bn == 0:
-        pytest.skip('pwconv-only case')
     g = torch.Generator(device='cpu').manual_seed(7 + C + K)
     rows = N * H * W
     y = bf(torch.randn(rows, C, generator=g) * 2 + 0.5).to(DEV)
