@@ -63,7 +63,7 @@ def main():
             rows.append(round(pair_ms(s, a.cycles) / one, 2))
         res['priority_%d' % p] = rows
         print('priority %d: pair/one per new stream %s' % (p, rows), flush=True)
-    # the engine's role streams (ops.role_stream: high-priority pool streams)
+    # the engine's role streams (ops.role_stream: default-priority pool streams, cached)
     try:
         import os
         import sys

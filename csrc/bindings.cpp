@@ -345,6 +345,56 @@ PYBIND11_MODULE(_C, m) {
     order_check_launch(P<int>(o), slot, ref, mult, add, ge, tick, at, S(st));
     check_launch("order_check");
   });
+  // one-graph DP train replay (EngineOptions.comm_events): the train segments' captured graphs
+  // chained as child-graph nodes with an event-record NODE after each bucket's segment, in ONE
+  // linear executable graph.  hipGraphLaunch enqueues the record nodes in order, so a
+  // hipStreamWaitEvent issued after the launch waits on that node of this replay.  (torch's
+  // ROCm build refuses torch.cuda.Event(external=True) and HIP refuses hipEventRecordExternal
+  // inside a capture, so the nodes are added explicitly.)
+  m.def("ext_event_create", []() {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("hipEventCreateWithFlags failed");
+    return reinterpret_cast<uintptr_t>(e);
+  });
+  m.def("ext_event_wait", [](uintptr_t st, uintptr_t e) {
+    const hipError_t r = hipStreamWaitEvent(S(st), reinterpret_cast<hipEvent_t>(e), 0);
+    if (r != hipSuccess)
+      throw std::runtime_error(std::string("hipStreamWaitEvent: ") + hipGetErrorString(r));
+  });
+  m.def("ext_event_destroy", [](uintptr_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
+  m.def("graph_chain", [](std::vector<uintptr_t> graphs, std::vector<uintptr_t> events) {
+    if (graphs.size() != events.size()) throw std::runtime_error("graph_chain: one event slot per graph");
+    auto ck = [](hipError_t r, const char* what) {
+      if (r != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(r));
+    };
+    hipGraph_t parent = nullptr;
+    ck(hipGraphCreate(&parent, 0), "hipGraphCreate");
+    hipGraphNode_t prev = nullptr;
+    for (size_t k = 0; k < graphs.size(); ++k) {
+      hipGraphNode_t n = nullptr;
+      ck(hipGraphAddChildGraphNode(&n, parent, prev ? &prev : nullptr, prev ? 1 : 0,
+                                   reinterpret_cast<hipGraph_t>(graphs[k])),
+         "hipGraphAddChildGraphNode");
+      prev = n;
+      if (events[k]) {
+        ck(hipGraphAddEventRecordNode(&n, parent, &prev, 1, reinterpret_cast<hipEvent_t>(events[k])),
+           "hipGraphAddEventRecordNode");
+        prev = n;
+      }
+    }
+    hipGraphExec_t ex = nullptr;
+    ck(hipGraphInstantiate(&ex, parent, nullptr, nullptr, 0), "hipGraphInstantiate");
+    ck(hipGraphDestroy(parent), "hipGraphDestroy");
+    return reinterpret_cast<uintptr_t>(ex);
+  });
+  m.def("graph_launch", [](uintptr_t ex, uintptr_t st) {
+    const hipError_t r = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), S(st));
+    if (r != hipSuccess) throw std::runtime_error(std::string("hipGraphLaunch: ") + hipGetErrorString(r));
+  });
+  m.def("graph_exec_destroy", [](uintptr_t ex) {
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(ex));
+  });
   m.def("igemm_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!igemm_read_stamps(v.data(), n)) v.clear();

@@ -216,37 +216,6 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const int C8 = a.C >> 3;
   constexpr bool two = TWO;
   const float inv = 1.f / (float)a.M;
-  const int T = gridDim.x * NT;
-  const int stride = T - T % C8;
-  const int i0 = blockIdx.x * NT + threadIdx.x;
-  const bool active = i0 < stride;
-  const int c8 = i0 % C8, c = c8 * 8;
-  const int rpi = stride / C8;
-  // the first row's tensors and this thread's per-channel constants are requested BEFORE the
-  // replica fold and its barrier (the compiler does not move loads across it): a launch
-  // exposes one memory latency up front instead of two (the train-batch passes are ~5 us,
-  // latency-bound); the next row's are requested before this row's math
-  bf16x8 d, o, y, y2;
-  auto load = [&](int rw) {
-    const size_t off = (size_t)rw * a.C + c;
-    d = *(const bf16x8*)(a.dout + off);
-    o = *(const bf16x8*)(a.out + off);
-    y = *(const bf16x8*)(a.y + off);
-    if (two) y2 = *(const bf16x8*)(a.y2 + off);
-  };
-  int row = active ? i0 / C8 : a.M;
-  if (row < a.M) load(row);
-  float s1[8], ss1[8], gm[8], s2[8], ss2[8], gm2[8];
-  if (active) {
-    load8(a.stats + c, s1);
-    load8(a.stats + a.C + c, ss1);
-    load8(a.gamma + c, gm);
-    if (two) {
-      load8(a.stats2 + c, s2);
-      load8(a.stats2 + a.C + c, ss2);
-      load8(a.gamma2 + c, gm2);
-    }
-  }
   // fold the SUMS_R replicas once per block (each value SUMS_R loads, shared by every thread)
   for (int j = threadIdx.x; j < (two ? 3 : 2) * a.C; j += NT)
     tot[j] = sum_sums(a.sums, a.C, j / a.C, j % a.C);
@@ -261,22 +230,37 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
       }
     }
   }
-  if (!active) return;
-  float mean[8], rstd[8], sdz[8], sx[8], mean2[8], rstd2[8], sx2[8];
+  const int T = gridDim.x * NT;
+  const int stride = T - T % C8;
+  const int i0 = blockIdx.x * NT + threadIdx.x;
+  if (i0 >= stride) return;
+  const int c8 = i0 % C8, c = c8 * 8;
+  const int rpi = stride / C8;
+  // the next row's tensors are requested before this row's math (and the first row's before
+  // the per-channel constants): one exposed memory latency per launch, not per row
+  bf16x8 d, o, y, y2;
+  auto load = [&](int rw) {
+    const size_t off = (size_t)rw * a.C + c;
+    d = *(const bf16x8*)(a.dout + off);
+    o = *(const bf16x8*)(a.out + off);
+    y = *(const bf16x8*)(a.y + off);
+    if (two) y2 = *(const bf16x8*)(a.y2 + off);
+  };
+  int row = i0 / C8;
+  if (row < a.M) load(row);
+  float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
+  mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
+  load8(a.gamma + c, gm);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    mean[k] = s1[k] * inv;
-    rstd[k] = rsqrtf(fmaxf(ss1[k] * inv - mean[k] * mean[k], 0.f) + a.eps);
     sdz[k] = tot[c + k];
     sx[k] = tot[a.C + c + k];
   }
   if (two) {
+    mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
+    load8(a.gamma2 + c, gm2);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mean2[k] = s2[k] * inv;
-      rstd2[k] = rsqrtf(fmaxf(ss2[k] * inv - mean2[k] * mean2[k], 0.f) + a.eps);
-      sx2[k] = tot[2 * a.C + c + k];
-    }
+    for (int k = 0; k < 8; ++k) sx2[k] = tot[2 * a.C + c + k];
   }
   float k1[8], k2[8], q1[8], k3[8], q2[8];
 #pragma unroll

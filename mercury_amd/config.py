@@ -148,8 +148,10 @@ class EngineOptions:
     # a downsampling block's first conv and its shortcut conv in one launch (profiles/r4/
     # ab_dual_fwd.json)
     dual_fwd: bool = True
-    # priority of the scoring / comm streams (ops.role_stream): -1 high, 0 default
-    role_prio: int = -1
+    # priority of the scoring / comm streams (ops.role_stream): 0 default, -1 high (a
+    # high-priority scoring queue is dispatched ahead of the critical train chain: MobileNetV2
+    # 2.78 vs 2.93 ms, VGG11 3.82 vs 4.10, ResNet-18 neutral, profiles/r4/ab_stream_prio.json)
+    role_prio: int = 0
     # the shortcut's backward pair in one launch with the block's last conv's pair (profiles/r4/
     # ab_dual_bwd.json)
     dual_bwd: bool = True
@@ -175,7 +177,7 @@ class EngineOptions:
     # ONE train graph with an external event-record node after each bucket's backward segment;
     # the host issues each bucket's all-reduce on the comm stream behind that event (no graph
     # segments, no graph-internal comm streams; profiles/r4/ab_comm_events.json)
-    comm_events: bool = False
+    comm_events: bool = True
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes

@@ -146,6 +146,8 @@ class NativeEngine(object):
         # stream that lands on the train stream's queue serialises the step (1.37 -> 2.1 ms)
         self.s_score = ops.role_stream(self.device, 'score', self.opts.role_prio)
         self.graphs = None
+        self._bucket_evs = []            # event-record nodes of the one-graph DP replay
+        self._train_exec = 0             # ... and that graph (hipGraphExec_t)
         self.shard = None
         self.primed = False              # a scored pool / drawn batch is pending
         self.scoring = True
@@ -1270,10 +1272,12 @@ class NativeEngine(object):
         return o[4], dict(slot=o[8], seen=o[9], want=o[10], at=o[11]) if o[4] else None
 
     # ------------------------------------------------------------------ graphs
-    def _capture(self, fn, stream):
-        g = torch.cuda.CUDAGraph()
+    def _capture(self, fn, stream, keep=False):
+        g = torch.cuda.CUDAGraph(keep_graph=keep)
         with torch.cuda.graph(g, stream=stream):
             fn()
+        if keep:
+            g.instantiate()
         return g
 
     def _train_dp_body(self):
@@ -1301,32 +1305,38 @@ class NativeEngine(object):
         torch.cuda.synchronize(self.device)
         cap = torch.cuda.Stream(self.device)
         segs = self.train_segments()
+        comm_ev = (self.dp and not self.capture_comm and self.s_comm is not None
+                   and self.opts.comm_events and len(segs) > 1)
+        if self._train_exec and not comm_ev:
+            ops.lib().graph_exec_destroy(self._train_exec)
+            self._train_exec = 0
         self.graphs = {
             'score': self._capture(self.score_forward if self._split_score else self.score_branch,
                                    cap),
-            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap), b) for fs, b in segs],
+            'train': [(self._capture(lambda fs=fs: [f() for f in fs], cap, keep=comm_ev), b)
+                      for fs, b in segs],
             'tail': self._capture(self.tail, cap),
         }
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
         if self.dp and self.capture_comm:
             self.graphs['train_dp'] = self._capture(self._train_dp_body, cap)
-        elif self.s_comm is not None and self.opts.comm_events and len(segs) > 1:
-            # one train graph; an EXTERNAL event record node marks each bucket's gradients
-            # final, so the host-issued all-reduce on the comm stream waits on that node of
-            # this replay (the segmented replays cost ~33 us per extra segment at W = 1)
-            self._bucket_evs = [torch.cuda.Event(external=True) for _, b in segs
-                                if b is not None]
-
-            def body():
-                k = 0
-                for fs, b in segs:
-                    for f in fs:
-                        f()
-                    if b is not None:
-                        self._bucket_evs[k].record()
-                        k += 1
-            self.graphs['train_ev'] = self._capture(body, cap)
+        elif comm_ev:
+            # ONE linear executable graph: the segment graphs as child nodes, an event-record
+            # node after each bucket's segment; each bucket's host-issued all-reduce on the comm
+            # stream waits on its node of this replay (segmented replays cost ~33 us per extra
+            # segment at W = 1).  The segment graphs stay for the timed (phase-marked) path.
+            L = ops.lib()
+            if not self._bucket_evs:
+                self._bucket_evs = [L.ext_event_create() for _, b in segs if b is not None]
+            evs, k = [], 0
+            for _, b in segs:
+                evs.append(self._bucket_evs[k] if b is not None else 0)
+                k += b is not None
+            if self._train_exec:
+                L.graph_exec_destroy(self._train_exec)
+            self._train_exec = L.graph_chain(
+                [g.raw_cuda_graph() for g, _ in self.graphs['train']], evs)
         self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
@@ -1384,9 +1394,9 @@ class NativeEngine(object):
             # DP train phase incl. every bucket all-reduce and the comm join: one replay
             graphs['train_dp'].replay()
             segs = []
-        elif graphs and 'train_ev' in graphs and not T.on and not debug:
+        elif graphs and self._train_exec and not T.on and not debug:
             # one train replay; each bucket's all-reduce waits on its event node in it
-            graphs['train_ev'].replay()
+            ops.lib().graph_launch(self._train_exec, s0.cuda_stream)
             for si, (_, bucket) in enumerate(segs):
                 if bucket is not None:
                     works.append(self._reduce_bucket(s0, bucket, nb, si,
@@ -1455,7 +1465,9 @@ class NativeEngine(object):
         if ev is None:
             ev = torch.cuda.Event()
             ev.record(s0)
-        self.s_comm.wait_event(ev)
+            self.s_comm.wait_event(ev)
+        else:
+            ops.lib().ext_event_wait(self.s_comm.cuda_stream, ev)
         with torch.cuda.stream(self.s_comm):
             if self.check_order:
                 # the bucket's gradients are final: train segment si has ticked this step

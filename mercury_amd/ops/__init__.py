@@ -61,21 +61,21 @@ def stream_ptr():
 _ROLE_STREAMS = {}
 
 
-def role_stream(device, role, priority=-1):
+def role_stream(device, role, priority=0):
     """The process-wide stream of ``role`` ('score', 'comm') on ``device``, shared by every
     engine of the process.
 
     HIP runs each stream on one of GPU_MAX_HW_QUEUES hardware queues PER PRIORITY and, past
     that many streams, makes a new stream share the least-used queue of its priority; two
     streams on one queue run back to back.  PyTorch hands out its pooled streams round-robin,
-    so an engine whose scoring stream landed on the train (default-priority) stream's queue ran
-    its step serially (1.37 -> 2.1-2.2 ms, bench/queue_probe.py, profiles/r4/queue_probe.json).
-    The role streams are therefore HIGH-priority pool streams -- a different queue pool from
-    the default-priority train stream -- taken once, consecutively (the pool assigns queues
-    round-robin, so score and comm get different queues), and cached.  (A CU-masked stream
-    gets an unpooled queue but measured serial too: 2.26 ms/step.)  ``priority=0`` takes them from
-    the default-priority pool instead (EngineOptions.role_prio), relying on GPU_MAX_HW_QUEUES
-    being raised for distinct queues."""
+    so with the 4 queues the boxes export an engine's scoring stream could land on the train
+    stream's queue and run its step serially (1.37 -> 2.1-2.2 ms, bench/queue_probe.py,
+    profiles/r4/queue_probe.json).  The package raises GPU_MAX_HW_QUEUES to 16 before HIP
+    starts, and the role streams are taken once, consecutively, and cached per process.
+    ``priority`` (EngineOptions.role_prio) 0 takes them from the default-priority pool: a
+    HIGH-priority (-1) scoring queue is dispatched ahead of the critical train chain
+    (MobileNetV2 2.93 vs 2.78 ms, VGG11 4.10 vs 3.82, profiles/r4/ab_stream_prio.json).  (A
+    CU-masked stream gets an unpooled queue but measured serial: 2.26 ms/step.)"""
     device = torch.device(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     key = (idx, int(priority))

@@ -193,9 +193,9 @@ def test_native_rccl_buckets_world1():
 
 
 def test_native_rccl_buckets_comm_events():
-    """EngineOptions.comm_events: ONE train graph with an external event-record node after each
-    bucket's backward segment, the host-issued all-reduces on the comm stream waiting on those
-    nodes.  The stream-order checker proves every all-reduce started after its segment ticked
+    """EngineOptions.comm_events: ONE train graph (the segment graphs as child nodes) with an
+    event-record node after each bucket's backward segment, the host-issued all-reduces on the
+    comm stream waiting on those nodes.  The stream-order checker proves every all-reduce started after its segment ticked
     in the same replay (a wait on a stale record would run it early), and training matches the
     unbucketed engine."""
     from mercury_amd.config import EngineOptions
@@ -209,7 +209,7 @@ def test_native_rccl_buckets_comm_events():
                 'xgmi': _engine(x, y, force_buckets=True, comm='xgmi',
                                 opts=EngineOptions(comm_events=True))}
         for r in runs.values():
-            assert 'train_ev' in r.graphs and len(r.bucket_plan()) > 1
+            assert r._train_exec and len(r.bucket_plan()) > 1
         for _ in range(8):
             base.step()
             for r in runs.values():
