@@ -148,10 +148,13 @@ class EngineOptions:
     # a downsampling block's first conv and its shortcut conv in one launch (profiles/r4/
     # ab_dual_fwd.json)
     dual_fwd: bool = True
-    # priority of the scoring / comm streams (ops.role_stream): 0 default, -1 high (a
-    # high-priority scoring queue is dispatched ahead of the critical train chain: MobileNetV2
-    # 2.78 vs 2.93 ms, VGG11 3.82 vs 4.10, ResNet-18 neutral, profiles/r4/ab_stream_prio.json)
-    role_prio: int = 0
+    # priority of the scoring / comm streams (ops.role_stream): '0' default, '-1' high, 'auto'
+    # = high under DP, default otherwise.  A high-priority scoring queue is dispatched ahead of
+    # the critical train chain (MobileNetV2 2.78 vs 2.93 ms, VGG11 3.82 vs 4.10, ResNet-18
+    # neutral, profiles/r4/ab_stream_prio.json); but once RCCL has created its streams, only
+    # the high-priority pool gives the role streams queues of their own (forced DP 2.79 ms on
+    # default-priority role streams, profiles/r4/session_r4s26/)
+    role_prio: str = 'auto'
     # the shortcut's backward pair in one launch with the block's last conv's pair (profiles/r4/
     # ab_dual_bwd.json)
     dual_bwd: bool = True

@@ -98,6 +98,8 @@ class NativeEngine(object):
         self._avg_op = None
         self.comm = None                 # own RCCL communicator (csrc/comm.hip)
         self.s_comm = None               # ... and the stream its bucket all-reduces run on
+        rp = self.opts.role_prio
+        self._role_prio = (-1 if self.dp else 0) if rp == 'auto' else int(rp)
         self.wire_bf16 = wire_bf16
         if self.dp:
             nccl = dist.get_backend() == 'nccl'
@@ -107,7 +109,7 @@ class NativeEngine(object):
             if comm in ('rccl', 'xgmi'):
                 from ..parallel.rccl import RcclComm
                 self.comm = RcclComm.shared()
-                self.s_comm = ops.role_stream(self.device, 'comm', self.opts.role_prio)
+                self.s_comm = ops.role_stream(self.device, 'comm', self._role_prio)
             elif comm != 'pg':
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
@@ -144,7 +146,7 @@ class NativeEngine(object):
         # profiles/ab_experiments_r1c.json)
         # the scoring and comm streams each own a hardware queue (ops.role_stream): a pooled
         # stream that lands on the train stream's queue serialises the step (1.37 -> 2.1 ms)
-        self.s_score = ops.role_stream(self.device, 'score', self.opts.role_prio)
+        self.s_score = ops.role_stream(self.device, 'score', self._role_prio)
         self.graphs = None
         self._bucket_evs = []            # event-record nodes of the one-graph DP replay
         self._train_exec = 0             # ... and that graph (hipGraphExec_t)
