@@ -13,7 +13,7 @@ slices; for every link to carry a slice worth its latency the bucket should
 be >= 7 x ~512 KB, while fewer, larger buckets amortise the ~10-20 us launch
 latency of each collective.  ``default_bucket_bytes`` documents the size model
 (see its docstring); the W = 8 choice is a model, not a measurement -- no
-multi-GPU node has run this code yet.  At W = 1 the model gives one bucket.
+multi-GPU node has run this code yet.
 
 ``average`` uses ``ReduceOp.AVG`` on RCCL (folds the 1/W into the collective,
 removing the reference's extra divide) and SUM + scale on gloo.  Optional
@@ -26,7 +26,7 @@ import torch.distributed as dist
 
 
 def default_bucket_bytes(world_size):
-    """16 MiB buckets for W >= 2 and ONE bucket at W = 1, from this cost model:
+    """16 MiB buckets at every world size, from this cost model:
 
     * a bucket of S bytes all-reduced by RCCL's rings at W ranks moves 2(W-1)/W * S bytes per
       GPU; on a fully connected 8-GPU MI355X node that traffic is spread over 7 xGMI links
@@ -46,11 +46,10 @@ def default_bucket_bytes(world_size):
     ms of fixed costs and 64 MiB (1) would expose the whole 0.26 ms.  The W = 1 forced-bucket
     sweep (profiles/r3/bucket_size_sweep_w1.json: 4 MiB 1.514, 8 MiB 1.485, 16 MiB 1.469, 32
     MiB 1.458 ms) measures only the fixed costs and agrees with the n * 33 us term.
-    At W = 1 the bandwidth term is zero (RCCL's one-rank all-reduce is a local pass), so nothing
-    is gained by overlapping and every extra bucket is pure fixed cost: one bucket (a forced-DP
-    one-GPU run then pays one graph boundary and one collective)."""
-    if world_size <= 1:
-        return 1 << 60
+    One bucket is NOT better at W = 1 even though the bandwidth term is zero: RCCL's one-rank
+    all-reduce is still a local pass over the bucket, and with one bucket it runs exposed after
+    the backward (forced DP, same box: 1 bucket 1.480 ms, 16 MiB 1.437, non-DP 1.355,
+    profiles/r4/session_r4s27/)."""
     return 16 << 20
 
 
