@@ -177,9 +177,10 @@ class EngineOptions:
     fused_opt: bool = True
     # bucket all-reduces captured inside the train graph (dp_capture_ab.json: off)
     capture_comm: bool = False
-    # ONE train graph with an external event-record node after each bucket's backward segment;
-    # the host issues each bucket's all-reduce on the comm stream behind that event (no graph
-    # segments, no graph-internal comm streams; profiles/r4/ab_comm_events.json)
+    # the DP train phase as ONE executable graph (the segment graphs chained as child nodes) with
+    # an event-record node after each bucket's segment; the host issues each bucket's all-reduce
+    # on the comm stream behind its node (no graph-internal comm streams;
+    # profiles/r4/ab_comm_events.json)
     comm_events: bool = True
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
