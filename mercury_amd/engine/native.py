@@ -1342,6 +1342,21 @@ class NativeEngine(object):
         self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
+    def __del__(self):
+        # the one-graph DP replay's executable graph and its event-record nodes' events are
+        # HIP objects of the extension, not torch's: release them with the engine
+        try:
+            L = ops.lib()
+            if getattr(self, '_train_exec', 0):
+                torch.cuda.synchronize(self.device)     # no replay of it still in flight
+                L.graph_exec_destroy(self._train_exec)
+                self._train_exec = 0
+            for e in getattr(self, '_bucket_evs', ()):
+                L.ext_event_destroy(e)
+            self._bucket_evs = []
+        except Exception:       # interpreter shutdown: the runtime may already be gone
+            pass
+
     def prime(self):
         """Score a first pool and gather the first training batch (reference `train()` entry)."""
         s0 = torch.cuda.current_stream(self.device)

@@ -74,7 +74,9 @@ def role_stream(device, role, priority=0):
     starts, and the role streams are taken once, consecutively, and cached per process.
     ``priority`` (EngineOptions.role_prio) 0 takes them from the default-priority pool: a
     HIGH-priority (-1) scoring queue is dispatched ahead of the critical train chain
-    (MobileNetV2 2.93 vs 2.78 ms, VGG11 4.10 vs 3.82, profiles/r4/ab_stream_prio.json).  (A
+    (MobileNetV2 2.93 vs 2.78 ms, VGG11 4.10 vs 3.82, profiles/r4/ab_stream_prio.json); but
+    once RCCL has created its own streams, default-priority role streams shared queues again
+    (forced DP 2.79 vs 1.44 ms), so DP engines take -1 (EngineOptions.role_prio 'auto').  (A
     CU-masked stream gets an unpooled queue but measured serial: 2.26 ms/step.)"""
     device = torch.device(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
