@@ -36,6 +36,8 @@ from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_p
                         stem_ok, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
+
+_RELEASE = []    # (hipGraphExec_t, [hipEvent_t]) of collected engines, freed by build_graphs
 from ..trainer import Trainer
 from ..utils import profiling as prof
 from ..utils.meters import Accuracy, Average, EMAverage
@@ -1305,6 +1307,12 @@ class NativeEngine(object):
 
     def build_graphs(self):
         torch.cuda.synchronize(self.device)
+        while _RELEASE:                  # graphs / events of collected engines (__del__)
+            ex, evs = _RELEASE.pop()
+            if ex:
+                ops.lib().graph_exec_destroy(ex)
+            for e in evs:
+                ops.lib().ext_event_destroy(e)
         cap = torch.cuda.Stream(self.device)
         segs = self.train_segments()
         comm_ev = (self.dp and not self.capture_comm and self.s_comm is not None
@@ -1343,18 +1351,15 @@ class NativeEngine(object):
         torch.cuda.synchronize(self.device)
 
     def __del__(self):
-        # the one-graph DP replay's executable graph and its event-record nodes' events are
-        # HIP objects of the extension, not torch's: release them with the engine
+        # the one-graph DP replay's executable graph and its events are HIP objects of the
+        # extension, not torch's.  No HIP call here (a collection can run inside another
+        # engine's graph capture): they are queued and released by the next build_graphs,
+        # after its device synchronisation
         try:
-            L = ops.lib()
-            if getattr(self, '_train_exec', 0):
-                torch.cuda.synchronize(self.device)     # no replay of it still in flight
-                L.graph_exec_destroy(self._train_exec)
-                self._train_exec = 0
-            for e in getattr(self, '_bucket_evs', ()):
-                L.ext_event_destroy(e)
-            self._bucket_evs = []
-        except Exception:       # interpreter shutdown: the runtime may already be gone
+            ex, evs = getattr(self, '_train_exec', 0), getattr(self, '_bucket_evs', ())
+            if ex or evs:
+                _RELEASE.append((ex, list(evs)))
+        except Exception:       # interpreter shutdown
             pass
 
     def prime(self):
