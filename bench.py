@@ -102,8 +102,9 @@ def diagnostics(eng, steps, ws):
           (dist.get_world_size() if dist.is_initialized() else 1),
           'buckets_bytes': [4 * (e - s) for s, e in sorted(plan.values(), reverse=True)],
           'wire': 'ternary' if eng.grad_compress else ('bf16' if eng.wire_bf16 else 'fp32'),
-          # bucket all-reduces captured inside the train graph (timed diag steps: segmented)
-          'comm_in_graph': bool(eng.graphs and 'train_dp' in eng.graphs),
+          # one chained train executable with an event node per bucket (timed diag steps:
+          # segmented replays)
+          'comm_events': bool(eng._train_exec),
           'allreduce_ms_per_step': med.get('comm'), 'comm_exposed_ms': med.get('comm_exposed'),
           'overlap_frac': med.get('overlap')}
     torch.cuda.synchronize()
@@ -259,9 +260,9 @@ def main():
     ms = t_is * 1e3 / args.steps
     value = ws * args.batch * args.steps / t_is
     overhead = None
+    eng_u = None
     if not args.no_overhead:
-        del eng
-        torch.cuda.synchronize()
+        eng.close()                      # deterministic teardown before the next engine
         eng_u = make(False)
         t_u = run(eng_u, args.steps, args.warmup, scoring=False)
         overhead = 100.0 * max(0.0, 1.0 - t_u / t_is)
@@ -286,6 +287,9 @@ def main():
         }
         out.update(diag)
         print(json.dumps(out), flush=True)
+    for e in (eng, eng_u):
+        if e is not None:
+            e.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -21,7 +21,7 @@ def gtime(fn, reps=16, iters=7):
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
-    with torch.cuda.graph(g, stream=s):
+    with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
         for _ in range(reps):
             fn()
     g.replay()

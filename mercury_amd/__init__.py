@@ -20,8 +20,27 @@ import os
 # (bench.py, collab.py and tests/conftest.py set it first thing; a DP program of your own should
 # export GPU_MAX_HW_QUEUES=16).  Raised, not defaulted: the MI355X boxes export the HIP default
 # (4) explicitly, which a setdefault would keep (profiles/r4/ab_hw_queues.json).
-if int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:
+# MERCURY_KEEP_HW_QUEUES=1 opts out.  ``HW_QUEUES`` records what happened; NativeEngine warns
+# once when the raise could not take effect (HIP was already initialised at import).
+import sys  # noqa: E402
+import warnings  # noqa: E402
+
+HW_QUEUES = {'before': os.environ.get('GPU_MAX_HW_QUEUES'), 'raised': False, 'effective': True}
+_hip_up = 'torch' in sys.modules and sys.modules['torch'].cuda.is_initialized()
+if os.environ.get('MERCURY_KEEP_HW_QUEUES', '0') != '1' and \
+        int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:
+    before = HW_QUEUES['before']
+    if before not in (None, '', '4'):
+        # (4 is HIP's own default, which the MI355X boxes export explicitly)
+        warnings.warn('mercury_amd: raising GPU_MAX_HW_QUEUES from %s to 16 (the step overlaps '
+                      'three streams; set MERCURY_KEEP_HW_QUEUES=1 to keep yours)' % before,
+                      RuntimeWarning, stacklevel=2)
     os.environ['GPU_MAX_HW_QUEUES'] = '16'
+    HW_QUEUES['raised'] = True
+    HW_QUEUES['effective'] = not _hip_up
+elif int(os.environ.get('GPU_MAX_HW_QUEUES') or 0) < 16:
+    HW_QUEUES['effective'] = False
+del _hip_up
 
 import torch  # noqa: F401,E402  (load torch's HIP runtime before our extension)
 

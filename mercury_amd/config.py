@@ -175,8 +175,6 @@ class EngineOptions:
     dgrad_s2: bool = True
     # one-launch optimizer that also writes the bf16 weight copies (bench_fused_opt_r2h.json)
     fused_opt: bool = True
-    # bucket all-reduces captured inside the train graph (dp_capture_ab.json: off)
-    capture_comm: bool = False
     # the DP train phase as ONE executable graph (the segment graphs chained as child nodes) with
     # an event-record node after each bucket's segment; the host issues each bucket's all-reduce
     # on the comm stream behind its node (no graph-internal comm streams;

@@ -22,8 +22,10 @@ a step costs a handful of host calls.  All buffers are allocated up front.
 """
 from __future__ import annotations
 
+import gc
 import math
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -37,7 +39,44 @@ from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_p
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
 
-_RELEASE = []    # (hipGraphExec_t, [hipEvent_t]) of collected engines, freed by build_graphs
+_RELEASE = []    # (hipGraphExec_t, [hipEvent_t]) of un-closed collected engines
+
+
+_HWQ_WARNED = []
+LIVE = weakref.WeakSet()   # open engines of this process (close_all: test / program teardown)
+
+
+def close_all():
+    """Close every open engine of this process (deterministic teardown)."""
+    for e in list(LIVE):
+        e.close()
+
+
+def _warn_hw_queues():
+    """Once per process: the step's three streams need >= 16 hardware queues, set before HIP
+    starts (mercury_amd/__init__.py); say so when that did not happen."""
+    import warnings
+    from .. import HW_QUEUES
+    if HW_QUEUES['effective'] or _HWQ_WARNED:
+        return
+    _HWQ_WARNED.append(1)
+    warnings.warn('mercury_amd: the HIP runtime started with GPU_MAX_HW_QUEUES=%s (< 16): the '
+                  'scoring / train / comm streams can share hardware queues and the step runs '
+                  'serially (~1.6x slower).  Import mercury_amd (or export GPU_MAX_HW_QUEUES=16) '
+                  'before anything initialises the GPU.' % (HW_QUEUES['before'] or 'default 4'),
+                  RuntimeWarning, stacklevel=3)
+
+
+def _release_queued():
+    """Destroy what collected (never closed) engines queued -- caller has synchronised."""
+    while _RELEASE:
+        ex, evs = _RELEASE.pop()
+        if ex:
+            ops.lib().graph_exec_destroy(ex)
+        for e in evs:
+            ops.lib().ext_event_destroy(e)
+
+
 from ..trainer import Trainer
 from ..utils import profiling as prof
 from ..utils.meters import Accuracy, Average, EMAverage
@@ -76,6 +115,7 @@ class NativeEngine(object):
                  wire_bf16=False, debug=False, check_order=False, grad_compress=None,
                  opts=None):
         ops.lib()
+        _warn_hw_queues()
         from ..config import EngineOptions
         self.opts = opts if opts is not None else EngineOptions.from_env()
         if autotune is not None:
@@ -115,14 +155,6 @@ class NativeEngine(object):
             elif comm != 'pg':
                 raise ValueError("comm must be 'auto', 'rccl', 'xgmi' or 'pg'")
         self.comm_kind = comm if self.dp else None
-        # the bucket all-reduces captured INSIDE the train graph (event fork onto the comm stream
-        # after each bucket's backward segment, one join before the tail).  OFF: at W = 1 (forced
-        # buckets) it ran 2.48-3.91 ms/step vs 1.47 segmented; the trace shows the captured
-        # fork/join replayed on several graph-internal streams, the train chain's kernels spread
-        # over three hardware queues waiting on each other (profiles/r4/
-        # timeline_forced_dp_captured_traced.txt).  EngineOptions.comm_events is the one-graph
-        # alternative without graph-internal streams.
-        self.capture_comm = self.s_comm is not None and self.opts.capture_comm
         self.xgmi = None                 # direct-xGMI two-shot all-reduce (parallel/xgmi.py)
         if grad_compress not in (None, 'none', 'ternary'):
             raise ValueError("grad_compress must be None, 'none' or 'ternary'")
@@ -130,6 +162,9 @@ class NativeEngine(object):
             raise ValueError('grad_compress=ternary is its own wire format (no bf16 / xgmi)')
         self.grad_compress = grad_compress if grad_compress != 'none' else None
         self.tern = None                 # ternary-compressed all-reduce (parallel/compress.py)
+        self._pg_works = []              # ProcessGroup works issued by the last step ('pg')
+        self._closed = False
+        LIVE.add(self)
         self._tern_ctr = 0
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
         self.units = []
@@ -172,8 +207,7 @@ class NativeEngine(object):
         self.dw_pair = o.dw_pair
         self.fuse_bn_halo = o.fuse_bn_halo
         self.persist_bn = o.persist_bn
-        hconv.configure(o)
-        ops.conv.DGRAD_S2 = o.dgrad_s2
+        self._apply_globals()
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
             raise ValueError("sampler must be 'alias', 'cdf' or 'groupwise'")
@@ -191,7 +225,10 @@ class NativeEngine(object):
         self.global_ema = global_ema
         if self.dp and (exchange_scores or global_ema):
             from ..parallel.scores import ScoreExchange
-            self.score_exchange = ScoreExchange(self.P, self.device, force=world_size == 1)
+            # on the engine's own communicator when it has one: stream-ordered on the score
+            # stream, no ProcessGroup work in flight during a step or a capture
+            self.score_exchange = ScoreExchange(self.P, self.device, force=world_size == 1,
+                                                comm=self.comm)
         from .timing import StepTimer
         self.timer = StepTimer(self.device)   # per-phase device timing (off until enabled)
         self.wire = None
@@ -208,6 +245,14 @@ class NativeEngine(object):
             from ..parallel.compress import TernaryAllReduce
             cap = max(e - s_ for s_, e in self.bucket_plan().values())
             self.tern = TernaryAllReduce(cap, self.device, comm=self.comm, seed=seed)
+
+    def _apply_globals(self):
+        """The few EngineOptions that live in process-wide state (the halo-conv launcher's
+        persistent grid / waves / plan overrides, the stride-2 dgrad switch) are re-applied by
+        every phase of THIS engine that reads them -- plan building (set_shard / mode), eager
+        launches and graph capture -- so engines with different options can share a process."""
+        hconv.configure(self.opts)
+        ops.conv.DGRAD_S2 = self.opts.dgrad_s2
 
     # ------------------------------------------------------------------ parameters
     def _final_chw(self):
@@ -309,6 +354,7 @@ class NativeEngine(object):
     def mode(self, name, N=None, group_imgs=0, train=False):
         if name in self.modes:
             return self.modes[name]
+        self._apply_globals()
         m = _Mode(name, N, group_imgs, train)
         dev = self.device
         H, W = self.H, self.W
@@ -1277,45 +1323,52 @@ class NativeEngine(object):
 
     # ------------------------------------------------------------------ graphs
     def _capture(self, fn, stream, keep=False):
+        """Capture ``fn`` on ``stream`` in THREAD-LOCAL mode.  The default global mode forbids
+        "unsafe" HIP calls on every thread of the process while a capture is open; the
+        ProcessGroupNCCL watchdog thread polls its works' events every ~100 ms, and a poll that
+        lands inside a global capture fails and aborts the process from that native thread (the
+        round-4 driver suite abort).  Thread-local mode confines the restriction to this
+        thread; build_graphs additionally quiesces the process before capturing."""
         g = torch.cuda.CUDAGraph(keep_graph=keep)
-        with torch.cuda.graph(g, stream=stream):
+        with torch.cuda.graph(g, stream=stream, capture_error_mode='thread_local'):
             fn()
         if keep:
             g.instantiate()
         return g
 
-    def _train_dp_body(self):
-        """Train fwd + bwd with every bucket's all-reduce forked onto the comm stream right
-        after the backward segment that finishes it, and ONE join at the end -- the whole DP
-        train phase as a single capturable stream program (graph capture follows the event
-        fork / join, so RCCL's kernels become nodes of the train graph)."""
-        s0 = torch.cuda.current_stream(self.device)
-        nb = 0
-        for si, (fs, bucket) in enumerate(self.train_segments()):
-            for f in fs:
-                f()
-            if bucket is not None:
-                self._reduce_bucket(s0, bucket, nb, si)
-                nb += 1
-        if nb:
-            if self.check_order:
-                with torch.cuda.stream(self.s_comm):
-                    self._order(tick=1, at=2)
-            ev = torch.cuda.Event()
-            ev.record(self.s_comm)
-            s0.wait_event(ev)
+    def _quiesce(self):
+        """Nothing of this process may run a HIP call into an open capture: drain the device,
+        the score exchange and every ProcessGroup work this engine issued, then run the
+        collector NOW (finalizers of dead engines -- torch graphs, queued HIP objects -- execute
+        here, not inside a capture) and release what dead engines queued."""
+        torch.cuda.synchronize(self.device)
+        if self.score_exchange is not None:
+            self.score_exchange.wait()
+        works, self._pg_works = self._pg_works, []
+        if works and dist.is_initialized():      # (a destroyed group's works are moot)
+            for w in works:
+                w.wait()
+        torch.cuda.synchronize(self.device)
+        gc.collect()
+        _release_queued()
 
     def build_graphs(self):
-        torch.cuda.synchronize(self.device)
-        while _RELEASE:                  # graphs / events of collected engines (__del__)
-            ex, evs = _RELEASE.pop()
-            if ex:
-                ops.lib().graph_exec_destroy(ex)
-            for e in evs:
-                ops.lib().ext_event_destroy(e)
+        self._check_open()
+        self._quiesce()
+        # no collector pass (and so no finalizer HIP call) while a capture is open
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            self._build_graphs()
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def _build_graphs(self):
+        self._apply_globals()
         cap = torch.cuda.Stream(self.device)
         segs = self.train_segments()
-        comm_ev = (self.dp and not self.capture_comm and self.s_comm is not None
+        comm_ev = (self.dp and self.s_comm is not None
                    and self.opts.comm_events and len(segs) > 1)
         if self._train_exec and not comm_ev:
             ops.lib().graph_exec_destroy(self._train_exec)
@@ -1329,9 +1382,7 @@ class NativeEngine(object):
         }
         if self._split_score:
             self.graphs['score_sample'] = self._capture(self.score_sample, cap)
-        if self.dp and self.capture_comm:
-            self.graphs['train_dp'] = self._capture(self._train_dp_body, cap)
-        elif comm_ev:
+        if comm_ev:
             # ONE linear executable graph: the segment graphs as child nodes, an event-record
             # node after each bucket's segment; each bucket's host-issued all-reduce on the comm
             # stream waits on its node of this replay (segmented replays cost ~33 us per extra
@@ -1350,12 +1401,55 @@ class NativeEngine(object):
         self._graph_scoring = self.scoring
         torch.cuda.synchronize(self.device)
 
+    def close(self):
+        """Release everything this engine owns that is not plain device memory, in a fixed
+        order, now: drain the device and outstanding collectives, drop the torch graphs
+        (their executables and private pools), destroy the chained DP executable and its
+        events, unmap / free the xGMI exchange buffers.  Idempotent; the engine cannot step
+        afterwards.  The shared RCCL communicator is left to ``RcclComm.close`` (other engines
+        of the process use it)."""
+        if getattr(self, '_closed', True):
+            return
+        self._quiesce()
+        if self.graphs:
+            for v in self.graphs.values():
+                for g in (v if isinstance(v, list) else [v]):
+                    g = g[0] if isinstance(g, tuple) else g
+                    g.reset()
+        self.graphs = None
+        L = ops.lib()
+        if self._train_exec:
+            L.graph_exec_destroy(self._train_exec)
+            self._train_exec = 0
+        for e in self._bucket_evs:
+            L.ext_event_destroy(e)
+        self._bucket_evs = []
+        self.score_exchange = None
+        torch.cuda.synchronize(self.device)
+        self._closed = True
+        LIVE.discard(self)
+        x, self.xgmi = self.xgmi, None
+        if x is not None:
+            x.close()                    # collective at W > 1; raises XgmiTimeout last
+
+    def _check_open(self):
+        if self._closed:
+            raise RuntimeError('NativeEngine was closed')
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def __del__(self):
-        # the one-graph DP replay's executable graph and its events are HIP objects of the
-        # extension, not torch's.  No HIP call here (a collection can run inside another
-        # engine's graph capture): they are queued and released by the next build_graphs,
-        # after its device synchronisation
+        # an engine that was never closed: its chained DP executable and events are HIP objects
+        # of the extension, not torch's.  No HIP call here (a collection can run at any point):
+        # they are queued and released by the next _quiesce, after a device synchronisation
         try:
+            if getattr(self, '_closed', True):
+                return
             ex, evs = getattr(self, '_train_exec', 0), getattr(self, '_bucket_evs', ())
             if ex or evs:
                 _RELEASE.append((ex, list(evs)))
@@ -1364,6 +1458,8 @@ class NativeEngine(object):
 
     def prime(self):
         """Score a first pool and gather the first training batch (reference `train()` entry)."""
+        self._check_open()
+        self._apply_globals()
         s0 = torch.cuda.current_stream(self.device)
         self.s_score.wait_stream(s0)
         with torch.cuda.stream(self.s_score):
@@ -1379,8 +1475,12 @@ class NativeEngine(object):
         together; after each bucket segment of the backward the comm stream all-reduces that
         bucket (RCCL, AVG) while later segments and the scoring keep computing; the tail on the
         train stream waits for the scoring stream and the last bucket."""
+        if self._closed:
+            raise RuntimeError('NativeEngine was closed')
         s0 = torch.cuda.current_stream(self.device)
         graphs = self.graphs if self.use_graphs else None
+        if not graphs:
+            self._apply_globals()            # eager launches read the launcher globals
         if graphs and self._graph_scoring != self.scoring:
             raise RuntimeError('scoring was toggled after build_graphs(); rebuild the graphs')
         T = self.timer
@@ -1412,11 +1512,7 @@ class NativeEngine(object):
         works = []
         segs = graphs['train'] if graphs else self.train_segments()
         nb = 0
-        if graphs and 'train_dp' in graphs and not T.on:
-            # DP train phase incl. every bucket all-reduce and the comm join: one replay
-            graphs['train_dp'].replay()
-            segs = []
-        elif graphs and self._train_exec and not T.on and not debug:
+        if graphs and self._train_exec and not T.on and not debug:
             # one train replay; each bucket's all-reduce waits on its event node in it
             ops.lib().graph_launch(self._train_exec, s0.cuda_stream)
             for si, (_, bucket) in enumerate(segs):
@@ -1452,6 +1548,8 @@ class NativeEngine(object):
                 self._finish_work(wk)
                 if self.check_order and wk is works[-1]:
                     self._order(tick=1, at=2)
+        # (kept until the next step / quiesce: drained before any capture)
+        self._pg_works = [wk[0] for wk in works if wk is not None]
         if debug and self.dp:
             self._debug_sync('allreduce')
         if not debug:
@@ -1553,10 +1651,26 @@ class NativeEngine(object):
         self.ema.zero_()
 
     def broadcast_from(self, src=0):
-        dist.broadcast(self.opt.p, src)
+        """Initial replica sync (reference `pytorch_collab.py:84-87` averages parameters only;
+        this broadcasts parameters AND BN running stats from ``src``).  On the engine's own
+        RCCL communicator when it has one (stream-ordered, no ProcessGroup work left in flight
+        for a later graph capture), else the ProcessGroup, drained before returning."""
+        self._check_open()
+        bufs = [self.opt.p]
+        seen = set()
         for u in self.units:
-            dist.broadcast(u.bn.running_mean, src)
-            dist.broadcast(u.bn.running_var, src)
+            for b in (u.bn.running_mean, u.bn.running_var):
+                if id(b) not in seen:
+                    seen.add(id(b))
+                    bufs.append(b)
+        if self.comm is not None:
+            for b in bufs:
+                self.comm.broadcast(b, src)
+        else:
+            works = [dist.broadcast(b, src, async_op=True) for b in bufs]
+            for w in works:
+                w.wait()
+            torch.cuda.synchronize(self.device)
         self.opt.pack_weights()
 
     @torch.no_grad()
@@ -1588,6 +1702,10 @@ class NativeEngine(object):
 
     def read_meters(self):
         b = self.meters.tolist()
+        if self.xgmi is not None:
+            # host-synchronised already: a device barrier that gave up on a peer (its error word)
+            # fails loudly here instead of turning into silent replica divergence
+            self.xgmi.check()
         return {'loss_sum': b[0], 'count': b[1], 'correct': b[2], 'pool_mean': b[3], 'ema': b[4]}
 
 

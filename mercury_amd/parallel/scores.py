@@ -21,10 +21,14 @@ import torch.distributed as dist
 
 class ScoreExchange(object):
 
-    def __init__(self, pool_size, device, group=None, force=False):
+    def __init__(self, pool_size, device, group=None, force=False, comm=None):
         self.group = group
         self.force = force            # run the collective even at world size 1 (path testing)
-        self.ws = dist.get_world_size(group) if dist.is_initialized() else 1
+        # the native engine's RcclComm: the all-gather is then stream-ordered on the caller's
+        # stream (the score stream) and leaves no ProcessGroup work in flight
+        self.comm = comm
+        self.ws = comm.size if comm is not None else (
+            dist.get_world_size(group) if dist.is_initialized() else 1)
         self.local = torch.zeros(pool_size, dtype=torch.float32, device=device)
         self.gathered = torch.zeros(self.ws, pool_size, dtype=torch.float32, device=device)
         self._h = None
@@ -36,6 +40,9 @@ class ScoreExchange(object):
         self.local.copy_(scores.reshape(-1))
         if self.ws == 1 and not self.force:
             self.gathered[0].copy_(self.local)
+            return self
+        if self.comm is not None:
+            self.comm.all_gather(self.gathered.view(-1), self.local)
             return self
         self._h = dist.all_gather_into_tensor(self.gathered.view(-1), self.local, group=self.group,
                                               async_op=True)

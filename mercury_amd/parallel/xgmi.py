@@ -115,7 +115,7 @@ class XgmiAllReduce(object):
         """Raise ``XgmiTimeout`` if a device barrier gave up on a peer (host sync)."""
         e = int(self._err.item())
         if e:
-            late = [q for q in range(self.size) if e >> q & 1]
+            late = [q for q in range(32) if e >> q & 1]
             raise XgmiTimeout('xgmi barrier: peers %s did not arrive within %.1f s'
                               % (late, self.timeout_s))
 
@@ -143,15 +143,33 @@ class XgmiAllReduce(object):
         L.xgmi_all_gather(bufs, n, bf, ptr(t), st)
         return t
 
-    def close(self):
+    def close(self, sync_peers=True):
+        """Collective at W > 1 (every rank calls it): one last barrier so no peer is still
+        reading this rank's slots, then unmap the peers' buffers and free our own
+        (``sync_peers=False``: the caller has synchronised the ranks on the host already).
+        Raises ``XgmiTimeout`` if a barrier of this exchange ever gave up on a peer."""
         L = lib()
+        if not self.buf:
+            return
+        if sync_peers and self.size > 1:
+            if self.barrier_kind == 'device':
+                self.barrier()
+            torch.cuda.synchronize(self.device)
+            if self._err.item():
+                # a peer is gone or desynchronised: fall back to the host barrier
+                dist.barrier(group=self.group)
         torch.cuda.synchronize(self.device)
+        err = int(self._err.item())
         for p in self._opened:
             L.xgmi_ipc_close(p)
         self._opened = []
         if self.buf:
             L.xgmi_free(self.buf)
             self.buf = 0
+        if err:
+            late = [q for q in range(32) if err >> q & 1]
+            raise XgmiTimeout('xgmi barrier: peers %s did not arrive within %.1f s'
+                              % (late, self.timeout_s))
 
 
 def emulated_allreduce(tensors, avg=True, wire_bf16=False):

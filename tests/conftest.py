@@ -24,3 +24,22 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if 'gpu' in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _engine_teardown(request):
+    """GPU tests: every engine a test built is closed when it ends, then the collector runs and
+    the device drains -- no graph, event or exchange buffer of one test is released by a
+    garbage-collection pass inside a later test's graph capture."""
+    yield
+    if 'gpu' not in request.keywords:
+        return
+    import gc
+    import torch
+    if not torch.cuda.is_available():
+        return
+    mod = sys.modules.get('mercury_amd.engine.native')
+    if mod is not None:
+        mod.close_all()
+    gc.collect()
+    torch.cuda.synchronize()

@@ -130,13 +130,12 @@ def _engine(x, y, **kw):
 def test_native_rccl_buckets_world1():
     """The RCCL data-parallel path executed on one GPU: backend nccl at W = 1 with the bucket
     all-reduces forced on.  Checks: the native communicator's AVG all-reduces run on the comm
-    stream between graph replays (device timing sees every bucket), ProcessGroupNCCL's async
+    stream behind their segments (device timing sees every bucket), ProcessGroupNCCL's async
     AVG path too, the stream-order race detector stays clean, the score all-gather works, and
     training matches the unbucketed engine (AVG over one rank is the identity)."""
     from mercury_amd.data.datasets import synthetic_arrays
     x, y = synthetic_arrays(3000, 10, seed=5)
     _init_nccl_w1()
-    os.environ['MERCURY_ENGINE_OPTS'] = 'capture_comm=1'
     try:
         base = _engine(x, y)
         runs = {'rccl': _engine(x, y, force_buckets=True, comm='rccl', check_order=True,
@@ -147,11 +146,11 @@ def test_native_rccl_buckets_world1():
                 'tern': _engine(x, y, force_buckets=True, comm='rccl', grad_compress='ternary')}
         e = runs['rccl']
         assert e.comm is not None and e.comm.size == 1 and len(e.bucket_plan()) > 1
-        # capture_comm=1 (EngineOptions, set by the test): the untimed DP step is ONE captured train
-        # graph with the all-reduces inside it
+        # the score all-gather rides the engine's own communicator: no ProcessGroup work
+        assert e.score_exchange.comm is e.comm
         for name in ('rccl', 'bf16', 'xgmi', 'tern'):
-            assert 'train_dp' in runs[name].graphs, name
-        assert 'train_dp' not in runs['pg'].graphs
+            assert runs[name]._train_exec, name          # one chained train executable
+        assert not runs['pg']._train_exec
         for _ in range(6):
             base.step()
             for r in runs.values():
@@ -187,8 +186,42 @@ def test_native_rccl_buckets_world1():
         e.comm.allreduce(gg, avg=True)
         torch.cuda.synchronize()
         assert torch.equal(gg, ref)
+        for r in list(runs.values()) + [tern, base]:
+            r.close()
     finally:
-        os.environ.pop('MERCURY_ENGINE_OPTS', None)
+        dist.destroy_process_group()
+
+
+def test_capture_beside_outstanding_processgroup_work():
+    """Regression for the round-4 driver abort (SIGABRT on a native thread while engines were
+    being captured after a 'pg' engine had left ProcessGroupNCCL works behind).  The
+    ProcessGroupNCCL watchdog thread polls its works' events; a global-mode capture forbids that
+    poll process-wide and the watchdog aborts.  Engines capture thread-locally after quiescing,
+    so captures with PG works still listed -- the pg engine's buckets plus a batch of large async
+    all-reduces issued by the test itself -- must be harmless, repeatedly."""
+    from mercury_amd.data.datasets import synthetic_arrays
+    x, y = synthetic_arrays(3000, 10, seed=5)
+    _init_nccl_w1()
+    try:
+        pg = _engine(x, y, force_buckets=True, comm='pg')
+        others = []
+        for k in range(3):
+            pg.step()                                  # bucket works in the watchdog's list
+            big = torch.randn(1 << 22, device='cuda')
+            works = [dist.all_reduce(big, async_op=True) for _ in range(16)]
+            others.append(_engine(x, y, force_buckets=True, comm='rccl'))
+            for w in works:
+                w.wait()
+        for _ in range(3):
+            pg.step()
+            for o in others:
+                o.step()
+        torch.cuda.synchronize()
+        for o in others + [pg]:
+            assert torch.isfinite(o.opt.p).all() and np.isfinite(o.read_meters()['loss_sum'])
+        for o in others + [pg]:
+            o.close()
+    finally:
         dist.destroy_process_group()
 
 

@@ -4,8 +4,8 @@ Collected for W in {2, 4, every device}: on the 8-GPU driver node that is W = 2,
 whole node, the size the scaling bench runs at); on a one-GPU box every case skips.  Same checks
 as the gloo test of test_native_dp_gpu.py, over the engine's own RCCL communicator and comm
 stream: bucketed AVG all-reduce (each bucket issued on the comm stream right after the train-graph
-segment that finishes it; EngineOptions.capture_comm captures them into one graph), replicas
-bit-identical,
+segment that finishes it, behind that segment's event node of the chained train executable),
+replicas bit-identical,
 score all-gather, global EMA; also the direct-xGMI two-shot (experimental) and the ternary wire.
 
 ``test_rccl_collectives_real_gpus`` drives every ``RcclComm`` entry point across the ranks --

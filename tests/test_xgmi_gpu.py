@@ -139,3 +139,102 @@ def test_engine_xgmi_world1_matches_default():
             assert torch.isfinite(e.opt.p).all() and d < 5e-2, d
     finally:
         dist.destroy_process_group()
+
+
+def _timeout_rank(rank, ws, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws))
+    dist.init_process_group('gloo', rank=rank, world_size=ws)
+    try:
+        torch.cuda.set_device(0)
+        from mercury_amd.parallel.xgmi import XgmiAllReduce, XgmiTimeout
+        try:
+            x = XgmiAllReduce(1 << 12, 'cuda', barrier='device', timeout_s=0.5)
+        except RuntimeError as e:
+            q.put(('skip', str(e)))
+            return
+        dist.barrier()
+        if rank == 0:
+            # the peer never arrives: both device barriers of the all-reduce give up after 0.5 s
+            t = torch.ones(1 << 12, device='cuda')
+            x.allreduce(t, avg=True, slot=0)
+            torch.cuda.synchronize()
+            try:
+                x.check()
+                q.put(('no-raise', None))
+            except XgmiTimeout as e:
+                q.put(('timeout', str(e)))
+        else:
+            q.put(('idle', None))
+        dist.barrier()
+        try:
+            x.close(sync_peers=False)
+        except XgmiTimeout:
+            pass
+    finally:
+        dist.destroy_process_group()
+
+
+def test_device_barrier_timeout_is_reported():
+    """A peer that never reaches the device flag barrier: the barrier gives up after timeout_s
+    and ``check()`` (which the engine runs in read_meters) raises XgmiTimeout naming the peer."""
+    import queue
+    import time
+    import torch.multiprocessing as mp
+    from mercury_amd.parallel.dist import free_port
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_timeout_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res, deadline = [], time.time() + 100
+    while len(res) < 2 and time.time() < deadline:
+        try:
+            res.append(q.get(timeout=2))
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert len(res) == 2, 'ranks exited %s' % [p.exitcode for p in procs]
+    if any(r[0] == 'skip' for r in res):
+        pytest.skip('IPC unavailable on this box')
+    kinds = sorted(r[0] for r in res)
+    assert kinds == ['idle', 'timeout'], res
+    assert 'peers [1]' in [r for r in res if r[0] == 'timeout'][0][1]
+
+
+def test_engine_read_meters_raises_on_xgmi_timeout():
+    """The engine surfaces a device-barrier timeout at its next host sync (read_meters)."""
+    import torch.distributed as dist
+    from mercury_amd.data.datasets import synthetic_arrays
+    from mercury_amd.engine.native import NativeEngine
+    from mercury_amd.models import ResNet18
+    from mercury_amd.parallel.dist import free_port
+    from mercury_amd.parallel.xgmi import XgmiTimeout
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % free_port(), rank=0,
+                            world_size=1, device_id=torch.device('cuda', 0))
+    try:
+        x, y = synthetic_arrays(1000, 10, seed=5)
+        e = NativeEngine(ResNet18(10).cuda(), 'cuda', 32, 10, bucket_bytes=4 << 20, seed=3,
+                         force_buckets=True, comm='xgmi')
+        e.set_shard(x, y)
+        e.prime()
+        e.step()
+        e.read_meters()                       # clean
+        e.xgmi._err.fill_(1 << 3)             # as the barrier kernel records a late peer 3
+        with pytest.raises(XgmiTimeout, match='peers \\[3\\]'):
+            e.read_meters()
+        e.xgmi._err.zero_()
+        e.close()
+        with pytest.raises(RuntimeError, match='closed'):
+            e.step()
+    finally:
+        dist.destroy_process_group()
