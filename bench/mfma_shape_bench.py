@@ -1,4 +1,4 @@
-"""v_mfma_f32_16x16x32_bf16 vs v_mfma_f32_32x32x16_bf16 on MI355X (csrc/ubench.hip).
+"""v_mfma_f32_16x16x32_bf16 vs v_mfma_f32_32x32x16_bf16 on MI355X (csrc/tools/ubench.hip).
 
 Same output tile per wave (64 x 64), one wave per SIMD (256-thread blocks, one per CU), random
 bf16 operands, operands in registers (lds=0) or re-read from LDS every K step (lds=1).  The two
@@ -26,9 +26,13 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--grid', type=int, default=256)
     args = ap.parse_args()
+    import ctypes
     import torch
-    from mercury_amd.ops import lib, ptr, stream_ptr
-    L = lib()
+    from mercury_amd import _build
+    from mercury_amd.ops import ptr, stream_ptr
+    L = ctypes.CDLL(_build.build_tools(verbose=False))   # csrc/tools/ubench.hip (C ABI)
+    L.ubench_mfma.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     src = (torch.rand(1 << 20, device='cuda') * 2 - 1).to(torch.bfloat16)
     out = torch.empty(args.grid * 256, device='cuda')
     flop = 524288.0 * 4 * args.grid * args.trips      # per trip per wave, 4 waves per block

@@ -26,10 +26,6 @@ int igemm_dual_launch(const bf16* srcA, const bf16* wtA, const ConvGeom& gA, con
                       const EpiParams& eB, int splitsB, int bm, int bn, hipStream_t st);
 int hconv_read_stamps(unsigned long long* host, int n);
 void hconv_configure(int grid, int waves);
-int wsconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
-                  int grid, hipStream_t st);
-int ubench_mfma(int shape, int lds, const bf16* src, int trips, int grid, float* out,
-                hipStream_t st);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);
@@ -401,27 +397,7 @@ PYBIND11_MODULE(_C, m) {
     return v;
   });
   m.def("hconv_configure", &hconv_configure);
-  // weight-stationary persistent halo conv (wsconv.hip): stride-1 3x3, 64 / 128 input channels;
-  // returns False when the conv is outside its contract
-  m.def("wsconv", [](uintptr_t src, uintptr_t wt, uintptr_t out, uintptr_t stats, int group_rows,
-                     const std::vector<int>& geo, int grid, uintptr_t st) {
-    if (geo.size() != 19) throw std::invalid_argument("wsconv: geometry needs 19 ints");
-    HconvGeom g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9],
-                geo[10], geo[11], geo[12], geo[13], geo[14], geo[15], geo[16], geo[17], geo[18],
-                0, nullptr};
-    const int K = geo[6];
-    EpiParams e{P<bf16>(out), K, nullptr, P<float>(stats), K, group_rows, 0, nullptr, nullptr,
-                nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
-    const int ok = wsconv_launch(P<const bf16>(src), P<const bf16>(wt), g, e, grid, S(st));
-    check_launch("wsconv");
-    return ok != 0;
-  });
-  m.def("ubench_mfma", [](int shape, int lds, uintptr_t src, int trips, int grid, uintptr_t out,
-                          uintptr_t st) {
-    if (!ubench_mfma(shape, lds, P<const bf16>(src), trips, grid, P<float>(out), S(st)))
-      throw std::invalid_argument("ubench_mfma: shape 16 / 32, lds 0 / 1");
-    check_launch("ubench_mfma");
-  });   // persistent halo grid (0: half the CUs), waves
+// persistent halo grid (0: half the CUs), waves
   m.def("hconv_stamps", [](int n) {   // diagnostic build only (MERCURY_STAMPS); else empty
     std::vector<unsigned long long> v((size_t)n * 12, 0ull);
     if (!hconv_read_stamps(v.data(), n)) v.clear();

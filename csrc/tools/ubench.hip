@@ -19,7 +19,7 @@
 // loop), which made the first version of this benchmark rank the 16x16x32 shape 1.3-1.65x slower
 // for that reason alone.  With the pin, the LDS=1 loops of both shapes are MFMA + ds_read only;
 // the LDS=0 16x16x32 loop still carries the copies (hipcc, loop-invariant operands) -- read LDS=1.
-#include "common.h"
+#include "../common.h"
 
 namespace {
 
@@ -135,8 +135,10 @@ __global__ __launch_bounds__(256, 1) void mfma_loop_kernel(const bf16* __restric
 }  // namespace
 
 // shape 16 / 32, lds 0 / 1; src: >= 2 MB of bf16 (random), out: grid * 256 floats
-int ubench_mfma(int shape, int lds, const bf16* src, int trips, int grid, float* out,
-                hipStream_t st) {
+// C ABI: this file is its own shared object (mercury_amd/_tools.so, loaded by ctypes from
+// bench/mfma_shape_bench.py), not part of the production extension
+extern "C" int ubench_mfma(int shape, int lds, const bf16* src, int trips, int grid, float* out,
+                           hipStream_t st) {
 #define UB_CASE(S_, L_)                                                                         \
   if (shape == S_ && lds == L_) {                                                               \
     hipLaunchKernelGGL((mfma_loop_kernel<S_, L_>), dim3(grid), dim3(256), 0, st, src, trips, out); \

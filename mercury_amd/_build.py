@@ -91,8 +91,35 @@ def build(verbose=True, jobs=None):
     return TARGET
 
 
+TOOLS = os.path.join(ROOT, 'mercury_amd', '_tools.so')
+
+
+def build_tools(verbose=True):
+    """Diagnostic kernels (``csrc/tools/*.hip``, C ABI, loaded by ctypes from ``bench/``) in a
+    shared object of their own, so nothing of them ships in the production extension."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, 'tools', '*.hip')))
+    if not srcs:
+        return None
+    hdr_t = _newest_header()
+    objs = []
+    for s in srcs:
+        o = os.path.join(OBJ, 'tools_' + os.path.basename(s) + '.o')
+        objs.append(o)
+        if _needs(s, o, hdr_t):
+            _compile(s, o, [])
+    if not os.path.exists(TOOLS) or any(os.path.getmtime(o) > os.path.getmtime(TOOLS)
+                                        for o in objs):
+        cmd = [HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objs + ['-o', TOOLS]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError('link failed: %s\n%s' % (r.stdout, r.stderr))
+        if verbose:
+            print('[mercury_amd] built %s' % os.path.relpath(TOOLS, ROOT), flush=True)
+    return TOOLS
+
+
 def clean():
-    for f in glob.glob(os.path.join(OBJ, '*.o')) + [TARGET]:
+    for f in glob.glob(os.path.join(OBJ, '*.o')) + [TARGET, TOOLS]:
         if os.path.exists(f):
             os.remove(f)
 
@@ -101,3 +128,4 @@ if __name__ == '__main__':
     if '--clean' in sys.argv:
         clean()
     build()
+    build_tools()

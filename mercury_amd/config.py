@@ -132,11 +132,6 @@ class EngineOptions:
     hconv_persist_grid: int = 0
     # waves per persistent halo block (8: 1.513 vs 1.521 ms/step over 4)
     hconv_persist_waves: int = 8
-    # stride-1 3x3 convs with 64 / 128 input channels on the weight-stationary persistent kernel
-    # (csrc/wsconv.hip): '1' both batch modes, 'score' / 'train' one, '0' off
-    wsconv: str = '0'
-    # its grid (0: half the CUs, like the persistent halo kernel beside the train stream)
-    wsconv_grid: int = 0
     # per-shape halo plan overrides for sweeps: "N,H,C,K=bm,bn,splits;..." ('none' = igemm)
     hconv_plans: str = ''
     # 1x1 convs on the persistent LDS-DMA pointwise GEMM (profiles/r3/pgemm_cmp_v2.jsonl)

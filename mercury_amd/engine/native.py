@@ -410,11 +410,6 @@ class NativeEngine(object):
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
-                    # ... the 64 / 128-channel ones with their weights held in registers
-                    uw = self.opts.wsconv == '1' or \
-                        self.opts.wsconv == ('train' if train else 'score')
-                    if uw and hconv.wsconv_ok(sp, bias=u.b_seg is not None):
-                        m.plan[u.name, 'wsconv'] = True
                     # ... and the convs that take their input's BN in the halo staging
                     fb = self.fuse_bn_halo == '1' or \
                         self.fuse_bn_halo == ('train' if train else 'score')
@@ -522,8 +517,6 @@ class NativeEngine(object):
             ops.dwconv_fwd(x, self._pview(u.w_seg), y, sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q,
                            sp.stride, sp.pad, stats=stats, group_rows=sp.group_rows or sp.M,
                            pro=pro if pro is not None and pro.get('dw') else None)
-        elif pro is None and (u.name, 'wsconv') in m.plan:
-            hconv.wsconv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats)
         elif pro is None and (u.name, 'hconv') in m.plan:
             hconv.hconv_fwd(x, self.w_krsc[u.name], y, sp, m.plan[u.name, 'hconv'], stats=stats,
                             slab=m.slab,
@@ -537,7 +530,7 @@ class NativeEngine(object):
         """True when _conv_fwd(m, u, ..., pro=None) runs u on the plain igemm kernel."""
         if u.depthwise or u.b_seg is not None:
             return False
-        if any((u.name, k) in m.plan for k in ('stem', 'wsconv', 'hconv')):
+        if any((u.name, k) in m.plan for k in ('stem', 'hconv')):
             return False
         return not ((u.name, 'pgemm') in m.plan and pgemm_plain_wins(m.spec[u.name]))
 

@@ -71,7 +71,7 @@ def lds_bytes(g, bm, bn, splits):
 
 
 # engine-selected settings (config.EngineOptions via ``configure``)
-_CFG = dict(persist=True, plans='', waves=8, grid=0, ws_grid=0)
+_CFG = dict(persist=True, plans='', waves=8, grid=0)
 
 
 def configure(opts):
@@ -79,7 +79,7 @@ def configure(opts):
     wave count are also handed to the C++ launcher)."""
     _CFG.update(persist=bool(opts.hconv_persist), plans=opts.hconv_plans or '',
                 waves=8 if opts.hconv_persist_waves == 8 else 4,
-                grid=int(opts.hconv_persist_grid), ws_grid=int(opts.wsconv_grid))
+                grid=int(opts.hconv_persist_grid))
     lib().hconv_configure(_CFG['grid'], _CFG['waves'])
 
 
@@ -411,55 +411,6 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
 
 
 # ---------------------------------------------------------------------- weight-stationary
-# csrc/wsconv.hip: stride-1 3x3 convs with 64 / 128 input channels, weights held in registers
-# for the whole persistent launch, only the halo streamed.  Instantiated geometries, by input
-# channels: (BM, BN, halo pitch HWP, max halo DMA pieces per wave)
-WS_TILES = {64: (256, 64, 40, 16), 128: (64, 128, 24, 8)}
 
 
-def wsconv_geometry(spec: ConvSpec):
-    """HconvGeom dict of the weight-stationary kernel for this conv, or None."""
-    if not (spec.R == spec.S == 3 and spec.stride == 1 and spec.pad == 1
-            and spec.C == spec.Cp and spec.C in WS_TILES):
-        return None
-    bm, bn, hwp, hrc = WS_TILES[spec.C]
-    if spec.K % bn or spec.M % bm or (spec.group_rows and spec.group_rows % bm):
-        return None
-    ts = _tile_shape(spec, bm)
-    if ts is None:
-        return None
-    img, tr = ts
-    hwd = spec.W + 2
-    if hwd > hwp:
-        return None
-    ht = tr + 2
-    hpix = img * ht * hwp
-    if -(-hpix // 32) > hrc:
-        return None
-    return dict(N=spec.N, H=spec.H, W=spec.W, C=spec.C, P=spec.P, Q=spec.Q, K=spec.K, R=3,
-                stride=1, pad=1, IMG=img, TR=tr, HT=ht, HWd=hwd, HWP=hwp, HALF=0, HS=1, SR=1,
-                HPIX=hpix)
-
-
-def wsconv_ok(spec: ConvSpec, bias=False):
-    return not bias and wsconv_geometry(spec) is not None
-
-
-def wsconv_fwd(x, w, out, spec: ConvSpec, stats=None, grid=0):
-    """out[M][K] = conv3x3(x NHWC, w [K][3][3][C]) with the ghost-BN statistics epilogue, on the
-    weight-stationary persistent kernel (``grid`` blocks; 0: half the CUs, EngineOptions)."""
-    g = wsconv_geometry(spec)
-    if g is None:
-        raise ValueError('wsconv: unsupported conv %s' % (spec,))
-    _chk(x, torch.bfloat16, 'x', spec.N * spec.H * spec.W * spec.C)
-    _chk(w, torch.bfloat16, 'w', spec.K * 9 * spec.C)
-    _chk(out, torch.bfloat16, 'out', spec.M * spec.K)
-    _chk(stats, torch.float32, 'stats')
-    grp = spec.group_rows if spec.group_rows else spec.M
-    if stats is not None:
-        _chk(stats, torch.float32, 'stats', (spec.M // grp) * 2 * spec.K)
-    grid = int(grid or _CFG.get('ws_grid') or 128)
-    if not lib().wsconv(ptr(x), ptr(w), ptr(out), ptr(stats), grp, [int(g[k]) for k in _ORDER],
-                        grid, stream_ptr()):
-        raise ValueError('wsconv: launch refused the conv %s' % (spec,))
     return out
