@@ -1,17 +1,21 @@
 """Time-to-accuracy: importance sampling vs uniform sampling (Mercury's actual claim).
 
 Mercury trades per-step throughput (every step also scores a 10x32 pool) for
-fewer steps to a target accuracy.  This runs the native engine twice on the
-same synthetic CIFAR-10-shaped shard, same init, same Adam -- once with the
-reference importance sampler, once uniform -- evaluates held-out accuracy
-every ``--eval-every`` steps, and reports steps and wall time (event-timed
-train steps only, evaluation excluded) to reach ``--target``.
+fewer steps to a target accuracy.  For each of ``--seeds`` seeds (model init,
+sampling and augmentation streams) this runs the native engine twice on the
+same synthetic CIFAR-10-shaped shard -- once with the reference importance
+sampler (`pytorch_collab.py:108-116`), once uniform -- evaluates held-out
+accuracy every ``--eval-every`` steps on ``--test`` held-out samples, and
+reports, per seed and as mean +- std over seeds: accuracy at every checkpoint,
+steps and wall time (event-timed train steps only, evaluation excluded) to
+reach ``--target``, and the IS-minus-uniform accuracy gap in units of its
+standard error at the first checkpoint where the IS mean reaches the target.
 
 The synthetic task (low-contrast class templates under pixel noise, plus a fraction of
 relabelled "hard" samples) is NOT CIFAR-10, so the numbers measure the
 mechanism, not the paper's accuracy curve (no dataset download is possible).
 
-    python bench/time_to_accuracy.py [--steps 3000] [--target 0.8] > tta.json
+    python bench/time_to_accuracy.py [--steps 3000] [--seeds 5] [--target 0.6] > tta.json
 """
 import argparse
 import json
@@ -38,12 +42,12 @@ def make_data(n, ncls, seed, noise, hard_frac, contrast):
     return x, y
 
 
-def run(importance, args, xtr, ytr, xte, yte):
+def run(importance, args, seed, xtr, ytr, xte, yte):
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import build_model
-    torch.manual_seed(args.seed)
+    torch.manual_seed(seed)
     net = build_model(args.model, 10).cuda()
-    eng = NativeEngine(net, 'cuda', 32, 10, lr=args.lr, seed=11, importance=importance,
+    eng = NativeEngine(net, 'cuda', 32, 10, lr=args.lr, seed=11 + 7 * seed, importance=importance,
                        use_graphs=True)
     eng.set_shard(xtr, ytr)
     eng.scoring = importance
@@ -64,10 +68,26 @@ def run(importance, args, xtr, ytr, xte, yte):
             curve.append((s, round(t_train, 4), round(acc, 4)))
             if reached is None and acc >= args.target:
                 reached = (s, t_train)
+    eng.close()
     return {'curve': curve, 'steps_to_target': reached[0] if reached else None,
             'seconds_to_target': round(reached[1], 3) if reached else None,
             'ms_per_step': round(1e3 * curve[-1][1] / curve[-1][0], 4) if curve else None,
             'final_acc': curve[-1][2] if curve else None}
+
+
+def summarise(runs, target):
+    """mean / std over seeds of accuracy at each checkpoint, steps to target."""
+    steps = [c[0] for c in runs[0]['curve']]
+    accs = np.array([[c[2] for c in r['curve']] for r in runs])
+    reach = [r['steps_to_target'] for r in runs]
+    hit = [x for x in reach if x is not None]
+    return {'steps': steps, 'acc_mean': [round(float(v), 4) for v in accs.mean(0)],
+            'acc_std': [round(float(v), 4) for v in accs.std(0, ddof=1)] if len(runs) > 1
+            else None,
+            'steps_to_target_per_seed': reach,
+            'seeds_reaching_target': '%d/%d' % (len(hit), len(runs)),
+            'steps_to_target_mean': round(float(np.mean(hit)), 1) if hit else None,
+            'steps_to_target_std': round(float(np.std(hit, ddof=1)), 1) if len(hit) > 1 else None}
 
 
 def main():
@@ -80,20 +100,49 @@ def main():
     ap.add_argument('--noise', type=int, default=64)
     ap.add_argument('--contrast', type=float, default=0.04)
     ap.add_argument('--hard-frac', type=float, default=0.1)
-    ap.add_argument('--seed', type=int, default=3)
+    ap.add_argument('--seeds', type=int, default=5)
+    ap.add_argument('--seed0', type=int, default=3)
+    ap.add_argument('--train', type=int, default=10000)
+    ap.add_argument('--test', type=int, default=6000)
     args = ap.parse_args()
-    x, y = make_data(12000, 10, 8, args.noise, args.hard_frac, args.contrast)
-    xtr, ytr, xte, yte = x[:10000], y[:10000], x[10000:], y[10000:]
+    x, y = make_data(args.train + args.test, 10, 8, args.noise, args.hard_frac, args.contrast)
+    xtr, ytr = x[:args.train], y[:args.train]
+    xte, yte = x[args.train:], y[args.train:]
     out = {'bench': 'time_to_accuracy', 'model': args.model, 'target_acc': args.target,
+           'seeds': [args.seed0 + k for k in range(args.seeds)], 'held_out': args.test,
            'data': 'synthetic cifar10-shape, template contrast %.2f, noise +-%d, %.0f%% '
                    'relabelled' % (args.contrast, args.noise, 100 * args.hard_frac)}
     t0 = time.time()
-    out['importance'] = run(True, args, xtr, ytr, xte, yte)
-    out['uniform'] = run(False, args, xtr, ytr, xte, yte)
+    per = {'importance': [], 'uniform': []}
+    for k in range(args.seeds):
+        seed = args.seed0 + k
+        for name, imp in (('importance', True), ('uniform', False)):
+            r = run(imp, args, seed, xtr, ytr, xte, yte)
+            r['seed'] = seed
+            per[name].append(r)
+            print('[tta] seed %d %s: steps to %.2f = %s, final acc %.4f' % (
+                seed, name, args.target, r['steps_to_target'], r['final_acc']),
+                file=sys.stderr, flush=True)
+    out['per_seed'] = per
+    out['importance'] = summarise(per['importance'], args.target)
+    out['uniform'] = summarise(per['uniform'], args.target)
     i, u = out['importance'], out['uniform']
-    if i['seconds_to_target'] and u['seconds_to_target']:
-        out['time_speedup_vs_uniform'] = round(u['seconds_to_target'] / i['seconds_to_target'], 3)
-        out['step_speedup_vs_uniform'] = round(u['steps_to_target'] / i['steps_to_target'], 3)
+    # the IS - uniform gap at the first checkpoint where the IS mean reaches the target, in
+    # units of the standard error of the difference of the two seed means
+    n = args.seeds
+    for j, st in enumerate(i['steps']):
+        if i['acc_mean'][j] >= args.target:
+            gap = i['acc_mean'][j] - u['acc_mean'][j]
+            se = ((i['acc_std'][j] ** 2 + u['acc_std'][j] ** 2) / n) ** 0.5 if n > 1 else None
+            out['at_target_step'] = {'step': st, 'is_acc_mean': i['acc_mean'][j],
+                                     'uniform_acc_mean': u['acc_mean'][j], 'gap': round(gap, 4),
+                                     'gap_in_std_err': round(gap / se, 2) if se else None,
+                                     'is_acc_std': i['acc_std'][j] if n > 1 else None,
+                                     'uniform_acc_std': u['acc_std'][j] if n > 1 else None}
+            break
+    ti = [r['seconds_to_target'] for r in per['importance']]
+    if all(ti):
+        out['is_seconds_to_target_mean'] = round(float(np.mean(ti)), 3)
     out['wall_s'] = round(time.time() - t0, 1)
     print(json.dumps(out))
 
