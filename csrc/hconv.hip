@@ -524,8 +524,27 @@ MA_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
 }
 // 16 bytes per lane, buffer -> LDS (lane l lands at the wave-uniform LDS address + 16 l)
 MA_DEV void bdma16(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned lds) {
+  // (readfirstlane: resource and base are wave-uniform; under register pressure the compiler
+  // may otherwise hand the asm VGPRs for them)
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-               ::"v"(off), "s"(r), "s"(lds) : "memory");
+               ::"v"(off), "s"(r), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+// the same DMA with the buffer resource assembled from (base, bytes) as four wave-uniform
+// dwords (readfirstlane): where register pressure is high the compiler kept a resource built by
+// __builtin_amdgcn_make_buffer_rsrc in VGPRs, which the asm cannot take
+typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+MA_DEV u32x4s rsrc_words(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  u32x4s v;
+  v[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  v[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  v[2] = __builtin_amdgcn_readfirstlane(bytes);
+  v[3] = 0x00020000u;
+  return v;
+}
+MA_DEV void bdma16w(u32x4s r, unsigned off, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               ::"v"(off), "s"(r), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
 constexpr unsigned OOB = 0x7ffffff0u;   // offset past every tensor: zeros
 
@@ -974,6 +993,430 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   MA_STAMP(3);
 }
 
+// ---------------------------------------------------------------- row-step persistent variant
+// The scoring pass's stride-1 3x3 convs (B = 320, SURVEY K5 / `pytorch_collab.py:95-103`).
+// hconv_persist synchronises its waves once per TAP (a 64-deep K step): its phase stamps put the
+// per-tap barrier at 433 cycles against 440 of MFMA issue (profiles/r4/stamps).  Here one STEP
+// is one filter ROW -- 3 taps x 64 channels, K = 192 -- so a block synchronises three times per
+// 64-channel slice, and each wave issues 6 sub-steps of TM x TN MFMAs per barrier:
+//   * weights: a ring of WS slots, each one filter row (3 taps x BN channel rows x 64 channels,
+//     the igemm image [row][64] with chunk c ^ (row & 7)); the row of step s + 1 is DMA'd during
+//     step s (weights are L2-resident: one step of ~1.5k cycles covers them);
+//   * STATIONARY (C = K = 64, ResNet layer1: one slice, one channel tile): the three filter
+//     rows fill the three slots once and stay for the block's life, so the only staged operand
+//     is the halo and a block synchronises once per TILE;
+//   * halo: the next slice's (the next tile's when the slice is a tile's last) is DMA'd in two
+//     halves during rows 0 and 1 of the current slice, AFTER that step's weight row: the wait
+//     for a weight row therefore never waits for an HBM halo piece issued in the same step,
+//     and a halo is waited for only at its own slice start (2-3 steps after issue);
+//   * waits are counted (`s_waitcnt vmcnt(N)`, N a per-row immediate); the epilogue's stores
+//     are the youngest VMEM ops at a slice start, so they never drain;
+//   * pieces past the halo's last re-issue the last real piece (same source, same LDS bytes),
+//     so every wave issues exactly HRC pieces per halo without a dump area (layer1's LDS is
+//     exactly 160 KiB: two 44 KiB halos + three 24 KiB weight rows).
+// Output layout, ghost-BN running sums and flushes are hconv_persist's (epi_lean / epi_flush).
+template <int BM, int BN, int WM, int NW, int HRC, bool STATS, bool STAT, int MODE>
+__global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict__ src,
+                                                         const bf16* __restrict__ wt, HconvGeom g,
+                                                         EpiParams e, HconvPro pro) {
+  constexpr int WN = NW / WM;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  constexpr int WROWS = 3 * BN;                     // weight rows per step (3 taps x BN)
+  static_assert(WROWS % (8 * NW) == 0, "whole weight pieces per wave");
+  constexpr int BI = WROWS / (8 * NW);              // weight DMA pieces per wave per step
+  constexpr int WSLOT = WROWS * 128;                // bytes per ring slot
+  static_assert(HRC % 2 == 0 && HRC <= HRMAX, "halo pieces split over rows 0 and 1");
+  constexpr int HH = HRC / 2;                       // halo pieces per wave on rows 0 and 1
+  constexpr int ST = TM * TN;                       // epilogue stores per wave (epi_lean)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int ntn = g.K / BN;
+  const int PQ = g.P * g.Q;
+  const int mtiles = g.N * PQ / BM;
+  const int ntiles = mtiles * ntn;
+  const int G = gridDim.x, b = blockIdx.x;
+  // a contiguous, N-tile-major range of tiles per block (epi_lean's running sums; STATIONARY:
+  // one channel tile for the whole range)
+  const int t0 = (int)((long long)ntiles * b / G);
+  const int my = (int)((long long)ntiles * (b + 1) / G) - t0;
+  if (my == 0) return;
+  const int nsl = g.C >> 6;
+  const int Kt = 9 * g.C;
+  // halo: 8-pixel pieces; piece q of the halo is wave q % NW's (q / NW)-th.  A wave's issues
+  // past its last real piece repeat that piece (same source, same LDS bytes), so every wave
+  // issues exactly HRC per halo and the buffer holds just the halo (host: pieces <= HRC)
+  const int HP8 = (g.HPIX + 7) >> 3;
+  const int HBYTES = HP8 * 8 * 128;
+  const int ilast = __builtin_amdgcn_readfirstlane((HP8 - 1 - wu) / NW);
+  const int lc = (lane & 7) ^ (lane >> 3);
+  const int per_img = g.HT * g.HWP;
+  const unsigned src_bytes = (unsigned)((size_t)g.N * g.H * g.W * g.C * 2);
+  const unsigned wt_bytes = (unsigned)((size_t)g.K * Kt * 2);
+
+  // ---- tile-invariant halo slots, one register each: byte offset from the tile's (image, row)
+  // base in the low 26 bits, the slot's input row above (63: padding column / beyond the halo;
+  // host: a tile's images are < 64 MiB of input and < 63 halo rows)
+  unsigned hslot[HRC];
+#pragma unroll
+  for (int i = 0; i < HRC; ++i) {
+    hslot[i] = 63u << 26;
+    const int pix = 8 * (w + NW * min(i, ilast)) + (lane >> 3);
+    if (pix < g.HPIX) {
+      const int img = pix / per_img, rem = pix - img * per_img;
+      const int hr = rem / g.HWP, col = rem - hr * g.HWP;
+      const int ww = col - g.pad;
+      if (col < g.HWd && (unsigned)ww < (unsigned)g.W)
+        hslot[i] = ((unsigned)hr << 26) | (unsigned)((((img * g.H + hr) * g.W + ww) * g.C + lc * 8) * 2);
+    }
+  }
+  unsigned hoff[HRC];
+  int hgrp = 0;                                      // statistics group of that halo (MODE 1)
+  const float rmt = 1.f / (float)mtiles, rpq = 1.f / (float)PQ, rq = 1.f / (float)g.Q;
+  auto tile_of = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
+    const int t = t0 + k;
+    const int nt = udiv24(t, mtiles, rmt), mt = t - nt * mtiles;
+    m0 = mt * BM;
+    n0 = nt * BN;
+  };
+  auto set_halo = [&](int m0) __attribute__((always_inline)) {
+    const int n0i = udiv24(m0, PQ, rpq);
+    const int p0 = udiv24(m0 - n0i * PQ, g.Q, rq);
+    const int h0 = p0 - g.pad;
+    const int toff = (n0i * g.H + h0) * g.W * g.C * 2;
+    if constexpr (MODE == 1) hgrp = pro.stats ? n0i / pro.group_imgs : 0;
+#pragma unroll
+    for (int i = 0; i < HRC; ++i) {
+      const int hr = (int)(hslot[i] >> 26);
+      hoff[i] = hr != 63 && (unsigned)(h0 + hr) < (unsigned)g.H
+                    ? (hslot[i] & 0x3ffffffu) + (unsigned)toff : OOB;
+    }
+  };
+  // MODE 1: the input is the producer's raw conv output; its BatchNorm (ghost-group batch or
+  // running statistics) + activation is applied in LDS to each landed halo piece, once, by the
+  // thread whose DMA brought it (8 channels lc of the slice: scale / shift loaded into registers
+  // right before the transform, in the last row of the slice before).  Padding stays zero.
+  float csc[8], csh[8];
+  auto load_coef = [&](int cb, int grp) __attribute__((always_inline)) {
+    if constexpr (MODE == 1) {
+      const int ch = cb * 64 + lc * 8;
+      f32x4 a0, a1, b0, b1;
+      if (pro.stats) {
+        const float* st = pro.stats + (size_t)grp * 2 * g.C + ch;
+        a0 = *(const f32x4*)st;
+        a1 = *(const f32x4*)(st + 4);
+        b0 = *(const f32x4*)(st + g.C);
+        b1 = *(const f32x4*)(st + g.C + 4);
+      } else {
+        a0 = *(const f32x4*)(pro.rmean + ch);
+        a1 = *(const f32x4*)(pro.rmean + ch + 4);
+        b0 = *(const f32x4*)(pro.rvar + ch);
+        b1 = *(const f32x4*)(pro.rvar + ch + 4);
+      }
+      const f32x4 g0 = *(const f32x4*)(pro.gamma + ch), g1 = *(const f32x4*)(pro.gamma + ch + 4);
+      const f32x4 e0 = *(const f32x4*)(pro.beta + ch), e1 = *(const f32x4*)(pro.beta + ch + 4);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float a = q < 4 ? a0[q] : a1[q - 4], bb = q < 4 ? b0[q] : b1[q - 4];
+        float mean = a, var = bb;
+        if (pro.stats) {
+          mean = a * pro.inv_count;
+          var = fmaxf(bb * pro.inv_count - mean * mean, 0.f);
+        }
+        csc[q] = (q < 4 ? g0[q] : g1[q - 4]) * rsqrtf(var + pro.eps);
+        csh[q] = (q < 4 ? e0[q] : e1[q - 4]) - mean * csc[q];
+      }
+    }
+  };
+  auto xform = [&](int hbuf) __attribute__((always_inline)) {
+    if constexpr (MODE == 1) {
+      float lo, hi;
+      act_bounds(pro.act, lo, hi);
+#pragma unroll
+      for (int i = 0; i < HRC; ++i) {
+        if (i > ilast || hoff[i] == OOB) continue;   // (a repeat of piece ilast; padding)
+        u32x4* lp = (u32x4*)(smem + hbuf * HBYTES + 8 * (w + NW * i) * 128 + lane * 16);
+        const bf16x8 y = __builtin_bit_cast(bf16x8, *lp);
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(fminf(fmaxf(bf2f(y[q]) * csc[q] + csh[q], lo), hi));
+        *lp = __builtin_bit_cast(u32x4, o);
+      }
+    }
+  };
+  // A-fragment byte offsets in a halo buffer per (tap, fragment row block), k = 0..31 half (the
+  // other half is ^ 64)
+  const int c16 = (lane >> 4) << 4;
+  int aoff[9][TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int row = wm * (BM / WM) + tm * 16 + (lane & 15);
+    const int img = row / (g.TR * g.Q), rem = row - img * g.TR * g.Q;
+    const int tr = rem / g.Q, q = rem - tr * g.Q;
+    const int apix = img * per_img + tr * g.HWP + q;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int p = apix + (t / 3) * g.HWP + t % 3;
+      aoff[t][tm] = (p << 7) + (c16 ^ ((p & 7) << 4));
+    }
+  }
+  // weight DMA: piece q of this wave = step rows 8 (w + NW q) .. + 8; lane -> row + lane >> 3
+  unsigned boff[BI];
+#pragma unroll
+  for (int q = 0; q < BI; ++q) {
+    const int row = 8 * (w + NW * q) + (lane >> 3);
+    const int j = row / BN, n = row - j * BN;
+    boff[q] = (unsigned)((n * Kt + j * g.C + lc * 8) * 2);
+  }
+  // B-fragment byte offsets inside a slot, tap 0 of the row (tap j adds j * BN * 128)
+  int bfo[2][TN];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = wn * (BN / WN) + tn * 16 + (lane & 15);
+      bfo[kk][tn] = n * 128 + (((kk * 4 + (lane >> 4)) ^ (n & 7)) << 4);
+    }
+  const unsigned s_halo = lds_addr(smem);
+  const unsigned s_ring = s_halo + 2 * HBYTES;
+
+  auto issue_h = [&](int cb, int buf, int i) __attribute__((always_inline)) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane(
+        s_halo + buf * HBYTES + 8 * (wu + NW * min(i, ilast)) * 128);
+    bdma16w(rsrc_words(src, src_bytes), hoff[i] + cb * 128, dst);
+  };
+  // filter row r of (channel tile n0, slice cb) into ring slot `slot`
+  auto issue_w = [&](int n0, int cb, int r, int slot) __attribute__((always_inline)) {
+    const unsigned k = (unsigned)((n0 * Kt + 3 * r * g.C + cb * 64) * 2);
+    const unsigned base = __builtin_amdgcn_readfirstlane(s_ring + slot * WSLOT + 8 * wu * 128);
+#pragma unroll
+    for (int q = 0; q < BI; ++q)
+      bdma16w(rsrc_words(wt, wt_bytes), boff[q] + k, base + 8 * NW * q * 128);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rsum[TN][4], rsq[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rsum[i][j] = rsq[i][j] = 0.f;
+
+  // ---- slice cursors: slice sig = (tile k, slice cl); the halo cursor (kD, clD) is one ahead
+  const int NS = my * nsl;
+  int m0, n0;
+  tile_of(0, m0, n0);
+  int kD = 0, clD = 0;
+  auto advance_d = [&]() __attribute__((always_inline)) {
+    if (++clD == nsl) {
+      clD = 0;
+      if (++kD < my) {
+        int mD, nD;
+        tile_of(kD, mD, nD);
+        set_halo(mD);
+      }
+    }
+  };
+  // ---- prologue: slice 0's halo and the first weight row(s), all landed
+  set_halo(m0);
+#pragma unroll
+  for (int j = 0; j < HRC; ++j) issue_h(0, 0, j);
+  if constexpr (STAT) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) issue_w(n0, 0, r, r);
+  } else {
+    issue_w(n0, 0, 0, 0);
+  }
+  vm_wait<0>();
+  if constexpr (MODE == 1) {
+    load_coef(0, hgrp);
+    xform(0);
+  }
+  advance_d();                                       // the halo cursor is at slice 1
+  bar_lds();
+
+  int cl = 0, k = 0, sb = 0;                         // sb: ring slot of this slice's row 0
+  for (int sig = 0; sig < NS; ++sig) {
+    const bool last_sl = cl + 1 == nsl;
+    const bool hd = sig + 1 < NS;                    // a next slice exists: prefetch its halo
+    const bool epi_prev = cl == 0 && k > 0;          // the previous slice ended a tile
+    int m0n = m0, n0n = n0;
+    const int cbn = last_sl ? 0 : cl + 1;
+    if (last_sl && hd) tile_of(k + 1, m0n, n0n);
+    const int buf = sig & 1;
+    const int cbD = clD;
+    const char* hb = smem + buf * HBYTES;
+
+    // row r's start: its weight row (and, at r = 0, this slice's halo) has landed everywhere;
+    // then the next row's weights and this row's share of the next slice's halo are issued.
+    // Row 0 syncs before any read of this slice; rows 1 and 2 sync before the LAST tap of the
+    // previous row computes (its fragments are in registers: bar_lds retires their reads
+    // before the ring slot they came from is refilled)
+    auto row_start = [&](int r) __attribute__((always_inline)) {
+      if constexpr (STAT) {
+        if (r == 0 && sig > 0) {
+          vm_wait<ST>();                             // only the last tile's stores may be newer
+          bar_lds();
+        }
+        if (MODE == 1 && r == 2 && hd) {
+          vm_wait<0>();                              // the next slice's halo has landed
+          load_coef(cbD, hgrp);
+          xform(buf ^ 1);
+        }
+      } else {
+        if (r == 0) {
+          if (sig > 0) {
+            if (epi_prev) vm_wait<ST>();
+            else vm_wait<0>();
+            bar_lds();
+          }
+        } else {
+          if (hd && !(MODE == 1 && r == 2)) vm_wait<HH>();
+          else vm_wait<0>();
+          bar_lds();
+          if (MODE == 1 && r == 2 && hd) {
+            load_coef(cbD, hgrp);
+            xform(buf ^ 1);
+          }
+        }
+        if (r < 2) issue_w(n0, cl, r + 1, (sb + r + 1) % 2);
+        else if (hd) issue_w(n0n, cbn, 0, (sb + 3) % 2);
+      }
+      if (r < 2 && hd) {
+#pragma unroll
+        for (int q = 0; q < HH; ++q) issue_h(cbD, buf ^ 1, r * HH + q);
+      }
+    };
+    // fragments of tap t (both 32-deep halves) into register set u
+    bf16x8 fa[2][2][TM], fb[2][2][TN];
+    auto rd = [&](int u, int t) __attribute__((always_inline)) {
+      const int r = t / 3, j = t % 3;
+      const char* bs = smem + 2 * HBYTES + (STAT ? r : (sb + r) % 2) * WSLOT + j * BN * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) fb[u][kk][tn] = *(const bf16x8*)(bs + bfo[kk][tn]);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+          fa[u][kk][tm] = *(const bf16x8*)(hb + (aoff[t][tm] ^ (kk << 6)));
+      }
+    };
+    row_start(0);
+    rd(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int u = t & 1;
+      if (t + 1 < 9) {
+        if ((t + 1) % 3 == 0) row_start((t + 1) / 3);
+        rd(u ^ 1, t + 1);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][kk][tn], fa[u][kk][tm],
+                                                                 acc[tm][tn], 0, 0, 0);
+      if (t + 1 < 9) {
+        // the next tap's reads one per MFMA gap of this tap (left to itself the scheduler
+        // issued each read right before its consumer with lgkmcnt(1) waits: LDS latency exposed)
+        constexpr int NR = 2 * (TM + TN), NM = 2 * TM * TN;
+        static_assert(NR <= NM, "reads fit the MFMA gaps");
+#pragma unroll
+        for (int x = 0; x < NR; ++x) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+      }
+    }
+    if (last_sl) {
+      epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0);
+      if (STATS) {
+        const int gcur = m0 / e.group_rows;
+        if (!hd || n0n != n0 || m0n / e.group_rows != gcur)
+          epi_flush<BM, BN, WM, NW>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur, n0);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (hd) advance_d();
+    m0 = m0n;
+    n0 = n0n;
+    sb = (sb + 3) % 2;
+    if (last_sl) {
+      cl = 0;
+      ++k;
+    } else {
+      ++cl;
+    }
+  }
+}
+
+template <int BM, int BN, int NW>
+int hrow_lds_bytes(const HconvGeom& g, bool stat) {
+  const int hbytes = ((g.HPIX + 7) >> 3) * 8 * 128;
+  constexpr int WM = BM / 64;   // (epilogue staging needs 2 * WM * BN floats of a halo buffer)
+  if (hbytes < 2 * WM * BN * 4) return 1 << 30;
+  return 2 * hbytes + (stat ? 3 : 2) * 3 * BN * 128;
+}
+
+template <int BM, int BN, int WM, int NW, int HRC, bool STAT, int MODE>
+void launch_hrow_k(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                   const HconvPro& pro, int grid, int bytes, hipStream_t st) {
+  static bool attr[2] = {false, false};
+  const bool stats = e.stats != nullptr;
+  if (!attr[stats]) {
+    (void)hipFuncSetAttribute(
+        stats ? (const void*)hrow_kernel<BM, BN, WM, NW, HRC, true, STAT, MODE>
+              : (const void*)hrow_kernel<BM, BN, WM, NW, HRC, false, STAT, MODE>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr[stats] = true;
+  }
+  if (stats)
+    hipLaunchKernelGGL((hrow_kernel<BM, BN, WM, NW, HRC, true, STAT, MODE>), dim3(grid),
+                       dim3(64 * NW), bytes, st, src, wt, g, e, pro);
+  else
+    hipLaunchKernelGGL((hrow_kernel<BM, BN, WM, NW, HRC, false, STAT, MODE>), dim3(grid),
+                       dim3(64 * NW), bytes, st, src, wt, g, e, pro);
+}
+
+// 8 waves (two per SIMD), wave tiles 64 rows x 32 channels
+template <int BM, int BN, int WM, int NW>
+int launch_hrow(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
+                const HconvPro& pro, int grid, hipStream_t st) {
+  const bool stat = g.C == 64 && g.K == BN;
+  const int bytes = hrow_lds_bytes<BM, BN, NW>(g, stat);
+  if (bytes > 160 * 1024) return 0;
+  // halo pieces of wave 0 (the most): 8 covers the ResNet layer1 / layer2 scoring tiles (6);
+  // larger halos spill at 2 waves per SIMD -- not instantiated
+  const int hr = ((g.HPIX + 7) / 8 + NW - 1) / NW;
+  if (hr > 8) return 0;
+  const int hrc = 8;
+#define HR_CASE(H_)                                                                             \
+  if (hrc == H_) {                                                                              \
+    if (stat) {                                                                                 \
+      if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, true, 1>(src, wt, g, e, pro, grid, bytes, st); \
+      else launch_hrow_k<BM, BN, WM, NW, H_, true, 0>(src, wt, g, e, pro, grid, bytes, st);    \
+    } else {                                                                                    \
+      if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, false, 1>(src, wt, g, e, pro, grid, bytes, st); \
+      else launch_hrow_k<BM, BN, WM, NW, H_, false, 0>(src, wt, g, e, pro, grid, bytes, st);   \
+    }                                                                                           \
+    return 1;                                                                                   \
+  }
+  HR_CASE(8)
+#undef HR_CASE
+  return 0;
+}
+
 // LDS of the persistent kernel: two halo buffers (each also the epilogue's staging area, so it
 // must hold Smem::RED_BYTES), the weight ring, the DMA sink (1 KB per wave), and (MODE 1) the
 // BN table of G x C scale / shift pairs
@@ -1130,6 +1573,29 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   const int M = g.N * g.P * g.Q;
   const int gx = ((M + bm - 1) / bm) * ((g.K + bn - 1) / bn);
   const int nchunks = g.C >> 6;
+  if (splits < 0) {
+    // row-step persistent kernel (splits -1; 8 waves, 256 x 64 tiles): plain stride-1 input,
+    // whole tiles, ghost-BN groups made of whole tiles
+    const bool ok = (pro.mode == 0 || (pro.mode == 1 && pro.keep == nullptr)) &&
+                    e.bias == nullptr && !e.accumulate &&
+                    e.bw_sums == nullptr && g.stride == 1 && g.R == 3 && M % bm == 0 &&
+                    g.K % bn == 0 && (e.stats == nullptr || e.group_rows % bm == 0);
+    if (!ok) return 0;
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+    }
+    int gmax = g_persist_grid > 0 ? g_persist_grid : cus / 2;
+    if (gmax > cus) gmax = cus;
+    const int grid = gx < gmax ? gx : gmax;
+    e.slab = nullptr;
+    if (bm == 256 && bn == 64) return launch_hrow<256, 64, 4, 8>(src, wt, g, e, pro, grid, st);
+    return 0;
+  }
   const bool persist = splits == 0;
   splits = splits < 1 ? 1 : (splits > nchunks ? nchunks : splits);
   g.chunks_per_split = (nchunks + splits - 1) / splits;

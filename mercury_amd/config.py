@@ -132,6 +132,10 @@ class EngineOptions:
     hconv_persist_grid: int = 0
     # waves per persistent halo block (8: 1.513 vs 1.521 ms/step over 4)
     hconv_persist_waves: int = 8
+    # stride-1 3x3 convs on the row-step persistent kernel (csrc/hconv.hip hrow_kernel) where it
+    # measured faster: '1' both batch modes, 'score' / 'train' one, '0' off (hconv.MEASURED_ROW;
+    # layer1 scoring conv 51.6 vs 60.4 us, profiles/r5/hrow_bench_v3.jsonl)
+    hconv_row: str = 'score'
     # per-shape halo plan overrides for sweeps: "N,H,C,K=bm,bn,splits;..." ('none' = igemm)
     hconv_plans: str = ''
     # 1x1 convs on the persistent LDS-DMA pointwise GEMM (profiles/r3/pgemm_cmp_v2.jsonl)
@@ -179,12 +183,14 @@ class EngineOptions:
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes
     debug_log: bool = False
-    # REJECTED paths kept for re-measurement (off): the input BN (+ residual / shortcut BN) in
+    # the scoring pass's intra-block BN + activation applied in the persistent / row-step halo
+    # staging, no bn_apply pass (profiles/r5/ab_row_persist_bn.json: with hconv_row 1.336 vs
+    # 1.348 ms/step; on the per-tap kernel alone it measured neutral, profiles/r4/)
+    persist_bn: bool = True
+    # REJECTED path kept for re-measurement (off): the input BN (+ residual / shortcut BN) in
     # the per-tile halo conv's staging ('1' / 'score' / 'train'; profiles/r2/ab_fuse_bn_halo.json:
-    # off 1.602, score 1.634, train 1.724 ms/step) and the scoring pass's intra-block BN inside
-    # the persistent halo conv (profiles/r2/ab_persist_bn.json: 1.528 off vs 1.551 on)
+    # off 1.602, score 1.634, train 1.724 ms/step; profiles/r4/ab_rejected_remeasured.json)
     fuse_bn_halo: str = '0'
-    persist_bn: bool = False
 
     @classmethod
     def from_env(cls, base=None):

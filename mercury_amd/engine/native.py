@@ -406,7 +406,8 @@ class NativeEngine(object):
                         coef = max(coef, m.G * 2 * sp.Cp)
                     # stride-1 3x3 convs on the halo-tile kernel where it measured faster
                     uh = self.use_hconv == '1' or self.use_hconv == ('train' if train else 'score')
-                    hp = hconv.engine_plan(sp, bias=u.b_seg is not None) if uh else None
+                    hp = hconv.engine_plan(sp, bias=u.b_seg is not None,
+                                           train=train) if uh else None
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hp))

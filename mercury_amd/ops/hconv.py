@@ -71,7 +71,7 @@ def lds_bytes(g, bm, bn, splits):
 
 
 # engine-selected settings (config.EngineOptions via ``configure``)
-_CFG = dict(persist=True, plans='', waves=8, grid=0)
+_CFG = dict(persist=True, plans='', waves=8, grid=0, row='score')
 
 
 def configure(opts):
@@ -79,13 +79,45 @@ def configure(opts):
     wave count are also handed to the C++ launcher)."""
     _CFG.update(persist=bool(opts.hconv_persist), plans=opts.hconv_plans or '',
                 waves=8 if opts.hconv_persist_waves == 8 else 4,
-                grid=int(opts.hconv_persist_grid))
+                grid=int(opts.hconv_persist_grid), row=opts.hconv_row)
     lib().hconv_configure(_CFG['grid'], _CFG['waves'])
 
 
 def persist_waves():
     """Waves per persistent block (the C++ launcher uses the same value: ``configure``)."""
     return _CFG['waves']
+
+
+# row-step persistent kernel (csrc/hconv.hip hrow_kernel): plans (256, 64, -1), 8 waves;
+# stride-1 3x3 convs, plain input
+ROW_TILES = ((256, 64),)
+
+
+def row_lds_bytes(g, bm, bn, splits):
+    """Dynamic LDS of the row-step kernel: two halo buffers (8-pixel pieces) and a ring of
+    filter rows (3 taps x bn channel rows x 64 channels): 3 slots when the weights are
+    stationary (C = K = bn), else 2."""
+    nw = 8
+    p8 = -(-g['HPIX'] // 8)
+    hb = p8 * 8 * 128
+    if -(-p8 // nw) > 8 or hb < 2 * (bm // 64) * bn * 4:
+        return 1 << 30
+    stat = g['C'] == 64 and g['K'] == bn
+    return 2 * hb + (3 if stat else 2) * 3 * bn * 128
+
+
+def row_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
+    """The row-step kernel runs this conv: stride-1 3x3, plain input or the input's BN +
+    activation (no residual, no kept activation), no bias, whole tiles, ghost-BN groups made of
+    whole tiles."""
+    if pro is not None and any(pro.get(k) is not None for k in ('res', 'y2', 'keep')):
+        return False
+    if bias is not None or (bm, bn) not in ROW_TILES:
+        return False
+    if spec.stride != 1 or spec.R != 3 or spec.M % bm or spec.K % bn:
+        return False
+    grp = spec.group_rows or spec.M
+    return not stats or grp % bm == 0
 
 
 def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
@@ -276,7 +308,13 @@ def _plan_override(key):
     return False, None
 
 
-def engine_plan(spec: ConvSpec, bias=False):
+# Row-step kernel winners (bench/hrow_bench.py, graph-timed at the engine's 128-block grid,
+# profiles/r5/hrow_bench.jsonl): the weight-stationary layer1 scoring conv 51.6 vs 60.4 us (the
+# per-tap persistent kernel); layer2 53.1 vs 52.1 stays on the persistent kernel
+MEASURED_ROW = {(320, 32, 64, 64): (256, 64, -1)}
+
+
+def engine_plan(spec: ConvSpec, bias=False, train=None):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured
     persistent-kernel winners (EngineOptions.hconv_persist=0 turns them off), measured per-tile
     winners, else the heuristic for stride-1 3x3 convs with >= 128 channels (where it won every
@@ -293,6 +331,13 @@ def engine_plan(spec: ConvSpec, bias=False):
             return p
     # (the measured tables are keyed by the square CIFAR shapes)
     key = (spec.N, spec.H, spec.C, spec.K) if spec.H == spec.W else None
+    row = _CFG['row']
+    if key in MEASURED_ROW and not bias and (row == '1' or (row == 'score' and train is False)
+                                             or (row == 'train' and train is True)):
+        p = MEASURED_ROW[key]
+        g = geometry_cached(spec, p[0], p[1])
+        if g is not None and row_ok(spec, p[0], p[1]) and row_lds_bytes(g, *p) <= LDS_MAX:
+            return p
     if _CFG['persist'] and not bias and key is not None:
         p = (MEASURED_PERSIST if spec.stride == 1 else MEASURED_PERSIST_S2).get(key)
         if p is not None and persistent_ok(spec, p[0], p[1]):
@@ -313,8 +358,11 @@ def engine_plan(spec: ConvSpec, bias=False):
 
 def persist_bn_plan(spec: ConvSpec, group_imgs):
     """The persistent plan with the input's BN + activation in the halo staging (no residual),
-    or None.  Scoring pass only (EngineOptions.persist_bn, engine)."""
-    p = engine_plan(spec)
+    or None: the row-step kernel where it runs this conv, else the per-tap persistent kernel.
+    Scoring pass only (EngineOptions.persist_bn, engine)."""
+    p = engine_plan(spec, train=False)
+    if p is not None and p[2] < 0:
+        return p
     if p is None or p[2] != 0:
         return None
     pro = dict(stats=True, group_imgs=group_imgs)
@@ -392,6 +440,16 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
         raise ValueError('hconv does not support this conv')
     bm, bn, splits = p[:3]
     g = geometry_cached(spec, bm, bn)
+    if splits < 0:
+        if g is None or row_lds_bytes(g, bm, bn, splits) > LDS_MAX:
+            raise ValueError('hconv: row-step tile %dx%d does not fit this conv' % (bm, bn))
+        if not row_ok(spec, bm, bn, stats is not None, bias, pro):
+            raise ValueError('hconv: the row-step plan does not take this conv')
+        grp = spec.group_rows if spec.group_rows else spec.M
+        lib().hconv(ptr(x), ptr(w), ptr(out), ptr(bias), ptr(stats), grp, 0,
+                    [int(g[k]) for k in _ORDER], bm, bn, splits, stream_ptr(),
+                    *_pro_args(pro, spec))
+        return out
     extra = persist_table_bytes(spec, pro) if splits == 0 else 0
     if g is None or lds_bytes(g, bm, bn, splits) + extra > LDS_MAX:
         raise ValueError('hconv: tile %dx%d does not fit this conv' % (bm, bn))
@@ -407,10 +465,4 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
     lib().hconv(ptr(x), ptr(w), ptr(out), ptr(bias), ptr(stats), grp,
                 ptr(slab) if splits > 1 else 0, [int(g[k]) for k in _ORDER], bm, bn, splits,
                 stream_ptr(), *_pro_args(pro, spec))
-    return out
-
-
-# ---------------------------------------------------------------------- weight-stationary
-
-
     return out

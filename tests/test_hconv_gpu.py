@@ -223,3 +223,75 @@ def test_hconv_persistent(case, with_stats):
         rg = bf(ref).view(G, -1, K, spec.P, spec.Q)
         close(ostats[:, 0].cpu(), rg.sum((1, 3, 4)), rtol=1e-2, atol=0.5)
         close(ostats[:, 1].cpu(), rg.pow(2).sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+
+
+ROW_CASES = [
+    # N, H, C, K, (bm, bn), splits (-1), ghost images (0: one group)
+    (320, 32, 64, 64, (256, 64), -1, 32),    # layer1 scoring: weight-stationary, 160 KiB LDS
+    (64, 32, 64, 64, (256, 64), -1, 0),      # stationary, no ghost groups, uneven tiles/block
+    (320, 16, 128, 128, (256, 64), -1, 32),  # layer2: two slices, two channel tiles (streamed)
+    (96, 16, 192, 128, (256, 64), -1, 0),    # three slices, uneven tiles per block
+    (64, 32, 64, 128, (256, 64), -1, 32),    # C = 64 but two channel tiles: streamed
+]
+
+
+@pytest.mark.parametrize('with_stats', [True, False, 'bn', 'bn_eval'])
+@pytest.mark.parametrize('case', ROW_CASES)
+def test_hconv_row_step(case, with_stats):
+    """Row-step persistent plan (splits < 0, csrc/hconv.hip hrow_kernel): one filter row per
+    pipeline step, weights stationary in LDS when C = K = 64 -- output and ghost-BN sums vs
+    torch fp32, and the output bit-identical to the persistent kernel's (same MFMA order per
+    output: every tap's two 32-deep halves in the same sequence)."""
+    from mercury_amd import ops
+    from mercury_amd.ops import hconv as H
+    from mercury_amd.ops.conv import ConvSpec
+    ops.lib()
+    N, Hh, C, K, (bm, bn), splits, gimgs = case
+    spec = ConvSpec(N, Hh, Hh, C, K, 3, 3, 1, 1)
+    G = N // gimgs if gimgs else 1
+    if gimgs:
+        spec.group_rows = gimgs * spec.P * spec.Q
+    geo = H.geometry(spec, bm, bn)
+    assert geo is not None and H.row_lds_bytes(geo, bm, bn, splits) <= H.LDS_MAX
+    assert H.row_ok(spec, bm, bn, stats=with_stats)
+    g = torch.Generator(device='cpu').manual_seed(7)
+    x = bf(torch.randn(N, C, Hh, Hh, generator=g) * 1.5 + 0.3)
+    w = bf(torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9))
+    pro, a = None, x
+    if with_stats in ('bn', 'bn_eval'):
+        # MODE 1: the input's BN (ghost-group batch or running statistics) + ReLU in the halo
+        gi = gimgs or N
+        cnt = gi * Hh * Hh
+        xg = x.view(N // gi, gi, C, Hh, Hh)
+        st_in = torch.stack([xg.sum((1, 3, 4)), xg.pow(2).sum((1, 3, 4))], 1).contiguous()
+        gamma = torch.rand(C, generator=g) + 0.5
+        beta = torch.randn(C, generator=g) * 0.3
+        pro = dict(gamma=gamma.to(DEV), beta=beta.to(DEV), act='relu', eps=1e-5, count=cnt,
+                   group_imgs=gi)
+        if with_stats == 'bn':
+            a = bf(torch.relu(_bn_ref(x, st_in, gamma, beta, cnt, N // gi)))
+            pro['stats'] = st_in.reshape(-1).to(DEV)
+        else:
+            run = (torch.randn(C, generator=g) * 0.2, torch.rand(C, generator=g) + 0.5)
+            a = bf(torch.relu(_bn_ref(x, None, gamma, beta, cnt, 1, running=run)))
+            pro.update(rmean=run[0].to(DEV), rvar=run[1].to(DEV))
+    ref = F.conv2d(a, w, padding=1)
+    wk, _ = ops.pack_conv_weight(w.to(DEV))
+    xn = ops.to_nhwc(x.to(DEV))
+    out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
+    ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
+    H.hconv_fwd(xn, wk, out, spec, (bm, bn, splits), stats=ostats, pro=pro)
+    torch.cuda.synchronize()
+    got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
+    assert not torch.isnan(got).any()
+    close(got, ref)
+    if with_stats:
+        rg = bf(ref).view(G, -1, K, spec.P, spec.Q)
+        close(ostats[:, 0].cpu(), rg.sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+        close(ostats[:, 1].cpu(), rg.pow(2).sum((1, 3, 4)), rtol=1e-2, atol=0.5)
+    if pro is None and H.persistent_ok(spec, bm, bn, stats=with_stats) and \
+            H.lds_bytes(geo, bm, bn, 0) <= H.LDS_MAX:
+        out2 = torch.empty_like(out)
+        H.hconv_fwd(xn, wk, out2, spec, (bm, bn, 0), stats=None)
+        torch.cuda.synchronize()
+        assert torch.equal(out2, out)
