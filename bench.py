@@ -180,6 +180,11 @@ def main():
     ap.add_argument('--diag-steps', type=int, default=5,
                     help='untimed steps after the timed loop with device-phase events')
     args = ap.parse_args()
+    # stdout carries exactly ONE line, the result JSON: everything else written to fd 1 while the
+    # job runs (RCCL's version banner at communicator init, library warnings) goes to stderr
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     pre = PRESETS[args.config]
     args.batch = args.batch or pre['batch']
 
@@ -250,9 +255,9 @@ def main():
         for _ in range(args.steps):
             rep()
         torch.cuda.synchronize()
-        print(json.dumps({'replay_only': args.replay_only, 'config': args.config,
-                          'ms_per_replay': round((time.perf_counter() - t0) * 1e3 / args.steps,
-                                                 4)}), flush=True)
+        os.write(out_fd, (json.dumps({'replay_only': args.replay_only, 'config': args.config,
+                                      'ms_per_replay': round((time.perf_counter() - t0) * 1e3 /
+                                                             args.steps, 4)}) + '\n').encode())
         return
     t_is = run(eng, args.steps, args.warmup)
     m = eng.read_meters()
@@ -286,7 +291,8 @@ def main():
             'final_train_loss': round(m['loss_sum'] / max(m['count'], 1), 4),
         }
         out.update(diag)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(out_fd, (json.dumps(out) + '\n').encode())
     for e in (eng, eng_u):
         if e is not None:
             e.close()

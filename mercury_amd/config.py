@@ -179,6 +179,9 @@ class EngineOptions:
     # on the comm stream behind its node (no graph-internal comm streams;
     # profiles/r4/ab_comm_events.json)
     comm_events: bool = True
+    # issue the RCCL all-reduce even on a one-rank communicator (forced buckets at W = 1; it is
+    # the identity there -- the tests exercise RCCL with it, the bench measures without)
+    rccl_one_rank: bool = False
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes

@@ -1599,6 +1599,11 @@ class NativeEngine(object):
                 # the fp32 bytes), decoded to the same mean on every rank; Philox stream =
                 # (device optimizer-step counter, bucket): fresh every replayed step
                 self.tern.allreduce(g, i, dctr=self.ctrl[2:3])
+            elif self.comm.size == 1 and not self.opts.rccl_one_rank:
+                # one rank (forced buckets): the AVG is the identity -- the bucket plan, the
+                # event waits and the comm stream run as at W > 1, RCCL's one-rank copy kernel
+                # does not (EngineOptions.rccl_one_rank issues it: the tests)
+                pass
             elif self.wire_bf16:
                 # bf16 on the wire: half the bytes over xGMI; the sum is rounded once per hop
                 if self.wire is None:

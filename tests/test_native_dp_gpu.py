@@ -106,6 +106,53 @@ def test_native_trainer_api_checkpoint(tmp_path):
     assert torch.equal(tr2.engine.table.importance, tab.importance)
 
 
+def _trainer_worker(rank, ws, tmp):
+    """One rank of the two-rank NativeTrainer run: different init per rank, fit -> replicas
+    identical -> per-rank checkpoint -> a fresh trainer (another init) resumes to the same
+    parameters and optimizer state."""
+    from mercury_amd.ckpt import load_checkpoint, save_checkpoint
+    from mercury_amd.collab import make_trainer
+    from mercury_amd.config import Config
+    from mercury_amd.data import load_cifar10_noniid
+    from mercury_amd.engine.native import NativeTrainer
+    from mercury_amd.models import ResNet18
+    torch.cuda.set_device(0)
+    np.random.seed(102)
+    pres, train, test = load_cifar10_noniid(ws, 0.5, data_dir='/nonexistent')
+    cfg = Config(num_epochs=1, max_samples=60 * ws, print_every=0, eval_every=0, log_dir=tmp)
+    torch.manual_seed(100 + rank)                          # different init per rank
+    net = ResNet18(10).cuda()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    tr = make_trainer(cfg, net, opt, train, pres[rank], test, 'cuda')
+    assert isinstance(tr, NativeTrainer) and tr.world_size == ws
+    tr.fit(1)                                              # average_model: broadcast from rank 0
+    assert tr.step > 20
+    torch.cuda.synchronize()
+    p = tr.engine.opt.p.clone()
+    gathered = [torch.zeros_like(p) for _ in range(ws)]
+    dist.all_gather(gathered, p)
+    assert torch.equal(gathered[0], gathered[1]), float((gathered[0] - gathered[1]).abs().max())
+    path = save_checkpoint(tr, os.path.join(tmp, 'ckpt_rank%d.pt' % rank))
+    torch.manual_seed(7 + rank)
+    net2 = ResNet18(10).cuda()
+    tr2 = make_trainer(cfg, net2, torch.optim.Adam(net2.parameters(), lr=1e-3), train,
+                       pres[rank], test, 'cuda')
+    load_checkpoint(tr2, path)
+    assert torch.equal(tr2.engine.opt.p, p)
+    assert torch.equal(tr2.engine.opt.m, tr.engine.opt.m)
+    assert tr2.step == tr.step and tr2.epoch == tr.epoch
+    tr.engine.close()
+    tr2.engine.close()
+
+
+def test_native_trainer_two_ranks_fit_checkpoint_resume(tmp_path):
+    """The reference train-loop API end to end on two ranks (gloo, both on cuda:0, the
+    reference's own topology): fit with different per-rank inits keeps the replicas
+    bit-identical, and each rank resumes from its own checkpoint."""
+    from mercury_amd.parallel import spawn
+    spawn(_trainer_worker, 2, args=(str(tmp_path),), backend='gloo')
+
+
 def _init_nccl_w1():
     from mercury_amd.parallel.dist import free_port
     if dist.is_initialized():
@@ -115,10 +162,12 @@ def _init_nccl_w1():
 
 
 def _engine(x, y, **kw):
+    from mercury_amd.config import EngineOptions
     from mercury_amd.engine.native import NativeEngine
     from mercury_amd.models import ResNet18
     torch.manual_seed(7)
     net = ResNet18(10).cuda()
+    kw.setdefault('opts', EngineOptions(rccl_one_rank=True))   # RCCL runs even at W = 1
     eng = NativeEngine(net, 'cuda', 32, 10, bucket_bytes=4 << 20, seed=3, **kw)
     eng.set_shard(x, y)
     eng.prime()
@@ -238,9 +287,9 @@ def test_native_rccl_buckets_comm_events():
     try:
         base = _engine(x, y)
         runs = {'rccl': _engine(x, y, force_buckets=True, comm='rccl', check_order=True,
-                                opts=EngineOptions(comm_events=True)),
+                                opts=EngineOptions(comm_events=True, rccl_one_rank=True)),
                 'xgmi': _engine(x, y, force_buckets=True, comm='xgmi',
-                                opts=EngineOptions(comm_events=True))}
+                                opts=EngineOptions(comm_events=True, rccl_one_rank=True))}
         for r in runs.values():
             assert r._train_exec and len(r.bucket_plan()) > 1
         for _ in range(8):
