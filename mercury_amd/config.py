@@ -186,10 +186,12 @@ class EngineOptions:
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes
     debug_log: bool = False
-    # the scoring pass's intra-block BN + activation applied in the persistent / row-step halo
-    # staging, no bn_apply pass (profiles/r5/ab_row_persist_bn.json: with hconv_row 1.336 vs
-    # 1.348 ms/step; on the per-tap kernel alone it measured neutral, profiles/r4/)
-    persist_bn: bool = True
+    # the scoring pass's intra-block BN + activation applied in the halo staging of the
+    # persistent convs, no bn_apply pass: '1' every persistent conv, 'row' only the row-step
+    # kernel's (hconv_row), '0' none.  On the per-tap kernel the staging transform costs more
+    # than the pass it saves (layer3 81.5 vs 57 us): 'row' 1.307 vs '1' 1.333 ms/step with the
+    # layer1 + layer2 convs on the row-step kernel (profiles/r5/ab_persist_bn_scope.json)
+    persist_bn: str = 'row'
     # REJECTED path kept for re-measurement (off): the input BN (+ residual / shortcut BN) in
     # the per-tile halo conv's staging ('1' / 'score' / 'train'; profiles/r2/ab_fuse_bn_halo.json:
     # off 1.602, score 1.634, train 1.724 ms/step; profiles/r4/ab_rejected_remeasured.json)

@@ -206,7 +206,8 @@ class NativeEngine(object):
         self.head_bw = o.head_bw
         self.dw_pair = o.dw_pair
         self.fuse_bn_halo = o.fuse_bn_halo
-        self.persist_bn = o.persist_bn
+        self.persist_bn = o.persist_bn if o.persist_bn in ('0', '1', 'row') else (
+            '1' if str(o.persist_bn).lower() in ('true', 'on', 'yes') else '0')
         self._apply_globals()
 
         if sampler not in ('alias', 'cdf', 'groupwise'):
@@ -417,9 +418,10 @@ class NativeEngine(object):
                     hb = hconv.fused_plan(sp) if fb else None
                     # scoring pass: an intra-block conv on the persistent kernel takes its
                     # input's BN + activation in the halo staging (no residual there)
-                    if hb is None and not train and group_imgs and self.persist_bn and \
+                    if hb is None and not train and group_imgs and self.persist_bn != '0' and \
                             u is not blk.units[0] and u is not blk.shortcut:
-                        hb = hconv.persist_bn_plan(sp, group_imgs)
+                        hb = hconv.persist_bn_plan(sp, group_imgs,
+                                                   row_only=self.persist_bn == 'row')
                     if hb is not None:
                         m.plan[u.name, 'hconv_bn'] = hb
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hb))

@@ -308,10 +308,12 @@ def _plan_override(key):
     return False, None
 
 
-# Row-step kernel winners (bench/hrow_bench.py, graph-timed at the engine's 128-block grid,
-# profiles/r5/hrow_bench.jsonl): the weight-stationary layer1 scoring conv 51.6 vs 60.4 us (the
-# per-tap persistent kernel); layer2 53.1 vs 52.1 stays on the persistent kernel
-MEASURED_ROW = {(320, 32, 64, 64): (256, 64, -1)}
+# Row-step kernel plans: the weight-stationary layer1 scoring conv 51.6 vs 60.4 us on the
+# per-tap persistent kernel (bench/hrow_bench.py, graph-timed at the engine's 128-block grid,
+# profiles/r5/hrow_bench_v3.jsonl); layer2 53.1 vs 52.1 in isolation, but with the intra-block
+# BN folded into both kernels' halos the step is faster with it on the row-step kernel
+# (1.307 vs 1.333 ms/step, profiles/r5/ab_persist_bn_scope.json)
+MEASURED_ROW = {(320, 32, 64, 64): (256, 64, -1), (320, 16, 128, 128): (256, 64, -1)}
 
 
 def engine_plan(spec: ConvSpec, bias=False, train=None):
@@ -356,13 +358,15 @@ def engine_plan(spec: ConvSpec, bias=False, train=None):
     return None
 
 
-def persist_bn_plan(spec: ConvSpec, group_imgs):
+def persist_bn_plan(spec: ConvSpec, group_imgs, row_only=False):
     """The persistent plan with the input's BN + activation in the halo staging (no residual),
-    or None: the row-step kernel where it runs this conv, else the per-tap persistent kernel.
-    Scoring pass only (EngineOptions.persist_bn, engine)."""
+    or None: the row-step kernel where it runs this conv, else (unless ``row_only``) the per-tap
+    persistent kernel.  Scoring pass only (EngineOptions.persist_bn, engine)."""
     p = engine_plan(spec, train=False)
     if p is not None and p[2] < 0:
         return p
+    if row_only:
+        return None
     if p is None or p[2] != 0:
         return None
     pro = dict(stats=True, group_imgs=group_imgs)

@@ -83,9 +83,10 @@ def test_train_forward_backward_matches_torch(arch, hw):
     print(arch, 'worst grad error relative to torch-bf16', worst)
 
 
-@pytest.mark.parametrize('persist_bn', ['0', '1'])
+@pytest.mark.parametrize('persist_bn', ['0', '1', 'row'])
 def test_scoring_ghost_bn_matches_ten_separate_forwards(persist_bn, monkeypatch):
-    """(persist_bn: the intra-block BN + ReLU applied inside the persistent halo conv)"""
+    """(persist_bn: the intra-block BN + ReLU applied inside the persistent halo convs -- the
+    per-tap and the row-step kernels, or the row-step kernel only)"""
     from mercury_amd.models import ResNet18
     monkeypatch.setenv('MERCURY_ENGINE_OPTS', 'persist_bn=' + persist_bn)
     torch.manual_seed(1)
@@ -94,6 +95,10 @@ def test_scoring_ghost_bn_matches_ten_separate_forwards(persist_bn, monkeypatch)
     sm = eng.score_mode
     if persist_bn == '1':
         assert any(k[1] == 'hconv_bn' and p[2] == 0 for k, p in sm.plan.items())
+    if persist_bn != '0':
+        assert any(k[1] == 'hconv_bn' and p[2] < 0 for k, p in sm.plan.items())
+    if persist_bn == 'row':
+        assert not any(k[1] == 'hconv_bn' and p[2] >= 0 for k, p in sm.plan.items())
     sm.stats_arena.zero_()
     from mercury_amd import ops
     ops.pool_build(eng.shard, eng.shard_labels, eng.ctrl, sm.input, sm.label, sm.index, 320, 32,
