@@ -116,9 +116,11 @@ def main():
                                   bn_apply_us=round(tb, 2), hconv=None)), flush=True)
             continue
         best = min(res, key=res.get)
+        # input BN in the staging: persistent / row-step plans only (the per-tile modes were
+        # removed in round 5)
         pro = dict(stats=ystats, gamma=gamma, beta=beta, act='relu', count=(gimgs or N) * Hh * Hh,
-                   group_imgs=gimgs or N, keep=a if H.keep_ok(sp) else None)
-        tbn = -1.0 if args.no_bn else gtime(
+                   group_imgs=gimgs or N)
+        tbn = -1.0 if args.no_bn or best[2] > 0 else gtime(
             lambda: H.hconv_fwd(y, wk, out, sp, best, stats=stats, slab=slab, pro=pro),
             reps=args.reps)
         row = dict(shape=[N, C, K, Hh, R, st], igemm_plan=list(ip), igemm_us=round(ti, 2),

@@ -701,18 +701,12 @@ PYBIND11_MODULE(_C, m) {
                          int H, int W, int C, int Pp, int Q, int stride, int pad, uintptr_t slab,
                          int reduce, uintptr_t st, uintptr_t bw_out, uintptr_t bw_y,
                          uintptr_t bw_stats, uintptr_t bw_sums, float bw_inv_count, float bw_eps,
-                         int bw_act, uintptr_t p_dout, uintptr_t p_out, uintptr_t p_y,
-                         uintptr_t p_stats, uintptr_t p_gamma, uintptr_t p_sums, uintptr_t p_dgamma,
-                         uintptr_t p_dbeta, float p_inv_count, float p_eps, int p_act) {
+                         int bw_act) {
     DwBw bw{P<const bf16>(bw_out), P<const bf16>(bw_y), P<const float>(bw_stats), P<float>(bw_sums),
             bw_inv_count, bw_eps, bw_act};
-    // p_dout != 0: dy is not read; it is the dw conv's output BN backward of (dout, out, y)
-    DwPro pro{P<const bf16>(p_dout), P<const bf16>(p_out), P<const bf16>(p_y),
-              P<const float>(p_stats), P<const float>(p_gamma), P<const float>(p_sums),
-              P<float>(p_dgamma), P<float>(p_dbeta), p_inv_count, p_eps, p_act};
     dwconv_bwd_launch(P<const bf16>(dy), P<const bf16>(x), P<const float>(w), P<bf16>(dx),
                       P<float>(dw), N, H, W, C, Pp, Q, stride, pad, P<float>(slab),
-                      bw_sums ? &bw : nullptr, reduce != 0, S(st), p_dout ? &pro : nullptr);
+                      bw_sums ? &bw : nullptr, reduce != 0, S(st));
     check_launch("dwconv_bwd");
   });
   m.def("dwconv_wgrad_reduce_batch", [](std::vector<uintptr_t> slabs, std::vector<uintptr_t> dws,

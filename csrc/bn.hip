@@ -212,7 +212,7 @@ MA_DEV float sum_sums(const float* sums, int C, int h, int j) {
 
 template <int ACT, bool TWO>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
-  __shared__ float tot[3 * 2048];   // the replicas' totals [3][C] (C <= 2048)
+  __shared__ __attribute__((aligned(16))) float tot[3 * 2048];   // replicas' totals [3][C]
   const int C8 = a.C >> 3;
   constexpr bool two = TWO;
   const float inv = 1.f / (float)a.M;
@@ -251,16 +251,22 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
   mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
   load8(a.gamma + c, gm);
+  // (16-byte LDS reads: eight scalar reads at an 8-float lane stride were 8-way bank conflicts,
+  // 5.8-13.6 conflict cycles per LDS instruction in profiles/r4/pmc/final_step_pass.txt)
+  auto tot8 = [&](int base, float (&v)[8]) {
+    const f32x4 lo = *(const f32x4*)(tot + base), hi = *(const f32x4*)(tot + base + 4);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sdz[k] = tot[c + k];
-    sx[k] = tot[a.C + c + k];
-  }
+    for (int k = 0; k < 4; ++k) {
+      v[k] = lo[k];
+      v[4 + k] = hi[k];
+    }
+  };
+  tot8(c, sdz);
+  tot8(a.C + c, sx);
   if (two) {
     mean_rstd8(a.stats2 + c, a.C, inv, a.eps, mean2, rstd2);
     load8(a.gamma2 + c, gm2);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sx2[k] = tot[2 * a.C + c + k];
+    tot8(2 * a.C + c, sx2);
   }
   float k1[8], k2[8], q1[8], k3[8], q2[8];
 #pragma unroll

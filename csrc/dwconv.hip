@@ -199,66 +199,13 @@ MA_DEV float dw_mask(float out, int act) {       // (bn.hip act_mask)
   return 1.f;
 }
 
-// PRO (DwPro): dy is not read; each dy chunk is built from the dw conv's output BN backward,
-// dy = A * dout * act'(out) + B * y + Cc, from per-channel coefficients the block computed
-// into LDS (dw_pro_coef).  Padding chunks stay zero.
-struct DwCoef {
-  float a[8], b[8], c[8];
-};
-MA_DEV void dw_coef8(const float* coef, int C, int c8, DwCoef& k) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    k.a[q] = coef[c8 * 8 + q];
-    k.b[q] = coef[C + c8 * 8 + q];
-    k.c[q] = coef[2 * C + c8 * 8 + q];
-  }
-}
-struct DwRaw {
-  bf16x8 d, o, y;
-};
-MA_DEV DwRaw dw_raw(const DwPro& p, size_t off, bool ok) {
-  return DwRaw{ld8(p.dout + off, ok), ld8(p.out + off, ok), ld8(p.y + off, ok)};
-}
-MA_DEV bf16x8 dw_apply(const DwRaw& r, const DwCoef& k, int act, bool ok) {
-  bf16x8 v;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float dz = bf2f(r.d[q]) * dw_mask(bf2f(r.o[q]), act);
-    v[q] = f2bf(ok ? k.a[q] * dz + k.b[q] * bf2f(r.y[q]) + k.c[q] : 0.f);
-  }
-  return v;
-}
-// coefficients [3][C] into LDS (every thread of the block), block 0 also writes dgamma / dbeta
-MA_DEV void dw_pro_coef(const DwPro& p, int C, float* coef) {
-  for (int j = threadIdx.x; j < C; j += DT) {
-    float sdz = 0.f, sx = 0.f;
-#pragma unroll
-    for (int r = 0; r < SUMS_R; ++r) {
-      sdz += p.sums[((size_t)r * 3) * C + j];
-      sx += p.sums[((size_t)r * 3 + 1) * C + j];
-    }
-    const float mean = p.stats[j] * p.inv_count;
-    const float rstd = rsqrtf(fmaxf(p.stats[C + j] * p.inv_count - mean * mean, 0.f) + p.eps);
-    const float a = p.gamma[j] * rstd, k2 = sdz * p.inv_count, q1 = sx * p.inv_count;
-    coef[j] = a;
-    coef[C + j] = -a * q1 * rstd;
-    coef[2 * C + j] = a * (q1 * rstd * mean - k2);
-    if (blockIdx.x == 0) {
-      p.dgamma[j] = sx;
-      p.dbeta[j] = sdz;
-    }
-  }
-  __syncthreads();
-}
-
 // BW: the dgrad also reduces the BN-backward sums of the BN feeding this conv (what
 // bn_bwd_reduce would do in a separate pass over dx, out and y): dz = dx * act'(out),
 // sums += (dz, dz * xhat), block-reduced through padded LDS rows, one atomic pair per channel.
 // (body shared by the standalone launch and the dgrad + wgrad pair: block ``bid`` of ``nblk``)
-template <int S, bool BW, bool PRO = false>
+template <int S, bool BW>
 MA_DEV void dw_dgrad_body(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
-                          int P, int Q, int pad, const DwBw& bw, float* part, int bid, int nblk,
-                          const DwPro& pro = DwPro{}, const float* coef = nullptr) {
+                          int P, int Q, int pad, const DwBw& bw, float* part, int bid, int nblk) {
   // part (BW): [DT][ST_LD] per-thread (sum dz, sum dz * xhat)
   const int C8 = C >> 3, WS = (W + DWL - 1) / DWL;
   const int total = N * H * WS * C8;
@@ -273,8 +220,6 @@ MA_DEV void dw_dgrad_body(const bf16* dy, const float* w, bf16* dx, int N, int H
   float wr[9][8];
   float mean[8], rstd[8];
   const int c8 = gt % C8;
-  DwCoef kp;
-  if constexpr (PRO) dw_coef8(coef, C, c8, kp);
   if (gt < lim) {
     load_w72(w, c8, wr);
     if constexpr (BW) {
@@ -316,24 +261,10 @@ MA_DEV void dw_dgrad_body(const bf16* dy, const float* w, bf16* dx, int N, int H
           const size_t roff = (size_t)(n * P + hp) * Q * C + c8 * 8;
           const bf16* row = dy + roff;
           bf16x8 col[DWL + 2];  // dy columns x0+pad-2 .. x0+DWL-1+pad
-          if constexpr (PRO) {
-            DwRaw raw[DWL + 2];   // every chunk's three loads in flight before any transform
 #pragma unroll
-            for (int j = 0; j < DWL + 2; ++j) {
-              const int q = x0 + pad - 2 + j;
-              raw[j] = dw_raw(pro, roff + (size_t)q * C, q >= 0 && q < Q);
-            }
-#pragma unroll
-            for (int j = 0; j < DWL + 2; ++j) {
-              const int q = x0 + pad - 2 + j;
-              col[j] = dw_apply(raw[j], kp, pro.act, q >= 0 && q < Q);
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < DWL + 2; ++j) {
-              const int q = x0 + pad - 2 + j;
-              col[j] = ld8(row + (size_t)q * C, q >= 0 && q < Q);
-            }
+          for (int j = 0; j < DWL + 2; ++j) {
+            const int q = x0 + pad - 2 + j;
+            col[j] = ld8(row + (size_t)q * C, q >= 0 && q < Q);
           }
 #pragma unroll
           for (int o = 0; o < DWL; ++o)
@@ -352,11 +283,7 @@ MA_DEV void dw_dgrad_body(const bf16* dy, const float* w, bf16* dx, int N, int H
             for (int t = 0; t < 3; ++t) {
               const int wp = x0 + o + pad - t;
               if (wp >= 0 && (wp % S) == 0 && wp / S < Q) {
-                bf16x8 v;
-                if constexpr (PRO)
-                  v = dw_apply(dw_raw(pro, roff + (size_t)(wp / S) * C, true), kp, pro.act, true);
-                else
-                  v = *(const bf16x8*)(row + (size_t)(wp / S) * C);
+                const bf16x8 v = *(const bf16x8*)(row + (size_t)(wp / S) * C);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(v[k]) * wr[rr * 3 + t][k];
               }
@@ -426,10 +353,9 @@ constexpr int WG_LD = 73;   // floats per thread row (odd: conflict-free row wri
 // A row is split into QS column segments of QL columns (one thread each): the serial walk --
 // one memory round trip per column -- is QS x shorter and the grid QS x larger (the train-batch
 // layers otherwise launch 48-100 blocks whose threads each walk 32 dependent columns).
-template <int S, bool PRO = false>
+template <int S>
 MA_DEV void dw_wgrad_body(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,
-                          int P, int Q, int pad, int QS, float* slab, float* part, int bid,
-                          const DwPro& pro = DwPro{}, const float* coef = nullptr) {
+                          int P, int Q, int pad, int QS, float* slab, float* part, int bid) {
   // part: [DT][WG_LD]
   const int C8 = C >> 3;
   const int total = N * P * QS * C8;
@@ -466,16 +392,7 @@ MA_DEV void dw_wgrad_body(const bf16* dy, const bf16* x, float* dw, int N, int H
       }
     const size_t goff = (size_t)(n * P + p) * Q * C + c8 * 8;
     const bf16* grow = dy + goff;
-    DwCoef kp;
-    DwRaw rg;
-    bf16x8 g;
-    if constexpr (PRO) {
-      dw_coef8(coef, C, c8, kp);
-      rg = dw_raw(pro, goff + (size_t)q0 * C, q0 < q1);
-      g = dw_apply(rg, kp, pro.act, q0 < q1);
-    } else {
-      g = ld8(grow + (size_t)q0 * C, q0 < q1);
-    }
+    bf16x8 g = ld8(grow + (size_t)q0 * C, q0 < q1);
     for (int q = q0; q < q1; ++q) {
       // column q+1's loads first
       bf16x8 n1[3], n2[3], ng = g;
@@ -486,11 +403,7 @@ MA_DEV void dw_wgrad_body(const bf16* dy, const bf16* x, float* dw, int N, int H
         if (S == 2) n1[rr] = ld8(rows[rr] + (size_t)(base + 1) * C, more && rok[rr] && base + 1 >= 0 && base + 1 < W);
         n2[rr] = ld8(rows[rr] + (size_t)(base + 2) * C, more && rok[rr] && base + 2 >= 0 && base + 2 < W);
       }
-      if constexpr (PRO) {
-        if (more) rg = dw_raw(pro, goff + (size_t)(q + 1) * C, true);
-      } else {
-        if (more) ng = *(const bf16x8*)(grow + (size_t)(q + 1) * C);
-      }
+      if (more) ng = *(const bf16x8*)(grow + (size_t)(q + 1) * C);
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
@@ -508,10 +421,7 @@ MA_DEV void dw_wgrad_body(const bf16* dy, const bf16* x, float* dw, int N, int H
         }
         win[rr][2] = n2[rr];
       }
-      if constexpr (PRO)
-        g = more ? dw_apply(rg, kp, pro.act, true) : g;   // after this column's FMAs
-      else
-        g = ng;
+      g = ng;
     }
   }
   float* mine = part + threadIdx.x * WG_LD;
@@ -544,19 +454,17 @@ __global__ __launch_bounds__(DT) void dw_wgrad_kernel(const bf16* dy, const bf16
 
 // dgrad + wgrad of one depthwise conv in ONE launch (they read the same dy and are
 // independent): blocks [0, nwg) are wgrad column segments, the rest dgrad strips
-template <int S, bool BW, bool PRO = false>
+template <int S, bool BW>
 __global__ __launch_bounds__(DT) void dw_bwd_kernel(const bf16* dy, const bf16* x, const float* w,
                                                     bf16* dx, float* dw, int N, int H, int W,
                                                     int C, int P, int Q, int pad, int QS,
-                                                    float* slab, int nwg, DwBw bw, DwPro pro) {
+                                                    float* slab, int nwg, DwBw bw) {
   extern __shared__ float part[];
-  float* coef = part + DT * WG_LD;     // PRO: [3][C] BN-backward coefficients of dy
-  if constexpr (PRO) dw_pro_coef(pro, C, coef);
   if ((int)blockIdx.x < nwg)
-    dw_wgrad_body<S, PRO>(dy, x, dw, N, H, W, C, P, Q, pad, QS, slab, part, blockIdx.x, pro, coef);
+    dw_wgrad_body<S>(dy, x, dw, N, H, W, C, P, Q, pad, QS, slab, part, blockIdx.x);
   else
-    dw_dgrad_body<S, BW, PRO>(dy, w, dx, N, H, W, C, P, Q, pad, bw, part, blockIdx.x - nwg,
-                              gridDim.x - nwg, pro, coef);
+    dw_dgrad_body<S, BW>(dy, w, dx, N, H, W, C, P, Q, pad, bw, part, blockIdx.x - nwg,
+                         gridDim.x - nwg);
 }
 
 // the partials reduce of several depthwise wgrads in one launch (blockIdx.z = layer): the
@@ -668,47 +576,32 @@ int dwconv_wgrad_blocks(int N, int P, int Q, int C) {
 
 void dwconv_bwd_launch(const bf16* dy, const bf16* x, const float* w, bf16* dx, float* dw, int N,
                        int H, int W, int C, int P, int Q, int stride, int pad, float* slab,
-                       const DwBw* bw, bool reduce, hipStream_t st, const DwPro* pro) {
+                       const DwBw* bw, bool reduce, hipStream_t st) {
   const int QS = dw_qs(N, P, Q, C);
   const int nwg = dwconv_wgrad_blocks(N, P, Q, C);
   const long long dtotal = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
   long long ndg = (dtotal + DT - 1) / DT;
   if (bw && ndg > 256) ndg = 256;
-  // >= the dgrad's [DT][ST_LD]; PRO: + [3][C] coefficients
-  const size_t shm = (size_t)DT * WG_LD * sizeof(float) + (pro ? (size_t)3 * C * sizeof(float) : 0);
-  if (shm > 160 * 1024) throw std::runtime_error("dwconv_bwd: prologue coefficients exceed LDS");
+  const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // >= the dgrad's [DT][ST_LD]
   static const bool attr = [] {
     const void* ks[] = {(const void*)dw_bwd_kernel<1, false>, (const void*)dw_bwd_kernel<1, true>,
-                        (const void*)dw_bwd_kernel<2, false>, (const void*)dw_bwd_kernel<2, true>,
-                        (const void*)dw_bwd_kernel<1, false, true>,
-                        (const void*)dw_bwd_kernel<1, true, true>,
-                        (const void*)dw_bwd_kernel<2, false, true>,
-                        (const void*)dw_bwd_kernel<2, true, true>};
+                        (const void*)dw_bwd_kernel<2, false>, (const void*)dw_bwd_kernel<2, true>};
     for (const void* k : ks)
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
   const DwBw none{};
-  const DwPro nopro{};
   const dim3 grid((unsigned)(nwg + ndg));
-#define DW_B(S_, BW_, PRO_) hipLaunchKernelGGL((dw_bwd_kernel<S_, BW_, PRO_>), grid, dim3(DT), shm, st, \
-                                               dy, x, w, dx, dw, N, H, W, C, P, Q, pad, QS, slab, \
-                                               nwg, bw ? *bw : none, pro ? *pro : nopro)
-  if (pro) {
-    if (stride == 1) {
-      if (bw) DW_B(1, true, true);
-      else DW_B(1, false, true);
-    } else {
-      if (bw) DW_B(2, true, true);
-      else DW_B(2, false, true);
-    }
-  } else if (stride == 1) {
-    if (bw) DW_B(1, true, false);
-    else DW_B(1, false, false);
+#define DW_B(S_, BW_) hipLaunchKernelGGL((dw_bwd_kernel<S_, BW_>), grid, dim3(DT), shm, st, dy, x, \
+                                         w, dx, dw, N, H, W, C, P, Q, pad, QS, slab, nwg,          \
+                                         bw ? *bw : none)
+  if (stride == 1) {
+    if (bw) DW_B(1, true);
+    else DW_B(1, false);
   } else {
-    if (bw) DW_B(2, true, false);
-    else DW_B(2, false, false);
+    if (bw) DW_B(2, true);
+    else DW_B(2, false);
   }
 #undef DW_B
   if (reduce) {

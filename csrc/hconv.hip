@@ -1,5 +1,6 @@
-// Halo-tile implicit-GEMM convolution with the producer's BatchNorm fused into the operand
-// staging (reference conv/BN/ReLU stack `pytorch_model.py:19-36,72-97`).
+// Halo-tile implicit-GEMM convolution, the persistent variants with the producer's BatchNorm
+// fused into the operand staging (reference conv/BN/ReLU stack
+// `pytorch_model.py:19-36,72-97`).
 //
 // Why a halo tile.  The generic implicit GEMM (igemm.hip) gathers every input pixel once per
 // filter tap: a 3x3 conv moves 9x its input through each CU's vector-memory path.  Here a
@@ -7,19 +8,17 @@
 // it needs for one 64-channel slice is a small rectangle (the halo), staged into LDS ONCE and
 // read by every tap at a uniform pixel offset; per tap only the BN x 64 weight tile streams in.
 //
-// Why the BN goes here.  A ResNet block's BatchNorm (+ residual, + shortcut BatchNorm) and
-// ReLU are elementwise on the conv INPUT, and a halo stages each input element exactly once:
-// applying scale/shift + activation there costs one FMA/max per element, not 9.  The activation
-// is also written back once (``keep``) where the training backward or the next residual needs
-// it, by the blocks of the first N tile, for the pixels that tile owns.
+// Why the BN goes here.  A ResNet block's intra-block BatchNorm and ReLU are elementwise on the
+// conv INPUT, and a halo stages each input element exactly once: applying scale/shift +
+// activation there costs one FMA/max per element, not 9 (the persistent kernels' MODE 1, the
+// scoring pass; the per-tile kernel below runs plain input: its staged BN modes measured
+// slower than a bn_apply pass, profiles/r2/ab_fuse_bn_halo.json, and were removed).
 //
 // Pipeline (everything global -> LDS is LDS-DMA, `global_load_lds_dwordx4`, so no VGPR ever
 // holds a tile in flight and every wait is an explicit counted `s_waitcnt vmcnt`):
 //   * weights: a 3-slot ring, the tile of step s + 2 issued while step s computes;
 //   * halo: slice c + 1's raw halo is issued in pieces during taps 0..T-3 of slice c into the
 //     second halo buffer (single-slice tiles use one buffer, two blocks share a CU instead);
-//   * MODE > 0: at a slice start the raw halo is normalised IN PLACE in LDS (+ residual / +
-//     shortcut BN loaded to registers, + activation, + the kept activation written once);
 //   * one barrier per step (a ring slot is rewritten only after every wave left it).
 // Issue counts per step are uniform by construction (halo pieces past the last load the zero
 // page into a dump area), so each wait is one of four immediates.
@@ -45,44 +44,6 @@ constexpr int HRMAX = 16;    // halo DMA pieces per wave (32 pixels per piece ov
 // kernel-uniform selector compiled to two scalar branches per element (255 in one halo
 // transform, ~3x the transform's cost)
 MA_DEV void act_bounds(int act, float& lo, float& hi) { act_clamp_bounds(act, lo, hi); }
-
-// per-channel scale / shift of one BatchNorm for 8 channels (same arithmetic as bn.hip), in two
-// halves so the 16-byte loads can be issued a whole slice before they are needed
-struct BnRaw {
-  f32x4 a0, a1, b0, b1, g0, g1, e0, e1;   // (sum | mean), (sumsq | var), gamma, beta
-};
-
-MA_DEV BnRaw bn_load(const float* stats, const float* rmean, const float* rvar,
-                     const float* gamma, const float* beta, int C, int g, int ch) {
-  BnRaw r;
-  const float* a = stats ? stats + (size_t)g * 2 * C + ch : rmean + ch;
-  const float* b = stats ? stats + (size_t)g * 2 * C + C + ch : rvar + ch;
-  r.a0 = *(const f32x4*)a;
-  r.a1 = *(const f32x4*)(a + 4);
-  r.b0 = *(const f32x4*)b;
-  r.b1 = *(const f32x4*)(b + 4);
-  r.g0 = *(const f32x4*)(gamma + ch);
-  r.g1 = *(const f32x4*)(gamma + ch + 4);
-  r.e0 = *(const f32x4*)(beta + ch);
-  r.e1 = *(const f32x4*)(beta + ch + 4);
-  return r;
-}
-
-MA_DEV void bn_finish(const BnRaw& r, bool batch, float inv_count, float eps, float (&sc)[8],
-                      float (&sh)[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float a = k < 4 ? r.a0[k] : r.a1[k - 4], b = k < 4 ? r.b0[k] : r.b1[k - 4];
-    const float gm = k < 4 ? r.g0[k] : r.g1[k - 4], be = k < 4 ? r.e0[k] : r.e1[k - 4];
-    float mean = a, var = b;
-    if (batch) {
-      mean = a * inv_count;
-      var = fmaxf(b * inv_count - mean * mean, 0.f);
-    }
-    sc[k] = gm * rsqrtf(var + eps);
-    sh[k] = be - mean * sc[k];
-  }
-}
 
 // 16 bytes per lane, global -> LDS (`global_load_lds_dwordx4`), lane l landing at the wave-uniform
 // LDS address + 16 l.  Issued from inline asm on purpose: the compiler models LDS-DMA as an LDS
@@ -112,10 +73,10 @@ MA_DEV void bar_raw() { asm volatile("s_barrier" ::: "memory"); }
 // ... after this wave's LDS writes have completed
 MA_DEV void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, int BN, int WM, int MODE>
+template <int BM, int BN, int WM>
 __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ src,
                                                       const bf16* __restrict__ wt, HconvGeom g,
-                                                      EpiParams e, HconvPro pro) {
+                                                      EpiParams e) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr int BI = BN / 32;                       // weight DMA pieces per wave per step
@@ -144,8 +105,6 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   const int nsl = cb1 - cb0;
   const int nst = nsl * T;
   const int Kt = T * g.C;
-  const bf16* zp = g.zero;
-  (void)zp;
   const int HR = (g.HPIX + 31) >> 5;                // DMA pieces per wave for a whole halo
   const int HBYTES = HR * 32 * 128;
   const int NH = g.chunks_per_split > 1 ? 2 : 1;
@@ -153,11 +112,9 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   const int lc = (lane & 7) ^ (lane >> 3);          // logical chunk this lane fetches
 
   // ---- halo slots of this thread: slot j is pixel (tid >> 3) + 32 j; source element offset
-  // of its logical chunk lc in slice 0 (or -1: padding / beyond the batch), and whether the
-  // pixel belongs to this tile (activation write-back)
+  // of its logical chunk lc in slice 0 (or -1: padding / beyond the batch)
   int hsrc[HRMAX];
   const bf16* hptr[HRMAX];                          // DMA source of slice 0 (zero rows for pads)
-  unsigned own = 0;
   const int per_img = g.HT * g.HWP;
   const int h0 = p0 * g.stride - g.pad;
 #pragma unroll
@@ -178,17 +135,11 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
       }
       const int h = h0 + hr * g.HS, ww = hc * g.HS - g.pad, n = n0i + img;
       ok = ok && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
-      if (ok) {
-        hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + lc * 8;
-        // the tile owns input rows [p0*stride, (p0+TR)*stride) of its images (all columns)
-        if (h >= p0 * g.stride && h < (p0 + g.TR) * g.stride) own |= 1u << i;
-      }
+      if (ok) hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + lc * 8;
     }
   }
 #pragma unroll
   for (int i = 0; i < HRMAX; ++i) hptr[i] = hsrc[i] >= 0 ? src + hsrc[i] : g_hzero + lc * 8;
-  const bool keep = MODE > 0 && pro.keep != nullptr && nt == 0;   // host: only when owned = all
-  const int grp = MODE > 0 ? n0i / pro.group_imgs : 0;
 
   // ---- A-fragment rows of this lane: LDS pixel of tap (0, 0) for each fragment
   int apix[TM];
@@ -231,71 +182,6 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
     dma16(hptr[j] + cb * 64, v ? s_halo + buf * HBYTES + (32 * j + 8 * wu) * 128 : s_dump);
   };
 
-  // ---- in-place BN (+ residual / shortcut BN) + activation of a landed raw halo
-  // BN coefficients of this thread's 8 channels (logical chunk lc) of slice cb: loaded one
-  // slice ahead (kernel start for the first), so their latency hides under the DMA / taps
-  BnRaw cr1{}, cr2{};
-  auto load_coef = [&](int cb) {
-#ifdef HC_NO_COEF
-    return;
-#endif
-    if constexpr (MODE > 0) {
-      const int ch = cb * 64 + lc * 8;
-      cr1 = bn_load(pro.stats, pro.rmean, pro.rvar, pro.gamma, pro.beta, g.C, grp, ch);
-      if constexpr (MODE == 3)
-        cr2 = bn_load(pro.stats2, pro.rmean2, pro.rvar2, pro.gamma2, pro.beta2, g.C, grp, ch);
-    }
-  };
-  auto transform = [&](int cb, int buf) {
-#ifdef HC_NO_TRANSFORM
-    return;
-#endif
-    if constexpr (MODE > 0) {
-      float sc[8], sh[8], sc2[8], sh2[8];
-      bn_finish(cr1, pro.stats != nullptr, pro.inv_count, pro.eps, sc, sh);
-      if constexpr (MODE == 3)
-        bn_finish(cr2, pro.stats2 != nullptr, pro.inv_count, pro.eps, sc2, sh2);
-      char* hb = smem + buf * HBYTES + (tid >> 3) * 128 + (tid & 7) * 16;
-      float alo, ahi;
-      act_bounds(pro.act, alo, ahi);
-      constexpr int BATCH = 8;
-#pragma unroll
-      for (int i0 = 0; i0 < HRMAX; i0 += BATCH) {
-        if (i0 >= HR) break;
-        u32x4 r[BATCH];
-        if constexpr (MODE >= 2) {
-#pragma unroll
-          for (int j = 0; j < BATCH; ++j) {
-            const int o = hsrc[i0 + j];
-            const bf16* base = MODE == 2 ? pro.res : pro.y2;
-            r[j] = *(const u32x4*)(o >= 0 ? base + o + cb * 64 : zp);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < BATCH; ++j) {
-          const int i = i0 + j;
-          if (i < HR && (tid >> 3) + 32 * i < g.HPIX) {
-            u32x4* lp = (u32x4*)(hb + i * 4096);
-            const bf16x8 y = __builtin_bit_cast(bf16x8, *lp);
-            const bf16x8 rr = __builtin_bit_cast(bf16x8, r[j]);
-            bf16x8 o;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              float a = bf2f(y[k]) * sc[k] + sh[k];
-              if constexpr (MODE == 2) a += bf2f(rr[k]);
-              if constexpr (MODE == 3) a += bf2f(rr[k]) * sc2[k] + sh2[k];
-              o[k] = f2bf(fminf(fmaxf(a, alo), ahi));
-            }
-            // padding stays zero in ACTIVATION space (the conv pads the normalised input)
-            const u32x4 v = hsrc[i] >= 0 ? __builtin_bit_cast(u32x4, o) : u32x4{0u, 0u, 0u, 0u};
-            *lp = v;
-            if (keep && ((own >> i) & 1)) *(u32x4*)(pro.keep + hsrc[i] + cb * 64) = v;
-          }
-        }
-      }
-    }
-  };
-
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -308,7 +194,6 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
   unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
   if (nst > 0) {
-    load_coef(cb0);
     // prologue: the first slice's whole halo, then the weight tiles of steps 0 and 1
 #pragma unroll
     for (int j = 0; j < HRMAX; ++j)
@@ -323,16 +208,6 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
       bar_raw();
       if (cl == 0) MA_STAMP(1);
       MA_LAP(3, tl);
-      if constexpr (MODE > 0) {
-        transform(cb0 + cl, buf);
-        // compiler-VISIBLE drain of the transform's own memory ops (residual loads, kept-
-        // activation stores): left pending, the compiler's later register-reuse waits count
-        // only them, and -- the DMAs being invisible to it -- would drain the whole LDS-DMA
-        // ring at every tap
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-        if (cl + 1 < nsl) load_coef(cb0 + cl + 1);
-        bar_lds();
-      }
       const char* hb = smem + buf * HBYTES;
 #pragma unroll
       for (int t = 0; t < T; ++t) {
@@ -1511,9 +1386,9 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   return launch_persist_w<BM, BN, WM4, 4>(src, wt, g, e, pro, grid, st);
 }
 
-template <int BM, int BN, int WM, int MODE>
+template <int BM, int BN, int WM>
 void launch_one(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
-                const HconvPro& pro, dim3 grid, hipStream_t st) {
+                dim3 grid, hipStream_t st) {
   const int hbytes = ((g.HPIX + 31) >> 5) * 32 * 128;
   const int nh = g.chunks_per_split > 1 ? 2 : 1;
   const int main_bytes = nh * hbytes + NSLOT * BN * 128 + 4096;
@@ -1521,23 +1396,11 @@ void launch_one(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiPa
   const int bytes = main_bytes > red ? main_bytes : red;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)hconv_kernel<BM, BN, WM, MODE>,
+    (void)hipFuncSetAttribute((const void*)hconv_kernel<BM, BN, WM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((hconv_kernel<BM, BN, WM, MODE>), grid, dim3(NT), bytes, st, src, wt, g, e,
-                     pro);
-}
-
-template <int BM, int BN, int WM>
-void launch_mode(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
-                 const HconvPro& pro, dim3 grid, hipStream_t st) {
-  switch (pro.mode) {
-    case 1: launch_one<BM, BN, WM, 1>(src, wt, g, e, pro, grid, st); break;
-    case 2: launch_one<BM, BN, WM, 2>(src, wt, g, e, pro, grid, st); break;
-    case 3: launch_one<BM, BN, WM, 3>(src, wt, g, e, pro, grid, st); break;
-    default: launch_one<BM, BN, WM, 0>(src, wt, g, e, pro, grid, st); break;
-  }
+  hipLaunchKernelGGL((hconv_kernel<BM, BN, WM>), grid, dim3(NT), bytes, st, src, wt, g, e);
 }
 
 }  // namespace
@@ -1617,10 +1480,11 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
     HP_CASE(64, 64, 1, 0)
 #undef HP_CASE
   }
+  if (pro.mode != 0) return 0;      // the per-tile kernel stages plain input only
   const dim3 grid(gx, gy);
 #define HC_CASE(BM_, BN_, WM_)                                  \
   if (bm == BM_ && bn == BN_) {                                 \
-    launch_mode<BM_, BN_, WM_>(src, wt, g, e, pro, grid, st);   \
+    launch_one<BM_, BN_, WM_>(src, wt, g, e, grid, st);         \
     return 1;                                                   \
   }
   HC_CASE(256, 64, 4)

@@ -296,18 +296,6 @@ struct DwBw {                      // BN-backward reduce fused into the depthwis
 //   A = gamma * rstd, B = -A * rstd * mean(dz*xhat), Cc = A * (rstd * mean * mean(dz*xhat) -
 //   mean(dz)) -- bn.hip bn_bwd_apply's arithmetic rearranged; the sums come complete from the
 // producing dgrad's epilogue.  Block 0 writes that BN's dgamma / dbeta.
-struct DwPro {
-  const bf16* dout;                // grad wrt the BN's activation output
-  const bf16* out;                 // that activation (mask)
-  const bf16* y;                   // the BN's input (the dw conv's output)
-  const float* stats;              // [2][C] batch sums of y
-  const float* gamma;
-  const float* sums;               // [SUMS_R][3][C] fused BN-backward sums (complete)
-  float* dgamma;
-  float* dbeta;
-  float inv_count, eps;
-  int act;
-};
 void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C,
                          int P, int Q, int stride, int pad, hipStream_t st,
                          const DwBw* bw = nullptr);
@@ -320,7 +308,7 @@ constexpr int DW_RED_MAX = 24;
 int dwconv_wgrad_blocks(int N, int P, int Q, int C);
 void dwconv_bwd_launch(const bf16* dy, const bf16* x, const float* w, bf16* dx, float* dw, int N,
                        int H, int W, int C, int P, int Q, int stride, int pad, float* slab,
-                       const DwBw* bw, bool reduce, hipStream_t st, const DwPro* pro = nullptr);
+                       const DwBw* bw, bool reduce, hipStream_t st);
 void dwconv_wgrad_reduce_batch_launch(const float* const* slabs, float* const* dws, const int* Cs,
                                       const int* nblks, int n, hipStream_t st);
 void dwconv_wgrad_launch(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C,

@@ -165,9 +165,6 @@ class EngineOptions:
     dw_pro: bool = True
     # depthwise dgrad + wgrad in one launch, wgrad reduces batched (ab_dw_pair.json)
     dw_pair: bool = True
-    # the depthwise conv's output-BN backward applied in that conv's backward dy loads, no
-    # bn_bwd_apply pass (profiles/r4/ab_dw_bn_pro.json)
-    dw_bn_pro: bool = False
     # the classifier head's backward reduces the final BN's backward sums (ab_head_bw.json)
     head_bw: bool = True
     # stride-2 dgrad as four parity classes (ab_dgrad_s2.json)
@@ -192,10 +189,6 @@ class EngineOptions:
     # than the pass it saves (layer3 81.5 vs 57 us): 'row' 1.307 vs '1' 1.333 ms/step with the
     # layer1 + layer2 convs on the row-step kernel (profiles/r5/ab_persist_bn_scope.json)
     persist_bn: str = 'row'
-    # REJECTED path kept for re-measurement (off): the input BN (+ residual / shortcut BN) in
-    # the per-tile halo conv's staging ('1' / 'score' / 'train'; profiles/r2/ab_fuse_bn_halo.json:
-    # off 1.602, score 1.634, train 1.724 ms/step; profiles/r4/ab_rejected_remeasured.json)
-    fuse_bn_halo: str = '0'
 
     @classmethod
     def from_env(cls, base=None):

@@ -205,7 +205,6 @@ class NativeEngine(object):
         self.res_pro = o.fuse_bn_fwd and o.res_pro
         self.head_bw = o.head_bw
         self.dw_pair = o.dw_pair
-        self.fuse_bn_halo = o.fuse_bn_halo
         self.persist_bn = o.persist_bn if o.persist_bn in ('0', '1', 'row') else (
             '1' if str(o.persist_bn).lower() in ('true', 'on', 'yes') else '0')
         self._apply_globals()
@@ -412,13 +411,10 @@ class NativeEngine(object):
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
-                    # ... and the convs that take their input's BN in the halo staging
-                    fb = self.fuse_bn_halo == '1' or \
-                        self.fuse_bn_halo == ('train' if train else 'score')
-                    hb = hconv.fused_plan(sp) if fb else None
                     # scoring pass: an intra-block conv on the persistent kernel takes its
                     # input's BN + activation in the halo staging (no residual there)
-                    if hb is None and not train and group_imgs and self.persist_bn != '0' and \
+                    hb = None
+                    if not train and group_imgs and self.persist_bn != '0' and \
                             u is not blk.units[0] and u is not blk.shortcut:
                         hb = hconv.persist_bn_plan(sp, group_imgs,
                                                    row_only=self.persist_bn == 'row')
@@ -669,38 +665,27 @@ class NativeEngine(object):
                      group_rows=sp.group_rows or sp.M, act=act, eps=BN_EPS, running=running,
                      res=res, **kw)
 
-    # -- BatchNorm folded into the halo conv (csrc/hconv.hip MODE 1-3): a BN output that the
-    # next conv can stage itself stays "pending" -- (raw conv output, its BN unit, activation,
-    # identity residual or shortcut BN) -- and that conv applies it while loading its halo,
-    # writing the activation back once (``keep``) where the residual / shortcut / backward
-    # needs it.  Policy and plans: ``hconv.fuse_ok`` / ``m.plan[name, 'hconv_bn']``.
-    def _pending(self, u, y, act, res=None, unit2=None, y2=None):
-        return dict(unit=u, y=y, act=act, res=res, unit2=unit2, y2=y2)
+    # -- BatchNorm folded into the halo conv (csrc/hconv.hip persistent / row-step MODE 1, the
+    # scoring pass): an intra-block BN output that the next conv can stage itself stays
+    # "pending" -- (raw conv output, its BN unit, activation) -- and that conv applies it while
+    # loading its halo.  Plans: ``hconv.persist_bn_plan`` / ``m.plan[name, 'hconv_bn']``.
+    def _pending(self, u, y, act):
+        return dict(unit=u, y=y, act=act)
 
     def _can_take(self, m, u):
         return (u.name, 'hconv_bn') in m.plan and not u.depthwise
 
-    def _hconv_pending(self, m, u, pend, y, stats, keep):
+    def _hconv_pending(self, m, u, pend, y, stats):
         """conv ``u`` on the pending activation ``pend``: hconv with the BN applied in staging."""
         sp = m.spec[u.name]
         pu = pend['unit']
         su = m.spec[pu.name]
-        batch = m.train or m.group_imgs
         pro = dict(gamma=self._gamma(pu), beta=self._beta(pu), act=pend['act'], eps=BN_EPS,
-                   keep=keep, count=su.group_rows or su.M, group_imgs=m.group_imgs or m.N)
-        if batch:
+                   count=su.group_rows or su.M, group_imgs=m.group_imgs or m.N)
+        if m.train or m.group_imgs:
             pro['stats'] = m.stats[pu.name]
         else:
             pro.update(rmean=pu.bn.running_mean, rvar=pu.bn.running_var)
-        if pend['res'] is not None:
-            pro['res'] = pend['res']
-        if pend['unit2'] is not None:
-            u2 = pend['unit2']
-            pro.update(y2=pend['y2'], gamma2=self._gamma(u2), beta2=self._beta(u2))
-            if batch:
-                pro['stats2'] = m.stats[u2.name]
-            else:
-                pro.update(rmean2=u2.bn.running_mean, rvar2=u2.bn.running_var)
         hconv.hconv_fwd(pend['y'], self.w_krsc[u.name], y, sp, m.plan[u.name, 'hconv_bn'],
                         stats=stats, slab=m.slab,
                         bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
@@ -709,7 +694,7 @@ class NativeEngine(object):
         """Forward through all blocks; returns the final activation buffer."""
         x = m.input if x is None else x
         stats_on = m.train or m.group_imgs
-        pend = None          # the previous block's output, not yet materialised in x's buffer
+        pend = None          # an intra-block BN output the next conv applies in its staging
         nblk = len(self.lw.blocks)
         pool_bn = None       # BN + activation the block's max pool applies (scoring/eval stem)
         pgp = None           # the previous block's final BN (+ identity residual), applied by the
@@ -729,12 +714,9 @@ class NativeEngine(object):
                         self._dual_fwd(m, u, blk.shortcut, inp, stats_on)):
                     sc_done = True
                 elif pend is not None:
-                    # BN (+ residual / shortcut BN) + act of the input applied while staging;
-                    # ``keep`` materialises x (block input) for the residual, shortcut and
-                    # backward; intra-block activations are kept only for the backward
-                    keep = x if i == 0 else (m.buf[blk.units[i - 1].name, 'a'] if m.train
-                                             else None)
-                    self._hconv_pending(m, u, pend, y, st, keep)
+                    # the previous unit's BN + act applied while staging (scoring pass: nothing
+                    # reads the intra-block activation)
+                    self._hconv_pending(m, u, pend, y, st)
                     pend = None
                 else:
                     self._conv_fwd(m, u, inp, y, st, pro=pro)
@@ -773,14 +755,6 @@ class NativeEngine(object):
                         # the next block's first (pointwise) conv applies this BN (+ identity
                         # residual) + activation in its operand tiles and writes ``out``
                         pgp = dict(y=y, pro=pgd)
-                    elif (nb is not None and not blk.pool and nb.units and
-                            self._can_take(m, nb.units[0]) and
-                            blk.final_act in ('relu', 'relu6', 'none')):
-                        # the next block's first conv applies this BN (+ residual) and writes
-                        # ``out`` through its keep
-                        pend = self._pending(u, y, blk.final_act,
-                                             res=res if ru is None else None,
-                                             unit2=ru, y2=res if ru is not None else None)
                     elif (blk.pool and not m.train and res is None and
                           blk.final_act in ('relu', 'relu6', 'none')):
                         # scoring / eval (nothing reads the pre-pool activation): the pool
@@ -858,21 +832,11 @@ class NativeEngine(object):
         else:
             ops.conv_wgrad(dy, x, gw, sp, plan=m.plan[u.name, 'wgrad'])
 
-    def _dw_pro_ok(self, m, u):
-        """Does depthwise unit ``u``'s backward take its output BN's backward in its dy loads?"""
-        return (self.opts.dw_bn_pro and u.depthwise and self.dw_pair and m.dw_slab is not None and
-                u.act in ('relu', 'relu6', 'none') and u.K == u.C and u.K * 3 * 4 <= 32 * 1024)
-
-    def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None, bwpro=None):
+    def _conv_bwd(self, m, u, dy, x, dx, accumulate, bw=None):
         """Weight gradient, then the data gradient.  ``bw``: the dgrad epilogue also reduces
         the BN-backward sums of the unit feeding ``dx`` (returns True when it did, so the
         caller skips bn_bwd's reduce pass)."""
         sp = m.spec[u.name]
-        if bwpro is not None and not (u.depthwise and dx is not None and m.dw_slab is not None and
-                                      self.dw_pair):
-            # only the depthwise pair launch applies it: materialise dy the usual way instead
-            self._bn_bwd(m, u, bwpro['dout'], bwpro['out'], u.act, dy, reduce=False)
-            bwpro = None
         if (dx is not None and not u.depthwise and self.pair_bwd and sp.K % 8 == 0):
             if bw is not None and (sp.Cp != sp.C or not self.fuse_bn_bwd):
                 bw = None
@@ -896,9 +860,8 @@ class NativeEngine(object):
             # deferred to one batched launch: at the end of the backward, or (DP) before the
             # bucket all-reduce that carries this weight gradient (train_segments)
             defer = True
-            ops.dwconv_bwd(None if bwpro is not None else dy, x, self._pview(u.w_seg), dx, gw,
-                           sp.N, sp.H, sp.W, sp.C, sp.P, sp.Q, sp.stride, sp.pad, region, bw=bw,
-                           reduce=not defer, pro=bwpro)
+            ops.dwconv_bwd(dy, x, self._pview(u.w_seg), dx, gw, sp.N, sp.H, sp.W, sp.C, sp.P,
+                           sp.Q, sp.stride, sp.pad, region, bw=bw, reduce=not defer)
             if defer:
                 m.dw_pending.append((region, gw, sp.C, nblk))
             return bw is not None
@@ -987,7 +950,6 @@ class NativeEngine(object):
         last = units[-1]
         sc = blk.shortcut
 
-        bwpro = {}   # unit name -> its output BN's backward, applied by its own backward (DwPro)
         # the shortcut's backward runs in ONE launch with the last conv's (both start from the
         # block-final BN's backward; EngineOptions.dual_bwd)
         merge = (sc is not None and dx is not None and len(units) > 1 and
@@ -1019,19 +981,9 @@ class NativeEngine(object):
                 if merge and u is last:
                     fused = self._conv_bwd_sc(m, u, d, inp, da, bw, sc, x, dx)
                 else:
-                    fused = self._conv_bwd(m, u, d, inp, da, accumulate=False, bw=bw,
-                                           bwpro=bwpro.pop(u.name, None))
-                if fused and self._dw_pro_ok(m, prev):
-                    # prev is a depthwise conv: its backward applies this BN's backward to the
-                    # gradient as it loads it (DwPro) -- no bn_bwd_apply pass, no dy tensor
-                    bwpro[prev.name] = dict(
-                        dout=da, out=m.buf[prev.name, 'a'], y=m.buf[prev.name, 'y'],
-                        stats=m.stats[prev.name], gamma=self._gamma(prev),
-                        sums=m.buf[prev.name, 'sums'], dgamma=self._gamma(prev, True),
-                        dbeta=self._beta(prev, True), act=prev.act, eps=BN_EPS)
-                else:
-                    self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
-                                 m.buf[prev.name, 'dy'], reduce=not fused)
+                    fused = self._conv_bwd(m, u, d, inp, da, accumulate=False, bw=bw)
+                self._bn_bwd(m, prev, da, m.buf[prev.name, 'a'], prev.act,
+                             m.buf[prev.name, 'dy'], reduce=not fused)
             else:
                 acc = blk.identity or sc is not None
                 bw = None
@@ -1043,7 +995,7 @@ class NativeEngine(object):
                         bw = self._bw(m, pb.units[-1], m.buf[bi - 1, 'out'], pb.final_act,
                                       unit2=pb.shortcut)
                 fused = self._conv_bwd(m, u, d, inp, dx if u.need_dgrad else None,
-                                       accumulate=acc, bw=bw, bwpro=bwpro.pop(u.name, None))
+                                       accumulate=acc, bw=bw)
                 if fused:
                     m.prereduced[bi - 1] = True
 

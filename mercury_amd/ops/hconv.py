@@ -111,7 +111,7 @@ def row_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
     activation (no residual, no kept activation), no bias, whole tiles, ghost-BN groups made of
     whole tiles."""
     if pro is not None and any(pro.get(k) is not None for k in ('res', 'y2', 'keep')):
-        return False
+        return False      # rejected by _pro_args too
     if bias is not None or (bm, bn) not in ROW_TILES:
         return False
     if spec.stride != 1 or spec.R != 3 or spec.M % bm or spec.K % bn:
@@ -125,7 +125,7 @@ def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
     kernel): plain input or the input's BN + activation (no residual, no kept activation), no
     bias, whole tiles, ghost-BN groups made of whole tiles."""
     if pro is not None and any(pro.get(k) is not None for k in ('res', 'y2', 'keep')):
-        return False
+        return False      # rejected by _pro_args too
     if bias is not None or (bm, bn) not in PERSIST_TILES:
         return False
     if spec.M % bm or spec.K % bn:
@@ -376,60 +376,26 @@ def persist_bn_plan(spec: ConvSpec, group_imgs, row_only=False):
     return p
 
 
-def fused_plan(spec: ConvSpec):
-    """Plan for running this conv with its INPUT's BatchNorm (+ residual / shortcut BN) +
-    activation applied in the halo staging, or None (bn_apply pass + plain conv instead).
-    Measured (bench/hconv_sweep.py, hconv_bn vs igemm + bn_apply; profiles/r2/
-    hconv_sweep_bn_b*.jsonl): a win on every 3x3 shape at the train batch (32: 130.6 vs 146.9 us
-    over the ResNet-18 layers) and on the >= 256-channel shapes at the scoring batch (320:
-    layer3 55.0 vs 59.5, layer4 65.4 vs 72.9 us), a loss on the 64/128-channel scoring shapes.
-    The kept activation must cover the input exactly once (keep_ok)."""
-    if not supported(spec) or not keep_ok(spec):
-        return None
-    if spec.N > 64 and spec.C < 256:
-        return None
-    p = (MEASURED if spec.stride == 1 else MEASURED_S2).get((spec.N, spec.H, spec.C, spec.K))
-    if p is not None:
-        g = geometry_cached(spec, p[0], p[1])
-        if g is not None and lds_bytes(g, *p) <= LDS_MAX:
-            return p
-    return plan(spec)
-
-
 def _pro_args(pro, spec):
-    """HconvPro from a dict: mode (0 plain, 1 bn, 2 bn + res, 3 bn + bn2(y2)), the producer's
-    stats [G][2][C] (or rmean/rvar), gamma, beta, act, eps, count (pixels per stat group),
-    group_imgs, res / y2 (+ stats2 / rmean2 / rvar2 / gamma2 / beta2), keep."""
+    """HconvPro from a dict: the input's BatchNorm + activation (mode 1) -- the producer's stats
+    [G][2][C] (or rmean/rvar), gamma, beta, act, eps, count (pixels per stat group), group_imgs.
+    The persistent kernels take no residual, second BN or kept activation: the per-tile
+    kernel's staged modes that did (2, 3, keep) measured slower than a bn_apply pass
+    (profiles/r2/ab_fuse_bn_halo.json) and were removed in round 5."""
     if pro is None:
         return (0,) + (0,) * 13 + (1, 1.0, 1e-5, 0)
-    mode = 1
-    if pro.get('res') is not None:
-        mode = 2
-    if pro.get('y2') is not None:
-        mode = 3
-    n_in = spec.N * spec.H * spec.W * spec.C
-    for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta', 'stats2', 'rmean2', 'rvar2', 'gamma2',
-              'beta2'):
+    bad = [k for k in ('res', 'y2', 'keep') if pro.get(k) is not None]
+    if bad:
+        raise ValueError('hconv: the staged prologue takes no %s' % ', '.join(bad))
+    for k in ('stats', 'rmean', 'rvar', 'gamma', 'beta'):
         _chk(pro.get(k), torch.float32, 'pro.' + k)
-    for k in ('res', 'y2', 'keep'):
-        _chk(pro.get(k), torch.bfloat16, 'pro.' + k, n_in)
     if pro.get('stats') is None and pro.get('rmean') is None:
         raise ValueError('pro needs stats or running statistics')
-    if mode == 3 and pro.get('stats2') is None and pro.get('rmean2') is None:
-        raise ValueError('pro with y2 needs stats2 or running statistics 2')
     gi = pro.get('group_imgs') or spec.N
-    return (mode, ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')),
-            ptr(pro['gamma']), ptr(pro['beta']), ptr(pro.get('res')), ptr(pro.get('y2')),
-            ptr(pro.get('stats2')), ptr(pro.get('rmean2')), ptr(pro.get('rvar2')),
-            ptr(pro.get('gamma2')), ptr(pro.get('beta2')), ptr(pro.get('keep')), gi,
-            1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)), _ACT[pro.get('act')])
-
-
-def keep_ok(spec: ConvSpec):
-    """The kept activation covers every input pixel exactly once (stride-1 same conv, or a
-    padded 3x3 stride-2 conv whose halos tile the input)."""
-    return spec.R == 3 and spec.pad == 1 and spec.H == spec.P * spec.stride \
-        and spec.W == spec.Q * spec.stride
+    return (1, ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')),
+            ptr(pro['gamma']), ptr(pro['beta'])) + (0,) * 8 + (
+            gi, 1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)),
+            _ACT[pro.get('act')])
 
 
 def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab=None, pro=None):
@@ -459,8 +425,8 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
         raise ValueError('hconv: tile %dx%d does not fit this conv' % (bm, bn))
     if splits == 0 and not persistent_ok(spec, bm, bn, stats is not None, bias, pro):
         raise ValueError('hconv: the persistent plan does not take this conv')
-    if pro is not None and pro.get('keep') is not None and not keep_ok(spec):
-        raise ValueError('hconv: keep needs a padded 3x3 conv whose halos tile the input')
+    if pro is not None and splits != 0:
+        raise ValueError('hconv: only the persistent plans take the input BN in staging')
     if splits > 1:
         need = slab_bytes(spec.M, spec.K, bm, bn, splits)
         if slab is None or slab.numel() * slab.element_size() < need:

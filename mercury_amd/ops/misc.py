@@ -100,29 +100,12 @@ def dwconv_dgrad(dy, w, dx, N, H, W, C, P, Q, stride, pad, bw=None):
     lib().dwconv_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, P, Q, stride, pad, stream_ptr(), *ba)
 
 
-def dwconv_bwd(dy, x, w, dx, dw, N, H, W, C, P, Q, stride, pad, slab, bw=None, reduce=True,
-               pro=None):
+def dwconv_bwd(dy, x, w, dx, dw, N, H, W, C, P, Q, stride, pad, slab, bw=None, reduce=True):
     """Depthwise dgrad (+ fused BN-backward sums ``bw``, as dwconv_dgrad) and slab wgrad in
     ONE launch.  ``slab`` (fp32, >= dwconv_wgrad_slab_floats): the wgrad blocks' partials;
-    ``reduce=False`` leaves them for dwconv_wgrad_reduce_batch (dw is then not yet updated).
-    ``pro``: dict(dout, out, y, stats, gamma, sums, dgamma, dbeta, act, eps) -- the conv's
-    OUTPUT BatchNorm backward is applied to dy as it is loaded (``dy`` is then not read and may
-    be None; ``sums`` must be complete, e.g. from the producing dgrad's epilogue) and that BN's
-    dgamma / dbeta are written: the bn_bwd_apply pass it replaces (csrc/dwconv.hip DwPro)."""
+    ``reduce=False`` leaves them for dwconv_wgrad_reduce_batch (dw is then not yet updated)."""
     _chk(slab, torch.float32, 'slab', dwconv_wgrad_slab_floats(N, P, Q, C))
-    pa = (0, 0, 0, 0, 0, 0, 0, 0, 0.0, 0.0, 0)
-    if pro is not None:
-        n_out = N * P * Q * C
-        for k in ('dout', 'out', 'y'):
-            _chk(pro[k], torch.bfloat16, 'pro.' + k, n_out)
-        for k in ('stats', 'gamma', 'dgamma', 'dbeta'):
-            _chk(pro[k], torch.float32, 'pro.' + k, 2 * C if k == 'stats' else C)
-        _chk(pro['sums'], torch.float32, 'pro.sums', int(getattr(lib(), 'SUMS_R', 1)) * 3 * C)
-        pa = (ptr(pro['dout']), ptr(pro['out']), ptr(pro['y']), ptr(pro['stats']),
-              ptr(pro['gamma']), ptr(pro['sums']), ptr(pro['dgamma']), ptr(pro['dbeta']),
-              1.0 / (N * P * Q), float(pro.get('eps', 1e-5)), _ACT[pro.get('act')])
-    else:
-        _chk(dy, torch.bfloat16, 'dy', N * P * Q * C)
+    _chk(dy, torch.bfloat16, 'dy', N * P * Q * C)
     ba = (0, 0, 0, 0, 0.0, 0.0, 0)
     if bw is not None:
         n_in = N * H * W * C
@@ -135,7 +118,7 @@ def dwconv_bwd(dy, x, w, dx, dw, N, H, W, C, P, Q, stride, pad, slab, bw=None, r
         ba = (ptr(bw['out']), ptr(bw['y']), ptr(bw['stats']), ptr(bw['sums']),
               1.0 / (N * H * W), float(bw.get('eps', 1e-5)), _ACT[bw.get('act')])
     lib().dwconv_bwd(ptr(dy), ptr(x), ptr(w), ptr(dx), ptr(dw), N, H, W, C, P, Q, stride, pad,
-                     ptr(slab), int(reduce), stream_ptr(), *ba, *pa)
+                     ptr(slab), int(reduce), stream_ptr(), *ba)
 
 
 def dwconv_wgrad_reduce_batch(items):

@@ -1116,54 +1116,6 @@ def test_dwconv_bwd_pair_matches_separate(stride, fused):
     close(ops.from_nhwc(dx1.view(N, H, H, C), C), xr.grad, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize('stride', [1, 2])
-@pytest.mark.parametrize('act', ['relu6', 'none'])
-def test_dwconv_bwd_output_bn_prologue(stride, act):
-    """dwconv_bwd(pro=...) applies the conv's OUTPUT BatchNorm backward to dy as it loads it
-    (no bn_bwd_apply pass): dx and dw match bn_bwd_apply -> dwconv_bwd, and that BN's dgamma /
-    dbeta match bn_bwd's (MobileNetV2: dw conv -> BN + ReLU6 -> project conv)."""
-    ops = _ops()
-    N, H, C = 8, 16, 96
-    P = (H + 2 - 3) // stride + 1
-    torch.manual_seed(5)
-    Mo = N * P * P
-    # the dw conv's output y, its BN (+ act) output a, and the gradient wrt a
-    y = bf(torch.randn(Mo, C, device=DEV) * 1.3 + 0.2).to(torch.bfloat16)
-    yf = y.float()
-    stats = torch.stack([yf.sum(0), yf.pow(2).sum(0)]).contiguous()
-    gamma = torch.rand(C, device=DEV) + 0.5
-    beta = torch.randn(C, device=DEV) * 0.2
-    a = torch.empty_like(y)
-    ops.bn_apply(y, stats.reshape(-1), gamma, beta, a, Mo, C, act=act)
-    da = bf(torch.randn(Mo, C, device=DEV) * 0.5).to(torch.bfloat16)
-    # complete BN-backward sums (what the project conv's dgrad epilogue reduces)
-    sums = torch.zeros(ops.sums_numel(C), device=DEV)
-    dyscr = torch.empty_like(y)
-    dg_ref = torch.zeros(C, device=DEV)
-    db_ref = torch.zeros(C, device=DEV)
-    ops.bn_bwd(da, a, y, stats.reshape(-1), gamma, sums, dyscr, Mo, C, act=act, eps=1e-5,
-               dgamma=dg_ref, dbeta=db_ref)
-    x = ops.to_nhwc(bf(torch.randn(N, C, H, H, device=DEV)))
-    wf = (torch.randn(C, 9, device=DEV) * 0.2).contiguous()
-    slab = torch.zeros(ops.dwconv_wgrad_slab_floats(N, P, P, C), device=DEV)
-    Mx = N * H * H
-    dx1 = torch.empty(Mx, C, dtype=torch.bfloat16, device=DEV)
-    dw1 = torch.zeros(C * 9, device=DEV)
-    ops.dwconv_bwd(dyscr, x, wf, dx1, dw1, N, H, H, C, P, P, stride, 1, slab)
-    dx2 = torch.empty_like(dx1)
-    dw2 = torch.zeros_like(dw1)
-    dg = torch.zeros(C, device=DEV)
-    db = torch.zeros(C, device=DEV)
-    slab.zero_()
-    ops.dwconv_bwd(None, x, wf, dx2, dw2, N, H, H, C, P, P, stride, 1, slab,
-                   pro=dict(dout=da, out=a, y=y, stats=stats, gamma=gamma, sums=sums, dgamma=dg,
-                            dbeta=db, act=act, eps=1e-5))
-    close(dx2.float(), dx1.float(), 2e-2, 2e-2)
-    close(dw2, dw1, 2e-2, 2e-2)
-    close(dg, dg_ref, 1e-5, 1e-5)
-    close(db, db_ref, 1e-5, 1e-5)
-
-
 @pytest.mark.parametrize('two', [False, True])
 def test_head_bwd_fused_bn_backward_reduce(two):
     """head_bwd(bw=...) reduces the final BN's backward sums from the activation gradient it
