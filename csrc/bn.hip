@@ -251,10 +251,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnBwdArgs a) {
   float mean[8], rstd[8], gm[8], sdz[8], sx[8], mean2[8], rstd2[8], gm2[8], sx2[8];
   mean_rstd8(a.stats + c, a.C, inv, a.eps, mean, rstd);
   load8(a.gamma + c, gm);
-  // (16-byte LDS reads: eight scalar reads at an 8-float lane stride were 8-way bank conflicts,
-  // 5.8-13.6 conflict cycles per LDS instruction in profiles/r4/pmc/final_step_pass.txt)
+  // (16-byte LDS reads, indexed as f32x4 so the compiler knows the alignment: eight scalar
+  // reads -- or ds_read2_b32 pairs when it could not prove base % 4 == 0 -- at an 8-float lane
+  // stride were 8-way bank conflicts, 5.8-13.6 conflict cycles per LDS instruction,
+  // profiles/r4/pmc/final_step_pass.txt)
   auto tot8 = [&](int base, float (&v)[8]) {
-    const f32x4 lo = *(const f32x4*)(tot + base), hi = *(const f32x4*)(tot + base + 4);
+    const f32x4* t4 = (const f32x4*)tot + (base >> 2);   // base = h * C + c, C % 8 == 0
+    const f32x4 lo = t4[0], hi = t4[1];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[k] = lo[k];

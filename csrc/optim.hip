@@ -170,7 +170,10 @@ __global__ __launch_bounds__(NT) void optimizer_fused_kernel(OptArgs a, const in
                                                              const long long* ewp, int new_) {
   const OptHyper h = opt_hyper(a);
   if ((int)blockIdx.x < njobs) {
+    // pitch 65 plus column XOR (row >> 3) * 4: the transposed reads (8 lanes down a column,
+    // 8 rows apart, 4 columns) hit 32 distinct banks; the row writes stay 2-way (free for b32)
     __shared__ float tile[64][65];
+    auto tcol = [](int r, int c) { return c ^ (((r >> 3) & 7) << 2); };
     const int* j = jobs + blockIdx.x * 4;
     const OptSeg sg = a.segs[j[0]];
     const int rs = j[1], k0 = j[2], c0 = j[3];
@@ -191,10 +194,10 @@ __global__ __launch_bounds__(NT) void optimizer_fused_kernel(OptArgs a, const in
         b[3] = f2bf(pn.w);
         *(bf16x4*)(sg.w_krsc + ((size_t)k * RS + rs) * sg.Cpad + c) = b;
       }
-      tile[r][tx * 4 + 0] = pn.x;
-      tile[r][tx * 4 + 1] = pn.y;
-      tile[r][tx * 4 + 2] = pn.z;
-      tile[r][tx * 4 + 3] = pn.w;
+      tile[r][tcol(r, tx * 4 + 0)] = pn.x;
+      tile[r][tcol(r, tx * 4 + 1)] = pn.y;
+      tile[r][tcol(r, tx * 4 + 2)] = pn.z;
+      tile[r][tcol(r, tx * 4 + 3)] = pn.w;
     }
     __syncthreads();
     // [C][R][S][K]: row (c, rs) holds k contiguous -> 8 chunks of 8 k per 64-k tile row
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(NT) void optimizer_fused_kernel(OptArgs a, const in
       if (cc < sg.C && kk < sg.K) {
         bf16x8 o;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) o[t] = f2bf(tile[kc + t][cr]);
+        for (int t = 0; t < 8; ++t) o[t] = f2bf(tile[kc + t][tcol(kc + t, cr)]);
         bf16* dst = sg.w_crsk + ((size_t)cc * RS + rs) * sg.K + kk;
         if (kk + 8 <= sg.K && (sg.K & 7) == 0) {
           *(bf16x8*)dst = o;
