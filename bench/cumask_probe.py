@@ -48,6 +48,8 @@ def main():
     ap.add_argument('--score-cus', type=int, default=0, help='CUs of the scoring stream (0: half)')
     ap.add_argument('--steps', type=int, default=300)
     ap.add_argument('--warmup', type=int, default=30)
+    ap.add_argument('--train-prio', type=int, default=0,
+                    help='priority of the train stream (-1: high; 0: the default stream)')
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -74,6 +76,8 @@ def main():
         ops._ROLE_STREAMS[(0, 0)] = {'score': masked_stream(torch, cus, sc),
                                      'comm': torch.cuda.Stream(dev)}
         train_s = masked_stream(torch, cus, tr)
+    if args.train_prio and train_s is None:
+        train_s = torch.cuda.Stream(dev, priority=args.train_prio)
     pre = PRESETS['resnet18-cifar10']
     hw, x_all, y_all = preset_data(pre)
     torch.manual_seed(1234)
@@ -96,7 +100,8 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) * 1e3 / args.steps
     eng.close()
-    print(json.dumps({'split': args.split, 'score_cus': S if args.split != 'none' else None,
+    print(json.dumps({'split': args.split, 'train_prio': args.train_prio,
+                      'score_cus': S if args.split != 'none' else None,
                       'cus': cus, 'ms_per_step': round(dt, 4)}), flush=True)
 
 
