@@ -18,7 +18,10 @@
 // mapping with 112-120 v_accvgpr_read/write per trip of the 16x16x32 loop (none in the 32x32x16
 // loop), which made the first version of this benchmark rank the 16x16x32 shape 1.3-1.65x slower
 // for that reason alone.  With the pin, the LDS=1 loops of both shapes are MFMA + ds_read only;
-// the LDS=0 16x16x32 loop still carries the copies (hipcc, loop-invariant operands) -- read LDS=1.
+// the LDS=0 16x16x32 loop still carries 56 v_accvgpr_read + 56 _write + 8 _mov per trip of
+// 32 MFMAs (hipcc, loop-invariant operands; opaque operands or VGPR pins leave 24-120 of them),
+// so its row (1,142 TF/s in profiles/r4/mfma_shape_bench.jsonl) measures the copies, not the
+// instruction -- compare the LDS=1 rows, where both loops are MFMA + ds_read only.
 #include "../common.h"
 
 namespace {
