@@ -24,6 +24,8 @@ def main():
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--shapes', default='0,1,2,3', help='indices into SHAPES')
     ap.add_argument('--plans', default='engine,row4,row8')
+    ap.add_argument('--pro', action='store_true',
+                    help="the input's ghost-BN + ReLU in the halo staging (MODE 1)")
     args = ap.parse_args()
     import torch
     from mercury_amd import ops
@@ -41,10 +43,16 @@ def main():
             wk, _ = ops.pack_conv_weight(torch.randn(K, C, 3, 3, device=dev) * 0.05)
             y = torch.empty(sp.M * K, dtype=torch.bfloat16, device=dev)
             stats = torch.zeros(10 * 2 * K, device=dev)
+            pro = None
+            if args.pro:
+                st_in = torch.rand(10 * 2 * C, device=dev) + 1.0
+                pro = dict(stats=st_in, gamma=torch.rand(C, device=dev) + 0.5,
+                           beta=torch.randn(C, device=dev) * 0.1, act='relu', eps=1e-5,
+                           count=32 * Hh * Hh, group_imgs=32)
             cur = H.engine_plan(sp)
             slab = torch.zeros(max(4, slab_bytes(sp.M, K, *cur[:3]) // 4 + 1), device=dev) \
                 if cur and cur[2] > 0 else None
-            row = {'shape': [N, Hh, C, K], 'grid': grid, 'gflop': round(2 * sp.M * K * 9 * C / 1e9, 2)}
+            row = {'shape': [N, Hh, C, K], 'grid': grid, 'pro': bool(args.pro), 'gflop': round(2 * sp.M * K * 9 * C / 1e9, 2)}
             cands = [('engine', cur)]
             bm = 256 if Hh >= 16 else 128
             cands += [('row4', (bm, 64, -1)), ('row8', (bm, 64, -2))]
@@ -56,8 +64,8 @@ def main():
                     row[name] = 'no-fit'
                     continue
                 try:
-                    us = gtime(lambda: H.hconv_fwd(x, wk, y, sp, p, stats=stats, slab=slab),
-                               reps=args.reps)
+                    us = gtime(lambda: H.hconv_fwd(x, wk, y, sp, p, stats=stats, slab=slab,
+                                                   pro=pro), reps=args.reps)
                 except Exception as e:  # noqa: BLE001
                     row[name] = 'error: %s' % e
                     continue

@@ -961,7 +961,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
     const int p0 = udiv24(m0 - n0i * PQ, g.Q, rq);
     const int h0 = p0 - g.pad;
     const int toff = (n0i * g.H + h0) * g.W * g.C * 2;
-    if constexpr (MODE == 1) hgrp = pro.stats ? n0i / pro.group_imgs : 0;
+    if constexpr (MODE >= 1) hgrp = pro.stats ? n0i / pro.group_imgs : 0;
 #pragma unroll
     for (int i = 0; i < HRC; ++i) {
       const int hr = (int)(hslot[i] >> 26);
@@ -969,12 +969,32 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
                     ? (hslot[i] & 0x3ffffffu) + (unsigned)toff : OOB;
     }
   };
-  // MODE 1: the input is the producer's raw conv output; its BatchNorm (ghost-group batch or
+  // MODE 1 / 2: the input is the producer's raw conv output; its BatchNorm (ghost-group batch or
   // running statistics) + activation is applied in LDS to each landed halo piece, once, by the
   // thread whose DMA brought it (8 channels lc of the slice: scale / shift loaded into registers
   // right before the transform, in the last row of the slice before).  Padding stays zero.
+  // MODE 1 loads the statistics from global memory per slice; MODE 2 (the launcher's choice when
+  // it fits: pro.coef_tab) reads scale / shift of the block's at most two statistics groups, ga
+  // and gb, from a table built once in the prologue into LDS after the weight ring --
+  // [2][C/8][scale 8 | shift 8] -- so the per-slice load is 4 LDS reads, not an exposed global
+  // round trip (layer 1 64.8 -> 62.1-62.6 us, layer 2 66.7-67.1 -> 60.2-60.4, profiles/r5/hrow_mode1)
   float csc[8], csh[8];
+  float* const ctab = (float*)(smem + 2 * HBYTES + (STAT ? 3 : 2) * WSLOT);
+  int ga = 0, gb = 0;
   auto load_coef = [&](int cb, int grp) __attribute__((always_inline)) {
+    if constexpr (MODE == 2) {
+      const int slot = __builtin_amdgcn_readfirstlane(grp == ga ? 0 : (g.C >> 3));
+      const f32x4* c = (const f32x4*)(ctab + (slot + cb * 8 + lc) * 16);
+      const f32x4 a = c[0], b2 = c[1], d = c[2], f = c[3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        csc[q] = a[q];
+        csc[4 + q] = b2[q];
+        csh[q] = d[q];
+        csh[4 + q] = f[q];
+      }
+      return;
+    }
     if constexpr (MODE == 1) {
       const int ch = cb * 64 + lc * 8;
       f32x4 a0, a1, b0, b1;
@@ -1006,7 +1026,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
     }
   };
   auto xform = [&](int hbuf) __attribute__((always_inline)) {
-    if constexpr (MODE == 1) {
+    if constexpr (MODE >= 1) {
       float lo, hi;
       act_bounds(pro.act, lo, hi);
 #pragma unroll
@@ -1107,8 +1127,33 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
   } else {
     issue_w(n0, 0, 0, 0);
   }
+  if constexpr (MODE == 2) {
+    int mA, nA, mB, nB;
+    tile_of(0, mA, nA);
+    tile_of(my - 1, mB, nB);
+    if (pro.stats) {
+      ga = __builtin_amdgcn_readfirstlane(udiv24(mA, PQ, rpq) / pro.group_imgs);
+      gb = __builtin_amdgcn_readfirstlane(udiv24(mB, PQ, rpq) / pro.group_imgs);
+    }
+    for (int i = tid; i < 2 * g.C; i += 64 * NW) {
+      const int sl = i >= g.C, c = i - sl * g.C, gi = sl ? gb : ga;
+      float mean, var;
+      if (pro.stats) {
+        mean = pro.stats[(size_t)gi * 2 * g.C + c] * pro.inv_count;
+        var = fmaxf(pro.stats[(size_t)gi * 2 * g.C + g.C + c] * pro.inv_count - mean * mean, 0.f);
+      } else {
+        mean = pro.rmean[c];
+        var = pro.rvar[c];
+      }
+      const float sc = pro.gamma[c] * rsqrtf(var + pro.eps);
+      float* t = ctab + (sl * (g.C >> 3) + (c >> 3)) * 16 + (c & 7);
+      t[0] = sc;
+      t[8] = pro.beta[c] - mean * sc;
+    }
+  }
   vm_wait<0>();
-  if constexpr (MODE == 1) {
+  if constexpr (MODE >= 1) {
+    if (MODE == 2) bar_lds();                     // the table is complete
     load_coef(0, hgrp);
     xform(0);
   }
@@ -1138,11 +1183,15 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
           vm_wait<ST>();                             // only the last tile's stores may be newer
           bar_lds();
         }
-        if (MODE == 1 && r == 2 && hd) {
+        if (MODE >= 1 && r == 2 && hd) {
           vm_wait<0>();                              // the next slice's halo has landed
           load_coef(cbD, hgrp);
           xform(buf ^ 1);
         }
+        // (plain input too: draining the next halo here, two rows after its first pieces were
+        // issued, instead of at the next slice's row 0 measured 54.0-54.5 -> 48.7 us on layer 1,
+        // profiles/r5/hrow_mode1)
+        if (MODE == 0 && r == 2 && hd) vm_wait<0>();
       } else {
         if (r == 0) {
           if (sig > 0) {
@@ -1151,10 +1200,10 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
             bar_lds();
           }
         } else {
-          if (hd && !(MODE == 1 && r == 2)) vm_wait<HH>();
+          if (hd && !(MODE >= 1 && r == 2)) vm_wait<HH>();
           else vm_wait<0>();
           bar_lds();
-          if (MODE == 1 && r == 2 && hd) {
+          if (MODE >= 1 && r == 2 && hd) {
             load_coef(cbD, hgrp);
             xform(buf ^ 1);
           }
@@ -1269,8 +1318,20 @@ template <int BM, int BN, int WM, int NW>
 int launch_hrow(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                 const HconvPro& pro, int grid, hipStream_t st) {
   const bool stat = g.C == 64 && g.K == BN;
-  const int bytes = hrow_lds_bytes<BM, BN, NW>(g, stat);
+  int bytes = hrow_lds_bytes<BM, BN, NW>(g, stat);
   if (bytes > 160 * 1024) return 0;
+  // MODE 1: the coefficient table when it fits beside the tile and a block's tile range touches
+  // at most two input statistics groups (N-tile-major ranges of <= one group's rows)
+  HconvPro pr = pro;
+  if (pro.mode == 1) {
+    const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
+    const int per = (ntiles + grid - 1) / grid;
+    const int grp_rows = pro.stats ? pro.group_imgs * g.P * g.Q : g.N * g.P * g.Q;
+    if (bytes + 2 * g.C * 8 <= 160 * 1024 && per * BM <= grp_rows) {
+      pr.coef_tab = 1;
+      bytes += 2 * g.C * 8;
+    }
+  }
   // halo pieces of wave 0 (the most): 8 covers the ResNet layer1 / layer2 scoring tiles (6);
   // larger halos spill at 2 waves per SIMD -- not instantiated
   const int hr = ((g.HPIX + 7) / 8 + NW - 1) / NW;
@@ -1279,11 +1340,13 @@ int launch_hrow(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiPa
 #define HR_CASE(H_)                                                                             \
   if (hrc == H_) {                                                                              \
     if (stat) {                                                                                 \
-      if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, true, 1>(src, wt, g, e, pro, grid, bytes, st); \
-      else launch_hrow_k<BM, BN, WM, NW, H_, true, 0>(src, wt, g, e, pro, grid, bytes, st);    \
+      if (pr.coef_tab) launch_hrow_k<BM, BN, WM, NW, H_, true, 2>(src, wt, g, e, pr, grid, bytes, st); \
+      else if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, true, 1>(src, wt, g, e, pr, grid, bytes, st); \
+      else launch_hrow_k<BM, BN, WM, NW, H_, true, 0>(src, wt, g, e, pr, grid, bytes, st);    \
     } else {                                                                                    \
-      if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, false, 1>(src, wt, g, e, pro, grid, bytes, st); \
-      else launch_hrow_k<BM, BN, WM, NW, H_, false, 0>(src, wt, g, e, pro, grid, bytes, st);   \
+      if (pr.coef_tab) launch_hrow_k<BM, BN, WM, NW, H_, false, 2>(src, wt, g, e, pr, grid, bytes, st); \
+      else if (pro.mode == 1) launch_hrow_k<BM, BN, WM, NW, H_, false, 1>(src, wt, g, e, pr, grid, bytes, st); \
+      else launch_hrow_k<BM, BN, WM, NW, H_, false, 0>(src, wt, g, e, pr, grid, bytes, st);   \
     }                                                                                           \
     return 1;                                                                                   \
   }

@@ -154,6 +154,7 @@ struct HconvPro {
   float inv_count;       // 1 / pixels per statistics group
   float eps;
   int act;               // 0 none, 1 relu, 2 relu6
+  int coef_tab = 0;      // (launcher-set) row-step kernel: BN coefficients from an LDS table
 };
 
 // returns 0 when (bm, bn) is not instantiated
