@@ -279,13 +279,6 @@ MEASURED = {
 MEASURED_IGEMM = {(32, 4, 512, 512)}
 
 
-# stride-2 3x3 convs (fused-BN use only): best plain plans of the same sweeps
-MEASURED_S2 = {
-    (32, 32, 64, 128): (64, 64, 1), (32, 16, 128, 256): (64, 64, 1),
-    (32, 8, 256, 512): (64, 64, 4), (320, 8, 256, 512): (64, 128, 1),
-}
-
-
 # Persistent-kernel winners (splits 0; bench/hconv_sweep.py at B=320, profiles/r2/
 # hconv_sweep_b320_persistent.jsonl): layer1 38.7 vs 53.9 us (best per-tile plan), layer2 35.4
 # vs 39.6, layer3 39.9 vs 40.9, the layer3 -> 4 stride-2 conv 33.6 vs igemm's 36.9 us.
@@ -297,7 +290,12 @@ MEASURED_PERSIST = {
     (32, 32, 64, 64): (256, 64, 0), (32, 16, 128, 128): (128, 64, 0),
     (32, 8, 256, 256): (64, 64, 0),
 }
-MEASURED_PERSIST_S2 = {(320, 8, 256, 512): (64, 64, 0)}
+# (the layer3 -> 4 stride-2 scoring conv left the persistent kernel in round 5: on igemm it runs
+# in one launch with its 1x1 shortcut (igemm_dual), 1.2922-1.2981 vs 1.2976-1.3026 ms/step,
+# scoring solo 1.013 vs 1.027-1.031 ms, profiles/r5/ab_l4_s2/ab.json)
+MEASURED_PERSIST_S2 = {}
+
+
 def _plan_override(key):
     """EngineOptions.hconv_plans = "N,H,C,K=bm,bn,splits;..." (A/B runs): a plan for that
     shape, or 'none' for igemm.  Returns (found, plan)."""
