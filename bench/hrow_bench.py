@@ -4,7 +4,7 @@ ResNet-18 scoring-pass stride-1 3x3 shapes (B = 320, 10 ghost-BN groups), graph-
     python bench/hrow_bench.py [--grids 128,256]
 
 One JSON line per (shape, grid): microseconds per conv for the engine's current plan, the
-row-step plans (4 and 8 waves), and TF/s."""
+row-step plan (256 x 64 tiles, 8 waves), and TF/s."""
 import argparse
 import json
 import os
@@ -23,7 +23,7 @@ def main():
     ap.add_argument('--grids', default='128,256')
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--shapes', default='0,1,2,3', help='indices into SHAPES')
-    ap.add_argument('--plans', default='engine,row4,row8')
+    ap.add_argument('--plans', default='engine,row4')
     ap.add_argument('--pro', action='store_true',
                     help="the input's ghost-BN + ReLU in the halo staging (MODE 1)")
     args = ap.parse_args()
@@ -55,7 +55,7 @@ def main():
             row = {'shape': [N, Hh, C, K], 'grid': grid, 'pro': bool(args.pro), 'gflop': round(2 * sp.M * K * 9 * C / 1e9, 2)}
             cands = [('engine', cur)]
             bm = 256 if Hh >= 16 else 128
-            cands += [('row4', (bm, 64, -1)), ('row8', (bm, 64, -2))]
+            cands += [('row4', (bm, 64, -1))]
             for name, p in cands:
                 if p is None or name not in args.plans.split(','):
                     continue

@@ -195,17 +195,25 @@ ROW_CASES = [
 ]
 
 
-@pytest.mark.parametrize('with_stats', [True, False, 'bn', 'bn_eval'])
+@pytest.mark.parametrize('with_stats', [True, False, 'bn', 'bn_eval', 'bn_grid4'])
 @pytest.mark.parametrize('case', ROW_CASES)
 def test_hconv_row_step(case, with_stats):
     """Row-step persistent plan (splits < 0, csrc/hconv.hip hrow_kernel): one filter row per
     pipeline step, weights stationary in LDS when C = K = 64 -- output and ghost-BN sums vs
     torch fp32, and the output bit-identical to the persistent kernel's (same MFMA order per
-    output: every tap's two 32-deep halves in the same sequence)."""
+    output: every tap's two 32-deep halves in the same sequence).  'bn' / 'bn_eval': the input's
+    BN from the per-block LDS coefficient table (MODE 2); 'bn_grid4': a 4-block grid, so a
+    block's tile range spans more than two ghost-BN groups and the kernel loads the statistics
+    per slice instead (MODE 1)."""
     from mercury_amd import ops
     from mercury_amd.ops import hconv as H
     from mercury_amd.ops.conv import ConvSpec
     ops.lib()
+    grid4 = with_stats == 'bn_grid4'
+    if grid4:
+        if not case[-1]:
+            pytest.skip('one statistics group: the table always fits')
+        with_stats = 'bn'
     N, Hh, C, K, (bm, bn), splits, gimgs = case
     spec = ConvSpec(N, Hh, Hh, C, K, 3, 3, 1, 1)
     G = N // gimgs if gimgs else 1
@@ -240,8 +248,14 @@ def test_hconv_row_step(case, with_stats):
     xn = ops.to_nhwc(x.to(DEV))
     out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
-    H.hconv_fwd(xn, wk, out, spec, (bm, bn, splits), stats=ostats, pro=pro)
-    torch.cuda.synchronize()
+    if grid4:
+        ops.lib().hconv_configure(4, H.persist_waves())
+    try:
+        H.hconv_fwd(xn, wk, out, spec, (bm, bn, splits), stats=ostats, pro=pro)
+        torch.cuda.synchronize()
+    finally:
+        if grid4:
+            ops.lib().hconv_configure(H._CFG['grid'], H.persist_waves())
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
     assert not torch.isnan(got).any()
     close(got, ref)
