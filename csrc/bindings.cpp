@@ -192,9 +192,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("hconv", [](uintptr_t src, uintptr_t wt, uintptr_t out, uintptr_t bias, uintptr_t stats,
                     int group_rows, uintptr_t slab, const std::vector<int>& geo, int bm, int bn,
                     int splits, uintptr_t st, int mode, uintptr_t p_stats, uintptr_t p_rmean,
-                    uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, uintptr_t p_res,
-                    uintptr_t p_y2, uintptr_t p_stats2, uintptr_t p_rmean2, uintptr_t p_rvar2,
-                    uintptr_t p_gamma2, uintptr_t p_beta2, uintptr_t p_keep, int p_group_imgs,
+                    uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, int p_group_imgs,
                     float p_inv_count, float p_eps, int p_act) {
     if (geo.size() != 19) throw std::invalid_argument("hconv: geometry needs 19 ints");
     HconvGeom g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9],
@@ -204,10 +202,8 @@ PYBIND11_MODULE(_C, m) {
     EpiParams e{P<bf16>(out), K, P<const float>(bias), P<float>(stats), K, group_rows, 0,
                 P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
     HconvPro pr{mode, P<const float>(p_stats), P<const float>(p_rmean), P<const float>(p_rvar),
-                P<const float>(p_gamma), P<const float>(p_beta), P<const bf16>(p_res),
-                P<const bf16>(p_y2), P<const float>(p_stats2), P<const float>(p_rmean2),
-                P<const float>(p_rvar2), P<const float>(p_gamma2), P<const float>(p_beta2),
-                P<bf16>(p_keep), p_group_imgs, p_inv_count, p_eps, p_act};
+                P<const float>(p_gamma), P<const float>(p_beta), p_group_imgs, p_inv_count, p_eps,
+                p_act};
     const int ok = hconv_launch(P<const bf16>(src), P<const bf16>(wt), g, e, pr, bm, bn, splits,
                                 S(st));
     if (!ok) throw std::invalid_argument("hconv: tile not instantiated");

@@ -1502,7 +1502,7 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   if (splits < 0) {
     // row-step persistent kernel (splits -1; 8 waves, 256 x 64 tiles): plain stride-1 input,
     // whole tiles, ghost-BN groups made of whole tiles
-    const bool ok = (pro.mode == 0 || (pro.mode == 1 && pro.keep == nullptr)) &&
+    const bool ok = (pro.mode == 0 || pro.mode == 1) &&
                     e.bias == nullptr && !e.accumulate &&
                     e.bw_sums == nullptr && g.stride == 1 && g.R == 3 && M % bm == 0 &&
                     g.K % bn == 0 && (e.stats == nullptr || e.group_rows % bm == 0);
@@ -1531,7 +1531,7 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   if (((g.HPIX + 31) >> 5) > HRMAX || g.R != 3) return 0;
   if (persist) {
     // persistent plan (splits == 0): plain whole tiles only, else the per-tile kernel below
-    const bool ok = (pro.mode == 0 || (pro.mode == 1 && pro.keep == nullptr)) &&
+    const bool ok = (pro.mode == 0 || pro.mode == 1) &&
                     e.bias == nullptr && !e.accumulate &&
                     e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
                     (e.stats == nullptr || e.group_rows % bm == 0);

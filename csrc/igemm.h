@@ -119,8 +119,9 @@ int conv_bwd_pair_launch(const bf16* dy, const bf16* wt, const ConvGeom& g, cons
 // Forward convolution whose A operand is a HALO TILE in LDS (hconv.hip): a block's output
 // tile is IMG whole images or TR whole output rows of one image, so the input it reads for
 // one 64-channel slice is a small rectangle, staged into LDS ONCE and read by every tap.
-// While staging, the producer's BatchNorm (+ residual / shortcut BN) + activation is applied
-// (HconvPro), so normalised activations never make a separate HBM round trip.
+// The persistent / row-step variants can apply the producer's BatchNorm + activation while
+// staging (HconvPro; the scoring pass's intra-block BN), so that normalised activation never
+// makes a separate HBM round trip.
 struct HconvGeom {
   int N, H, W, C;        // input NHWC (C padded to a multiple of 64)
   int P, Q, K;           // output pixels per image and channels
@@ -136,20 +137,12 @@ struct HconvGeom {
 };
 
 struct HconvPro {
-  int mode;              // 0 plain, 1 act(bn(y)), 2 act(bn(y) + res), 3 act(bn(y) + bn2(y2))
+  int mode;              // 0 plain input, 1 act(bn(y)) applied in the halo staging
   const float* stats;    // [G][2][C] batch / ghost-group sums of y, or null -> running stats
   const float* rmean;
   const float* rvar;
   const float* gamma;
   const float* beta;
-  const bf16* res;       // mode 2: residual, same NHWC shape as the input
-  const bf16* y2;        // mode 3: shortcut conv output, same shape
-  const float* stats2;
-  const float* rmean2;
-  const float* rvar2;
-  const float* gamma2;
-  const float* beta2;
-  bf16* keep;            // optional: the computed activation (same shape), written once
   int group_imgs;        // images per statistics group
   float inv_count;       // 1 / pixels per statistics group
   float eps;

@@ -378,10 +378,10 @@ def _pro_args(pro, spec):
     """HconvPro from a dict: the input's BatchNorm + activation (mode 1) -- the producer's stats
     [G][2][C] (or rmean/rvar), gamma, beta, act, eps, count (pixels per stat group), group_imgs.
     The persistent kernels take no residual, second BN or kept activation: the per-tile
-    kernel's staged modes that did (2, 3, keep) measured slower than a bn_apply pass
+    kernel's staged modes that did measured slower than a bn_apply pass
     (profiles/r2/ab_fuse_bn_halo.json) and were removed in round 5."""
     if pro is None:
-        return (0,) + (0,) * 13 + (1, 1.0, 1e-5, 0)
+        return (0, 0, 0, 0, 0, 0, 1, 1.0, 1e-5, 0)
     bad = [k for k in ('res', 'y2', 'keep') if pro.get(k) is not None]
     if bad:
         raise ValueError('hconv: the staged prologue takes no %s' % ', '.join(bad))
@@ -391,9 +391,8 @@ def _pro_args(pro, spec):
         raise ValueError('pro needs stats or running statistics')
     gi = pro.get('group_imgs') or spec.N
     return (1, ptr(pro.get('stats')), ptr(pro.get('rmean')), ptr(pro.get('rvar')),
-            ptr(pro['gamma']), ptr(pro['beta'])) + (0,) * 8 + (
-            gi, 1.0 / float(pro.get('count', 1)), float(pro.get('eps', 1e-5)),
-            _ACT[pro.get('act')])
+            ptr(pro['gamma']), ptr(pro['beta']), gi, 1.0 / float(pro.get('count', 1)),
+            float(pro.get('eps', 1e-5)), _ACT[pro.get('act')])
 
 
 def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab=None, pro=None):
