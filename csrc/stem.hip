@@ -184,9 +184,24 @@ int stem_fwd_launch(StemArgs a, hipStream_t st) {
   if (a.N <= 0 || a.P <= 0 || a.Q <= 0) return 1;
   const int tpi = ((a.P + ST_T - 1) / ST_T) * ((a.Q + ST_T - 1) / ST_T);
   // many more blocks than CU slots (no tail round), the rest as tiles per block (each block
-  // flushes its BN sums once: fewer blocks per group, less atomic contention)
-  int tpb = (tpi * a.N) / 4096;
+  // stages the weights once and flushes its BN sums once).  A 7x7 stem's weights are 3.5x a
+  // 3x3 one's, so it targets 4x fewer blocks; the tiles of an image are split evenly over its
+  // blocks (an uneven last block idles its CU); a 32x32 image (4 tiles) is one block when the
+  // batch alone fills the CUs.  bench/stem_bench.py, profiles/r5/stem_blocks: ResNet-50 B = 1280
+  // 1026 -> 844 us, B = 128 184 -> 125 us, CIFAR B = 320 30.1 -> 26.8 us, VGG unchanged.
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  int tpb = (tpi * a.N) / (a.R > 3 ? 1024 : 4096);
   tpb = tpb < 1 ? 1 : (tpb > tpi ? tpi : tpb);
+  if (tpi <= 4 && a.N >= cus) tpb = tpi;
+  const int bpi = (tpi + tpb - 1) / tpb;
+  tpb = (tpi + bpi - 1) / bpi;
   a.tpb = tpb;
   a.blocks_per_img = (tpi + tpb - 1) / tpb;
   if (a.group_imgs <= 0) a.group_imgs = a.N;
