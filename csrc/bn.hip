@@ -319,12 +319,24 @@ __global__ __launch_bounds__(NT) void bn_running_kernel(const BnRunEntry* tab, i
     const float* st = pass == 0 ? e.stats_train : e.stats_score;
     const int ng = pass == 0 ? e.n_train : e.n_score;
     const float cnt = pass == 0 ? e.cnt_train : e.cnt_score;
-    for (int g = 0; g < ng; ++g) {
-      const float s = st[(size_t)g * 2 * e.C + c], ss = st[(size_t)g * 2 * e.C + e.C + c];
-      const float mean = s / cnt;
-      const float var = fmaxf(ss / cnt - mean * mean, 0.f) * (cnt / fmaxf(cnt - 1.f, 1.f));
-      rm = (1.f - momentum) * rm + momentum * mean;
-      rv = (1.f - momentum) * rv + momentum * var;
+    // the groups' sums are loaded 8 at a time before the (sequential) momentum folds, so the
+    // loads of a batch are in flight together instead of one dependent round trip per group
+    for (int g0 = 0; g0 < ng; g0 += 8) {
+      float s8[8], ss8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const size_t o = (size_t)(g0 + j) * 2 * e.C + c;
+        s8[j] = g0 + j < ng ? st[o] : 0.f;
+        ss8[j] = g0 + j < ng ? st[o + e.C] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (g0 + j >= ng) break;
+        const float mean = s8[j] / cnt;
+        const float var = fmaxf(ss8[j] / cnt - mean * mean, 0.f) * (cnt / fmaxf(cnt - 1.f, 1.f));
+        rm = (1.f - momentum) * rm + momentum * mean;
+        rv = (1.f - momentum) * rv + momentum * var;
+      }
     }
   }
   e.rmean[c] = rm;
