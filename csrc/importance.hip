@@ -100,6 +100,33 @@ __global__ __launch_bounds__(256) void pool_build_kernel(PoolBuildArgs a) {
 constexpr int IS_T = 1024;
 constexpr int MAX_GROUPS = 1024;  // pool batches per pool
 constexpr int IS_LDS_MAX = 128 * 1024;   // dynamic LDS cap (static gsum[] rides on top)
+constexpr int IS_W = IS_T / 64;          // waves per block
+
+// Inclusive scan of one value per thread over the IS_T-thread block: a 64-lane shuffle scan per
+// wave, the IS_W wave totals scanned by wave 0, added back -- two barriers (a Hillis-Steele scan
+// over the block's LDS took 2 x log2(IS_T) = 20).  ``wt``: IS_W LDS slots of this call's own.
+template <typename T>
+MA_DEV T is_block_scan(T v, T* wt) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wt[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    T t = lane < IS_W ? wt[lane] : T(0);
+#pragma unroll
+    for (int o = 1; o < IS_W; o <<= 1) {
+      const T u = __shfl_up(t, o, 64);
+      if (lane >= o) t += u;
+    }
+    if (lane < IS_W) wt[lane] = t;
+  }
+  __syncthreads();
+  return w > 0 ? v + wt[w - 1] : v;
+}
 
 __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -160,14 +187,10 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
     p[i] = v;
     local += v;
   }
-  tsum[tid] = local;
+  __shared__ float wt_p[IS_W], wt_d[IS_W], wt_e[IS_W];
+  __shared__ int wt_c[IS_W];
+  tsum[tid] = is_block_scan(local, wt_p);
   __syncthreads();
-  for (int off = 1; off < IS_T; off <<= 1) {  // Hillis-Steele inclusive scan
-    const float add = tid >= off ? tsum[tid - off] : 0.f;
-    __syncthreads();
-    tsum[tid] += add;
-    __syncthreads();
-  }
   const float total = tsum[IS_T - 1];
   const int64_t dc = a.ctrl[1];
   if (a.alias) {
@@ -202,20 +225,10 @@ __global__ __launch_bounds__(IS_T) void is_sample_kernel(IsSampleArgs a) {
         he += v - 1.f;
       }
     }
-    ccnt[tid] = lc;
-    cdef[tid] = ld;
-    cexc[tid] = he;
+    ccnt[tid] = is_block_scan(lc, wt_c);
+    cdef[tid] = is_block_scan(ld, wt_d);
+    cexc[tid] = is_block_scan(he, wt_e);
     __syncthreads();
-    for (int off = 1; off < IS_T; off <<= 1) {
-      const int c_ = tid >= off ? ccnt[tid - off] : 0;
-      const float d_ = tid >= off ? cdef[tid - off] : 0.f;
-      const float e_ = tid >= off ? cexc[tid - off] : 0.f;
-      __syncthreads();
-      ccnt[tid] += c_;
-      cdef[tid] += d_;
-      cexc[tid] += e_;
-      __syncthreads();
-    }
     {
       int li = tid > 0 ? ccnt[tid - 1] : 0, hi = s0 - li;
       float dd = tid > 0 ? cdef[tid - 1] : 0.f, ee = tid > 0 ? cexc[tid - 1] : 0.f;
