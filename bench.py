@@ -106,7 +106,18 @@ def diagnostics(eng, steps, ws):
           # segmented replays)
           'comm_events': bool(eng._train_exec),
           'allreduce_ms_per_step': med.get('comm'), 'comm_exposed_ms': med.get('comm_exposed'),
-          'overlap_frac': med.get('overlap')}
+          'overlap_frac': med.get('overlap'),
+          # start-up timing of the engine's RCCL all-reduce and the bucket plan chosen from it
+          'calibration': eng.comm_calib,
+          # the cross-worker score all-gather on the score stream, device ms
+          'score_exchange': eng.score_exchange is not None,
+          'global_ema': bool(eng.global_ema and eng.score_exchange is not None),
+          'score_allgather_ms_per_step': med.get('score_xchg')}
+    if eng.dp and eng.comm is not None and eng.comm.size == 1 and \
+            not eng.opts.rccl_one_rank and eng.comm_kind == 'rccl':
+        # forced buckets on one GPU: the bucket plan, graph segments, event nodes and comm
+        # stream run as at W > 1, but RCCL's one-rank AVG (the identity) is skipped
+        dp['collective'] = 'none issued (one-rank AVG skipped; plumbing only)'
     torch.cuda.synchronize()
     if ws > 1:
         # every rank's communicator must span the whole job (one rank per GPU)
@@ -216,7 +227,11 @@ def main():
                            force_buckets=args.force_buckets, comm=args.comm,
                            wire_bf16=args.wire_bf16, sampler=args.sampler,
                            bucket_bytes=int(args.bucket_mb * (1 << 20)) or None,
-                           grad_compress=args.compress)
+                           grad_compress=args.compress,
+                           # under DP the north-star collective runs every step: the pool scores
+                           # all-gathered across ranks and one shared EMA normaliser
+                           exchange_scores=ws > 1 and args.sampler != 'groupwise',
+                           global_ema=ws > 1 and args.sampler != 'groupwise')
         eng.set_shard(x_all[idx], y_all[idx])
         if ws > 1:
             eng.broadcast_from(0)

@@ -375,7 +375,7 @@ void bn_bwd_launch(const BnBwdArgs& a, hipStream_t st) {
   // a.sums must be zero on entry (the engine zeroes one arena per step)
   const size_t chunks = (size_t)a.M * (a.C / 8);
   // 4 chunks per thread (one trip): measured at the MobileNetV2 train-batch shapes 4 / 8 / 16 /
-  // 32 / 64 chunks -> 179 / 186 / 218 / 295 / 453 us over the net (bench/small_bwd_bench.py):
+  // 32 / 64 chunks -> 179 / 186 / 218 / 295 / 453 us over the net (a round-3 probe, since removed):
   // the loop is latency-bound, not bound by the blocks' final atomics
   // activation and shortcut-BN presence are compile-time (runtime values made the per-element
   // code evaluate every activation form and select)

@@ -57,7 +57,7 @@ MA_DEV bf16x8 ld8(const bf16* p, bool ok) {
 constexpr int ST_LD = 17;   // floats per thread row of the forward's BN partials (odd stride)
 // LOOP: one statistics group (the train batch) on a capped grid that walks the strips (the
 // stride a multiple of C8, so a thread keeps its channels): fewer blocks add the BN sums, which
-// contend at the memory side (bench/stats_cost.py: B = 32 dw 96 ch 16.8 us with, 8.4 without)
+// contend at the memory side (profiles/r5/stats_cost/: B = 32 dw 96 ch 16.8 us with, 8.4 without)
 template <int S, bool PRO, bool LOOP>
 __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
   extern __shared__ float part[];  // [DT][ST_LD] per-thread BN partial sums (sum, sumsq)

@@ -1507,6 +1507,13 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
                     e.bw_sums == nullptr && g.stride == 1 && g.R == 3 && M % bm == 0 &&
                     g.K % bn == 0 && (e.stats == nullptr || e.group_rows % bm == 0);
     if (!ok) return 0;
+    // the kernel's address packing: a halo slot holds its byte offset within the tile's
+    // images in 26 bits and its halo row (63 = padding) above them, the tile base is an int and
+    // the buffer resource's byte count an unsigned (a plan override outside this contract
+    // falls back to the caller's other kernels instead of reading clamped addresses)
+    const long long tile_bytes = (long long)g.IMG * g.H * g.W * g.C * 2;
+    const long long in_bytes = (long long)g.N * g.H * g.W * g.C * 2;
+    if (g.HT >= 63 || tile_bytes >= (1ll << 26) || in_bytes >= (1ll << 31)) return 0;
     static int cus = 0;
     if (!cus) {
       int dev = 0;

@@ -179,6 +179,11 @@ class EngineOptions:
     # issue the RCCL all-reduce even on a one-rank communicator (forced buckets at W = 1; it is
     # the identity there -- the tests exercise RCCL with it, the bench measures without)
     rccl_one_rank: bool = False
+    # DP bucket plan from a start-up timing of the engine's RCCL all-reduce (parallel/buckets.py
+    # calibrate_allreduce): 'auto' when the engine chose the bucket size (W > 1, or W = 1 with
+    # rccl_one_rank), 'on' always (an explicit bucket_bytes still wins; the last-bucket size is
+    # taken from the calibration), 'off' never (16 MiB buckets, 1 MiB last bucket)
+    bucket_calib: str = 'auto'
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes

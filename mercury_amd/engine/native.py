@@ -163,10 +163,34 @@ class NativeEngine(object):
         self.grad_compress = grad_compress if grad_compress != 'none' else None
         self.tern = None                 # ternary-compressed all-reduce (parallel/compress.py)
         self._pg_works = []              # ProcessGroup works issued by the last step ('pg')
-        self._closed = False
-        LIVE.add(self)
+        self._closed = True              # (open once __init__ has finished: see its end)
         self._tern_ctr = 0
+        # DP verification hook (tests): grad_probe(stage, i, t) sees bucket i's gradient slice as
+        # the backward left it ('pre', on the stream that reduces it, before the collective) and
+        # the whole flat gradient the optimizer will read ('post', i = None, on the train stream
+        # before the tail).  Host-issued, so it sees every step, graphs or not.
+        self.grad_probe = None
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
+        # the last bucket (closed when the backward ends, so fully exposed) holds only the
+        # leading blocks' parameters up to this many bytes (bucket_plan)
+        self.last_bucket_bytes = 1 << 20
+        # measured all-reduce cost model (alpha, beta) and the plan derived from it: under DP on
+        # the engine's RCCL communicator the bucket sizes come from timing the real collective
+        # at start-up, not from an assumed link bandwidth (parallel/buckets.py)
+        self.comm_calib = None
+        cal = self.opts.bucket_calib
+        if cal not in ('auto', 'on', 'off'):
+            raise ValueError("EngineOptions.bucket_calib must be 'auto', 'on' or 'off'")
+        if self.comm is not None and comm == 'rccl' and grad_compress in (None, 'none') and (
+                cal == 'on' or (cal == 'auto' and bucket_bytes is None and
+                                (self.comm.size > 1 or self.opts.rccl_one_rank))):
+            from ..parallel.buckets import calibrate_allreduce, plan_from_calibration
+            self.comm_calib = calibrate_allreduce(self.comm, self.device)
+            bb, lb = plan_from_calibration(self.comm_calib)
+            if bucket_bytes is None:
+                self.bucket_bytes = bb
+            self.last_bucket_bytes = lb
+            self.comm_calib.update(bucket_bytes=self.bucket_bytes, last_bucket_bytes=lb)
         self.units = []
         for blk in self.lw.blocks:
             self.units += blk.units + ([blk.shortcut] if blk.shortcut else [])
@@ -225,10 +249,16 @@ class NativeEngine(object):
         self.global_ema = global_ema
         if self.dp and (exchange_scores or global_ema):
             from ..parallel.scores import ScoreExchange
-            # on the engine's own communicator when it has one: stream-ordered on the score
-            # stream, no ProcessGroup work in flight during a step or a capture
+            # on an RCCL communicator of its own when the engine has one: stream-ordered on the
+            # score stream, no ProcessGroup work in flight during a step or a capture, and not
+            # queued in front of the gradient buckets (RCCL runs one communicator's operations
+            # in issue order across streams, and the all-gather is issued first every step)
+            xc = None
+            if self.comm is not None:
+                from ..parallel.rccl import RcclComm
+                xc = RcclComm.shared(tag='score')
             self.score_exchange = ScoreExchange(self.P, self.device, force=world_size == 1,
-                                                comm=self.comm)
+                                                comm=xc)
         from .timing import StepTimer
         self.timer = StepTimer(self.device)   # per-phase device timing (off until enabled)
         self.wire = None
@@ -245,6 +275,10 @@ class NativeEngine(object):
             from ..parallel.compress import TernaryAllReduce
             cap = max(e - s_ for s_, e in self.bucket_plan().values())
             self.tern = TernaryAllReduce(cap, self.device, comm=self.comm, seed=seed)
+        # registered for close_all() only once fully built: a constructor that raised leaves
+        # nothing half-initialised for a later teardown to trip over
+        self._closed = False
+        LIVE.add(self)
 
     def _apply_globals(self):
         """The few EngineOptions that live in process-wide state (the halo-conv launcher's
@@ -1147,7 +1181,10 @@ class NativeEngine(object):
         if self.score_exchange is not None and self.scoring:
             # cross-worker importance-score all-gather, issued on the score stream
             # right after scoring; RCCL runs it beside the train backward
+            cs = torch.cuda.current_stream(self.device)
+            self.timer.mark('xchg0', cs)
             self.score_exchange.start(self.score_mode.losses)
+            self.timer.mark('xchg1', cs)
         if self._split_score:
             self.score_exchange.wait()          # stream-side wait on RCCL
             if graphs:
@@ -1231,6 +1268,13 @@ class NativeEngine(object):
         starts = self._block_starts()
         cuts = {}
         end = self.lw.total
+        # the last bucket: blocks 0 .. kl - 1, the largest leading run within last_bucket_bytes
+        # (a cut at block kl's start is forced; 0: no forced cut)
+        kl = 0
+        for k in range(1, len(starts)):
+            if starts[k] * 4 > self.last_bucket_bytes:
+                break
+            kl = k
         for bi in range(len(self.lw.blocks) - 1, -1, -1):
             blk = self.lw.blocks[bi]
             ustart = [min(s.off for s in (u.w_seg, u.g_seg, u.beta_seg)) for u in blk.units]
@@ -1242,7 +1286,8 @@ class NativeEngine(object):
                 if i > 0 and not inner:
                     continue
                 start = starts[bi] if i == 0 else ustart[i]
-                if (bi == 0 and i == 0) or (end - start) * 4 >= self.bucket_bytes:
+                if (bi == 0 and i == 0) or (end - start) * 4 >= self.bucket_bytes or (
+                        bi == kl and i == 0 and kl > 0 and end > start):
                     cuts[bi, i] = (0 if (bi == 0 and i == 0) else start, end)
                     end = start
         self._bucket_plan = cuts
@@ -1508,6 +1553,8 @@ class NativeEngine(object):
             prof.pop()
             prof.push('tail')
         T.mark('tail0', s0)
+        if self.grad_probe is not None and self.dp:
+            self.grad_probe('post', None, self.opt.g)
         if graphs:
             graphs['tail'].replay()
         else:
@@ -1526,6 +1573,8 @@ class NativeEngine(object):
         if self.tern is not None:
             self._tern_ctr += 1          # a fresh Philox stream per (step, bucket) (host path)
         if self.s_comm is None:          # torch ProcessGroup (gloo / CPU tests)
+            if self.grad_probe is not None:
+                self.grad_probe('pre', i, g)
             if self.tern is not None:
                 self.tern.allreduce(g, self._tern_ctr)
                 return None
@@ -1541,6 +1590,8 @@ class NativeEngine(object):
                 # the bucket's gradients are final: train segment si has ticked this step
                 self._order(slot=2, ref=3, mult=self._nseg, add=si + 1, ge=True, at=6)
             self.timer.bucket(i, 0, self.s_comm)
+            if self.grad_probe is not None:
+                self.grad_probe('pre', i, g)
             if self.xgmi is not None:
                 # direct two-shot over xGMI (all peers' exchange buffers mapped by IPC, device
                 # flag barriers); consecutive buckets alternate the two exchange slots; the bf16

@@ -14,6 +14,7 @@ each phase boundary is a HIP event recorded on the stream that runs the phase:
     tail   : BN running stats + optimizer + weight copies + next-batch gather
     comm_exposed : last all-reduce end - end of backward (> 0: communication on the
              critical path)
+    score_xchg : the cross-worker score all-gather on the score stream (0 when off)
 
 ``critical = max(score, train + wait) + tail`` reproduces ``step`` (the check printed by
 ``NativeTrainer`` at ``print_every``).  Events are pre-allocated; recording costs a few
@@ -67,6 +68,8 @@ class StepTimer(object):
                'tail': d('tail0', 'end')}
         comm = [ev[('b', i, 0)].elapsed_time(ev[('b', i, 1)]) for i in range(self._nb)]
         out['comm'] = sum(comm)
+        # the score all-gather's span on the score stream (DP with exchange_scores / global_ema)
+        out['score_xchg'] = d('xchg0', 'xchg1')
         out['comm_buckets'] = comm
         if self._nb:
             out['comm_exposed'] = max(0.0, d('train1', ('b', self._nb - 1, 1)))

@@ -116,6 +116,18 @@ def row_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
         return False
     if spec.stride != 1 or spec.R != 3 or spec.M % bm or spec.K % bn:
         return False
+    # the kernel's address arithmetic (csrc/hconv.hip hrow_kernel): a halo slot packs its byte
+    # offset inside the tile's images into 26 bits and its halo row into the 6 above (63 =
+    # padding), the tile base is an int, the buffer resource's size an unsigned
+    ts = _tile_shape(spec, bm)
+    if ts is None:
+        return False
+    img, tr = ts
+    halo_rows = (tr if img == 1 else spec.P) + 2
+    if halo_rows >= 63 or img * spec.H * spec.W * spec.C * 2 >= (1 << 26):
+        return False
+    if spec.N * spec.H * spec.W * spec.C * 2 >= (1 << 31):
+        return False
     grp = spec.group_rows or spec.M
     return not stats or grp % bm == 0
 

@@ -49,8 +49,77 @@ def default_bucket_bytes(world_size):
     One bucket is NOT better at W = 1 even though the bandwidth term is zero: RCCL's one-rank
     all-reduce is still a local pass over the bucket, and with one bucket it runs exposed after
     the backward (forced DP, same box: 1 bucket 1.480 ms, 16 MiB 1.437, non-DP 1.355,
-    profiles/r4/session_r4s27/)."""
+    profiles/r4/session_r4s27/).
+
+    The native engine replaces this model with measured numbers at start-up under DP
+    (``calibrate_allreduce`` + ``plan_from_calibration``); this constant is the fallback when
+    nothing was measured (ProcessGroup path, explicit sizes)."""
     return 16 << 20
+
+
+# sizes timed by calibrate_allreduce (fp32 elements): 256 KiB, 4 MiB, 16 MiB
+CALIB_SIZES = (1 << 16, 1 << 20, 1 << 22)
+
+
+def calibrate_allreduce(comm, device, sizes=CALIB_SIZES, reps=5):
+    """Time ``comm.allreduce`` (AVG, fp32) at a few sizes on a stream of its own and fit the
+    linear model T(S) = alpha + S / beta (S in bytes) by least squares.  Collective: every rank
+    of ``comm`` must call it.  Each size is issued once untimed, then ``reps`` times between two
+    events; the per-rank fits are averaged over the communicator and rank 0's rounding of them is
+    what every rank returns (the bucket plan built from them must be identical on every rank,
+    or the ranks would issue mismatched collectives).
+
+    Returns dict(alpha_us, beta_gbps, sizes_bytes, ms): ``ms`` the measured per-call times."""
+    import numpy as np
+    st = torch.cuda.Stream(device)
+    cur = torch.cuda.current_stream(device)
+    st.wait_stream(cur)
+    buf = torch.zeros(max(sizes), dtype=torch.float32, device=device)
+    ms = []
+    with torch.cuda.stream(st):
+        for n in sizes:
+            t = buf[:n]
+            comm.allreduce(t, avg=True)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                comm.allreduce(t, avg=True)
+            e1.record(st)
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1) / reps)
+    cur.wait_stream(st)
+    x = np.array([4.0 * n for n in sizes])
+    y = np.array(ms) * 1e-3
+    slope, icpt = np.polyfit(x, y, 1)
+    alpha = max(float(icpt), 1e-6)                  # a collective costs at least 1 us
+    beta = 1.0 / max(float(slope), 1e-15)           # bytes / s
+    fit = torch.tensor([alpha * 1e6, beta / 1e9], dtype=torch.float32, device=device)
+    if comm.size > 1:
+        with torch.cuda.stream(st):
+            comm.allreduce(fit, avg=True)
+            comm.broadcast(fit, 0)
+        st.synchronize()
+    a_us, b_gbps = (float(v) for v in fit.tolist())
+    return dict(alpha_us=round(a_us, 3), beta_gbps=round(b_gbps, 2),
+                sizes_bytes=[4 * n for n in sizes], ms=[round(m, 5) for m in ms])
+
+
+def plan_from_calibration(cal):
+    """(bucket_bytes, last_bucket_bytes) from a calibration (``calibrate_allreduce``).
+
+    * A bucket of S bytes costs alpha + S / beta; at S = 4 alpha beta the latency term is 20 %
+      of it.  Buckets of that size (clamped to [4, 32] MiB) keep the per-bucket fixed costs (one
+      more train-graph segment, the collective's latency) small against their transfer.
+    * The LAST bucket closes when the backward ends, so all of it is exposed: it holds only the
+      leading blocks' parameters (the ones the backward finishes last) up to alpha * beta bytes
+      (where the transfer term equals the latency; clamped to [0.5, 4] MiB) -- for ResNet-18 the
+      stem + layer1 (0.6 MB) or, on faster links, + layer2."""
+    ab = cal['alpha_us'] * 1e-6 * cal['beta_gbps'] * 1e9
+    mib = 1 << 20
+    bucket = int(min(max(4.0 * ab, 4 * mib), 32 * mib))
+    last = int(min(max(ab, mib // 2), 4 * mib))
+    return bucket, last
 
 
 class BucketedAllReduce(object):

@@ -16,8 +16,11 @@ This is independent of ``ProcessGroupNCCL``, so the engine can place a
 collective on any stream it owns (e.g. the score stream) without an extra
 ProcessGroup stream edge.
 
-Lifetime is explicit.  ``RcclComm.shared(group)`` hands out one communicator per
-torch.distributed group per process (engines share it); ``close()`` synchronises
+Lifetime is explicit.  ``RcclComm.shared(group, tag)`` hands out one communicator per
+(torch.distributed group, tag) per process (engines share it).  RCCL runs the operations of ONE
+communicator in issue order whatever stream they are issued on, so traffic that must not queue
+behind the gradient buckets -- the per-step score all-gather, issued on the score stream before
+the first bucket -- takes a communicator of its own (``tag='score'``).  ``close()`` synchronises
 the device and destroys it.  Nothing is destroyed from ``__del__``: a garbage
 collection pass can run at any point (inside another engine's construction, with
 collectives in flight on a stream), and ncclCommDestroy there aborted the process
@@ -39,10 +42,13 @@ class RcclComm(object):
     _shared = {}
 
     @classmethod
-    def shared(cls, group=None):
+    def shared(cls, group=None, tag=None):
+        """The process's communicator for (group, tag); creating one is collective over the
+        group (every rank must ask for the same tags in the same order)."""
         init = dist.is_initialized()
         key = (id(group) if group is not None else None,
-               dist.get_rank(group) if init else 0, dist.get_world_size(group) if init else 1)
+               dist.get_rank(group) if init else 0, dist.get_world_size(group) if init else 1,
+               tag)
         c = cls._shared.get(key)
         if c is None or not c.handle:
             c = cls._shared[key] = cls(group)

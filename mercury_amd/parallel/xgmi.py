@@ -144,22 +144,31 @@ class XgmiAllReduce(object):
         return t
 
     def close(self, sync_peers=True):
-        """Collective at W > 1 (every rank calls it): one last barrier so no peer is still
-        reading this rank's slots, then unmap the peers' buffers and free our own
+        """Collective at W > 1 ON THE NORMAL PATH (every rank calls it): one last barrier of
+        this exchange's kind -- whatever the kind, a peer may still be reading this rank's slot
+        in its all-gather -- then a device drain, then unmap the peers' buffers and free our own
         (``sync_peers=False``: the caller has synchronised the ranks on the host already).
-        Raises ``XgmiTimeout`` if a barrier of this exchange ever gave up on a peer."""
+
+        If a device barrier of this exchange ever gave up on a peer (the peer is gone or
+        desynchronised), nothing waits for it again: the mappings and the buffer are LEAKED
+        (freeing memory a live peer may still read would be a cross-GPU use-after-free, and a
+        host barrier with a vanished peer would block forever) and ``XgmiTimeout`` is raised."""
         L = lib()
         if not self.buf:
             return
-        if sync_peers and self.size > 1:
-            if self.barrier_kind == 'device':
-                self.barrier()
+        failed = bool(self._err.item()) if self.size > 1 else False
+        if sync_peers and self.size > 1 and not failed:
+            self.barrier()
             torch.cuda.synchronize(self.device)
-            if self._err.item():
-                # a peer is gone or desynchronised: fall back to the host barrier
-                dist.barrier(group=self.group)
+            failed = bool(self._err.item())
         torch.cuda.synchronize(self.device)
         err = int(self._err.item())
+        if failed:
+            self._opened = []
+            self.buf = 0
+            late = [q for q in range(32) if err >> q & 1]
+            raise XgmiTimeout('xgmi barrier: peers %s did not arrive within %.1f s (exchange '
+                              'buffers left mapped)' % (late, self.timeout_s))
         for p in self._opened:
             L.xgmi_ipc_close(p)
         self._opened = []

@@ -300,7 +300,14 @@ class Trainer(object):
                 self.train()
             stopped = self._stop()
             if self.epoch_step >= self.steps_per_epoch:
-                self.scheduler.step()
+                # resumed exactly at an epoch's end: this process has not stepped the optimizer
+                # yet, but the checkpointed run did -- advancing the restored schedule here
+                # reproduces the uninterrupted run's LR sequence (tests/test_resume.py), so
+                # torch's "scheduler before optimizer" warning does not apply
+                import warnings
+                with warnings.catch_warnings():
+                    warnings.filterwarnings('ignore', message='Detected call of `lr_scheduler')
+                    self.scheduler.step()
         for epoch in range(self.epoch + 1, epochs + 1):
             if stopped:
                 break

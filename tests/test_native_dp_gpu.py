@@ -195,8 +195,9 @@ def test_native_rccl_buckets_world1():
                 'tern': _engine(x, y, force_buckets=True, comm='rccl', grad_compress='ternary')}
         e = runs['rccl']
         assert e.comm is not None and e.comm.size == 1 and len(e.bucket_plan()) > 1
-        # the score all-gather rides the engine's own communicator: no ProcessGroup work
-        assert e.score_exchange.comm is e.comm
+        # the score all-gather rides an RCCL communicator of its own: no ProcessGroup work, and
+        # it does not queue in front of the gradient buckets
+        assert e.score_exchange.comm is not None and e.score_exchange.comm is not e.comm
         for name in ('rccl', 'bf16', 'xgmi', 'tern'):
             assert runs[name]._train_exec, name          # one chained train executable
         assert not runs['pg']._train_exec

@@ -115,7 +115,25 @@ def test_scoring_ghost_bn_matches_ten_separate_forwards(persist_bn, monkeypatch)
             ref.append(F.cross_entropy(o, sm.label[j * 32:(j + 1) * 32].long(), reduction='none'))
     ref = torch.cat(ref)
     assert _cos(sm.losses, ref) > 0.995
-    assert (sm.losses - ref).abs().mean().item() < 0.05
+    # the bound is what plain PyTorch reaches in bf16 on the same ten forwards (a per-sample
+    # bias would shift the sampling probabilities: bound the mean error AND the signed mean)
+    import copy
+    nb = copy.deepcopy(net).to(torch.bfloat16)
+    refb = []
+    with torch.no_grad():
+        for j in range(10):
+            o = nb(data[j * 32:(j + 1) * 32].to(torch.bfloat16)).float()
+            refb.append(F.cross_entropy(o, sm.label[j * 32:(j + 1) * 32].long(),
+                                        reduction='none'))
+    refb = torch.cat(refb)
+    err = (sm.losses - ref).abs().mean().item()
+    err_tb = (refb - ref).abs().mean().item()
+    bias = (sm.losses - ref).mean().item()
+    bias_tb = (refb - ref).mean().item()
+    print('ghost-BN scoring vs fp32: mean |err| %.5f (torch-bf16 %.5f), bias %.5f (torch-bf16 '
+          '%.5f)' % (err, err_tb, bias, bias_tb))
+    assert err <= max(2.5 * err_tb, 0.01), (err, err_tb)
+    assert abs(bias) <= max(2.5 * abs(bias_tb), 0.01), (bias, bias_tb)
 
 
 @pytest.mark.parametrize('graphs', [False, True])

@@ -61,12 +61,19 @@ def test_resume_at_epoch_boundary():
     part = _make(ck, max_samples=5)           # stops after the last step of epoch 1
     part.fit(2)
     rest = _make(tempfile.mkdtemp(), resume=os.path.join(ck, 'ckpt_rank{rank}.pt'))
-    rest.fit(2)
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        rest.fit(2)
+    assert not [x for x in w if 'lr_scheduler' in str(x.message)], [str(x.message) for x in w]
     full = _make(tempfile.mkdtemp())
     full.fit(2)
     assert [(s, e) for s, e, _ in part.log + rest.log] == [(s, e) for s, e, _ in full.log]
     assert [round(l, 12) for _, _, l in part.log + rest.log] == \
         [round(l, 12) for _, _, l in full.log]
+    # the first resumed step runs at epoch 2's LR, not epoch 1's again
+    assert rest.log[0][1] == 2 and abs(rest.log[0][2] - full.log[5][2]) < 1e-15
+    assert rest.log[0][2] != part.log[-1][2]
 
 
 def test_resume_path_resolution(tmp_path):
