@@ -117,15 +117,25 @@ DEFAULT_PMC = ['SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_VALU_MFMA_BUSY_CYCLES', '
                'SQ_INSTS_VALU', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_WAIT_INST_ANY']
 
 
+# MFMA utilisation pass (rocprofv3's MfmaUtil expression needs GRBM_GUI_ACTIVE beside the busy
+# cycles; without it the round-5 summaries read 0)
+MFMA_PMC = ['SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_INSTS_VALU_MFMA_MOPS_BF16', 'SQ_INSTS_MFMA',
+            'SQ_INSTS_VALU', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_WAIT_INST_LDS',
+            'SQ_WAVE_CYCLES', 'GRBM_GUI_ACTIVE']
+
+
 def job_pmc(o, a):
-    ctr = a.counters or DEFAULT_PMC
+    ctr = a.counters or (MFMA_PMC if a.mfma else DEFAULT_PMC)
     if sum(1 for c in ctr if c.startswith('SQ_')) > 8:
         raise SystemExit('at most 8 SQ counters per pass')
-    # (counters in their own pass, kernel trace only: no sys/runtime trace domains)
+    if sum(1 for c in ctr if c.startswith('GRBM_')) > 2:
+        raise SystemExit('at most 2 GRBM counters per pass')
+    bargs = shlex.split(a.args) if a.args else ['--steps', '10', '--warmup', '3', '--no-overhead']
+    # (counters in their own pass, kernel trace only: no sys/runtime trace domains; the profiler
+    # starts HIP before bench.py can raise the hardware-queue count)
     run(['timeout', '-s', 'KILL', '150', 'rocprofv3', '--pmc'] + ctr +
         ['--output-format', 'csv', '-d', os.path.join(o, 'p1'), '-o', 'run', '--', PY,
-         'bench.py', '--steps', '10', '--warmup', '3', '--no-overhead'],
-        os.path.join(o, 'p1.log'), 200)
+         'bench.py'] + bargs, os.path.join(o, 'p1.log'), 200, env={'GPU_MAX_HW_QUEUES': '16'})
     run([PY, 'bench/pmcsum.py', os.path.join(o, 'p1')], os.path.join(o, 'pmc_summary.txt'), 120)
     tail(os.path.join(o, 'pmc_summary.txt'), 30)
 
@@ -239,6 +249,7 @@ def main():
     ap.add_argument('--select', default='')
     ap.add_argument('--args', default='')
     ap.add_argument('--counters', nargs='*')
+    ap.add_argument('--mfma', action='store_true', help='pmc: the MFMA-utilisation counter pass')
     ap.add_argument('--env', nargs='*')
     ap.add_argument('--old', default='')
     ap.add_argument('--rounds', type=int, default=2)

@@ -194,10 +194,11 @@ PYBIND11_MODULE(_C, m) {
                     int splits, uintptr_t st, int mode, uintptr_t p_stats, uintptr_t p_rmean,
                     uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, int p_group_imgs,
                     float p_inv_count, float p_eps, int p_act) {
-    if (geo.size() != 19) throw std::invalid_argument("hconv: geometry needs 19 ints");
+    if (geo.size() != 20) throw std::invalid_argument("hconv: geometry needs 20 ints");
+    if (geo[19] < 0 || geo[19] > 7) throw std::invalid_argument("hconv: SWA in 0..7");
     HconvGeom g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9],
                 geo[10], geo[11], geo[12], geo[13], geo[14], geo[15], geo[16], geo[17], geo[18],
-                0, nullptr};
+                geo[19], 0, nullptr};
     const int K = geo[6];
     EpiParams e{P<bf16>(out), K, P<const float>(bias), P<float>(stats), K, group_rows, 0,
                 P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
@@ -468,10 +469,26 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd", [](uintptr_t act, uintptr_t w, uintptr_t b, uintptr_t label, uintptr_t isw,
                        uintptr_t pooled, uintptr_t logits, uintptr_t dlogits, uintptr_t losses,
                        uintptr_t meters, int B, int HW, int C, int classes, int mode, uintptr_t st,
-                       int score_kind) {
+                       int score_kind, uintptr_t bn_res, uintptr_t bn_stats, uintptr_t bn_rmean,
+                       uintptr_t bn_rvar, uintptr_t bn_gamma, uintptr_t bn_beta,
+                       float bn_inv_count, float bn_eps, int bn_group_imgs, int bn_act) {
     HeadArgs a{P<const bf16>(act), P<const float>(w), P<const float>(b), P<const int>(label),
                P<const float>(isw), P<float>(pooled), P<float>(logits), P<float>(dlogits),
                P<float>(losses), P<float>(meters), B, HW, C, classes, mode, 0, score_kind, 0};
+    if (bn_gamma) {
+      if (!pooled || C % 8 || bn_group_imgs <= 0 || (!bn_stats && !(bn_rmean && bn_rvar)))
+        throw std::invalid_argument("head_fwd: BN prologue needs pooled, C % 8 == 0, stats");
+      a.bn_res = P<const bf16>(bn_res);
+      a.bn_stats = P<const float>(bn_stats);
+      a.bn_rmean = P<const float>(bn_rmean);
+      a.bn_rvar = P<const float>(bn_rvar);
+      a.bn_gamma = P<const float>(bn_gamma);
+      a.bn_beta = P<const float>(bn_beta);
+      a.bn_inv_count = bn_inv_count;
+      a.bn_eps = bn_eps;
+      a.bn_group_imgs = bn_group_imgs;
+      a.bn_act = bn_act;
+    }
     head_fwd_launch(a, S(st));
     check_launch("head_fwd");
   });

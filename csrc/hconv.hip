@@ -124,6 +124,9 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
     if (i < HR && pix < g.HPIX) {
       const int img = pix / per_img, rem = pix - img * per_img;
       const int hr = rem / g.HWP, col = rem - hr * g.HWP;
+      // this lane's physical chunk (lane & 7) of pixel pix holds logical chunk
+      // (lane & 7) ^ swz(pix), swz(p) = (p + SWA * halo_row(p)) & 7 (pix & 7 == lane >> 3)
+      const int lcs = (lane & 7) ^ (((lane >> 3) + g.SWA * hr) & 7);
       int hc;
       bool ok;
       if (g.HALF) {
@@ -135,14 +138,14 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
       }
       const int h = h0 + hr * g.HS, ww = hc * g.HS - g.pad, n = n0i + img;
       ok = ok && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
-      if (ok) hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + lc * 8;
+      if (ok) hsrc[i] = ((n * g.H + h) * g.W + ww) * g.C + lcs * 8;
     }
   }
 #pragma unroll
   for (int i = 0; i < HRMAX; ++i) hptr[i] = hsrc[i] >= 0 ? src + hsrc[i] : g_hzero + lc * 8;
 
   // ---- A-fragment rows of this lane: LDS pixel of tap (0, 0) for each fragment
-  int apix[TM];
+  int apix[TM], aswz[TM];                           // aswz: p + SWA * halo_row at tap (0, 0)
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int row = wm * (BM / WM) + tm * 16 + (lane & 15);
@@ -151,6 +154,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
     const int hc = q * g.SR;
     const int col = g.HALF ? ((hc & 1) * g.HALF + (hc >> 1)) : hc;
     apix[tm] = img * per_img + tr * g.SR * g.HWP + col;
+    aswz[tm] = apix[tm] + g.SWA * tr * g.SR;
   }
   // weight rows this lane fetches (DMA piece j covers rows 8 * (w + 4 j) .. + 8)
   // (the host guarantees K % BN == 0: every weight row exists)
@@ -238,6 +242,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
         // MFMA phase: A from the halo at the tap's pixel offset, B from ring slot s % 3
         const int r = t / R, ss = t % R;
         const int toff = g.HALF ? r * g.HWP + (ss >> 1) + (ss & 1) * g.HALF : r * g.HWP + ss;
+        const int tsw = toff + g.SWA * r;                 // swizzle term of the tap's row
         const char* bs = ring + (t % NSLOT) * SLOT;
         // all 16 fragment reads of the tap first (both 32-deep halves in flight at once: one
         // wave per SIMD has no partner to hide LDS latency), then the MFMAs
@@ -253,7 +258,7 @@ __global__ __launch_bounds__(NT, 1) void hconv_kernel(const bf16* __restrict__ s
 #pragma unroll
           for (int tm = 0; tm < TM; ++tm) {
             const int p = apix[tm] + toff;
-            fa[kk][tm] = *(const bf16x8*)(hb + (p * 8 + (chunk ^ (p & 7))) * 16);
+            fa[kk][tm] = *(const bf16x8*)(hb + (p * 8 + (chunk ^ ((aswz[tm] + tsw) & 7))) * 16);
           }
         }
 #pragma unroll
@@ -1499,6 +1504,7 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   const int M = g.N * g.P * g.Q;
   const int gx = ((M + bm - 1) / bm) * ((g.K + bn - 1) / bn);
   const int nchunks = g.C >> 6;
+  if (splits <= 0 && g.SWA != 0) return 0;       // persistent / row-step halo images: SWA 0
   if (splits < 0) {
     // row-step persistent kernel (splits -1; 8 waves, 256 x 64 tiles): plain stride-1 input,
     // whole tiles, ghost-BN groups made of whole tiles

@@ -45,6 +45,57 @@ __global__ __launch_bounds__(NT) void head_pool_kernel(const bf16* act, float* p
   *(float4*)(o + 4) = make_float4(s[4] * inv, s[5] * inv, s[6] * inv, s[7] * inv);
 }
 
+// the pool with the final BN (+ identity residual) + activation applied on the fly (HeadArgs
+// bn_*; reference: the block output `pytorch_model.py:34-36` then avg_pool2d + flatten `:94-95`):
+// one thread per (sample, 8 channels), the raw conv output and the residual read once, each
+// element normalised exactly as bn_apply_kernel would (scale / shift from the ghost-group sums or
+// the running statistics) but kept in fp32 up to the mean
+__global__ __launch_bounds__(NT) void head_pool_bn_kernel(HeadArgs a) {
+  const int C8 = a.C >> 3;
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= a.B * C8) return;
+  const int b = i / C8, c = (i - b * C8) * 8;
+  float sc[8], sh[8];
+  {
+    float m8[8], v8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (a.bn_stats) {
+        const float* st = a.bn_stats + (size_t)(b / a.bn_group_imgs) * 2 * a.C + c + k;
+        m8[k] = st[0] * a.bn_inv_count;
+        v8[k] = fmaxf(st[a.C] * a.bn_inv_count - m8[k] * m8[k], 0.f);
+      } else {
+        m8[k] = a.bn_rmean[c + k];
+        v8[k] = a.bn_rvar[c + k];
+      }
+      sc[k] = a.bn_gamma[c + k] * rsqrtf(v8[k] + a.bn_eps);
+      sh[k] = a.bn_beta[c + k] - m8[k] * sc[k];
+    }
+  }
+  const float lo = a.bn_act ? 0.f : -3.4e38f, hi = a.bn_act == 2 ? 6.f : 3.4e38f;
+  const bf16* x = a.act + (size_t)b * a.HW * a.C + c;
+  const bf16* r = a.bn_res ? a.bn_res + (size_t)b * a.HW * a.C + c : nullptr;
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll 4
+  for (int hw = 0; hw < a.HW; ++hw) {
+    const bf16x8 v = *(const bf16x8*)(x + (size_t)hw * a.C);
+    bf16x8 rv;
+    if (r) rv = *(const bf16x8*)(r + (size_t)hw * a.C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = bf2f(v[k]) * sc[k] + sh[k];
+      if (r) t += bf2f(rv[k]);
+      s[k] += fminf(fmaxf(t, lo), hi);
+    }
+  }
+  const float inv = 1.f / (float)a.HW;
+  float* o = a.pooled + (size_t)b * a.C + c;
+  *(float4*)o = make_float4(s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv);
+  *(float4*)(o + 4) = make_float4(s[4] * inv, s[5] * inv, s[6] * inv, s[7] * inv);
+}
+
 // fp32 tiled GEMM for the wide head, C[m][n] = sum_r A(m, r) * B(n, r) (+ bias[n]), exact fp32
 // like the per-sample path: 64x64 output tile per block, 4x4 per thread, 16-deep r slices
 // through LDS with the next slice's global loads in flight during the current slice's FMAs.
@@ -214,6 +265,10 @@ __global__ __launch_bounds__(NT) void head_fwd_kernel(HeadArgs a) {
     const bf16* x = a.act + (size_t)b * a.HW * a.C;
     const float invhw = 1.f / (float)a.HW;
     for (int c = tid; c < a.C; c += NT) {
+      if (a.pooled_ready) {
+        pooled[c] = a.pooled[(size_t)b * a.C + c];
+        continue;
+      }
       float s = 0.f;
 #pragma unroll 8
       for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
@@ -312,6 +367,10 @@ __global__ __launch_bounds__(NT) void head_fc_chunk_kernel(HeadArgs a) {
   const bf16* x = a.act + (size_t)b * a.HW * a.C;
   const float invhw = 1.f / (float)a.HW;
   for (int c = tid; c < a.C; c += NT) {
+    if (a.pooled_ready) {
+      pooled[c] = a.pooled[(size_t)b * a.C + c];
+      continue;
+    }
     float s = 0.f;
 #pragma unroll 8
     for (int hw = 0; hw < a.HW; ++hw) s += bf2f(x[(size_t)hw * a.C + c]);
@@ -421,9 +480,16 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
   // wide heads: pool + fp32 tiled FC as their own launches (needs the pooled/logits workspaces);
   // the FC reduction is split over the channels so the launch fills the GPU (slices add into
   // the zeroed logits)
+  if (a.bn_gamma) {
+    // the final BN (+ residual) + activation in the pool: pooled[] first, then the FC
+    hipLaunchKernelGGL(head_pool_bn_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0,
+                       st, a);
+    a.pooled_ready = 1;
+  }
   if (wide && a.pooled && a.logits && a.C % 16 == 0) {
-    hipLaunchKernelGGL(head_pool_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0, st,
-                       a.act, a.pooled, a.B, a.HW, a.C);
+    if (!a.pooled_ready)
+      hipLaunchKernelGGL(head_pool_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0, st,
+                         a.act, a.pooled, a.B, a.HW, a.C);
     const int tiles = ((a.B + LT - 1) / LT) * ((a.classes + LT - 1) / LT);
     int z = 1;
     while (tiles * z * 2 <= 256 && a.C / (z * 2) >= 4 * LK) z *= 2;

@@ -132,6 +132,8 @@ struct HconvGeom {
                          // odd columns from HALF on (0 otherwise) -- both bank-conflict choices
   int HS, SR;            // input step per halo pixel; halo step per output pixel
   int HPIX;              // halo pixels per tile = IMG * HT * HWP
+  int SWA;               // halo chunk swizzle c ^ ((p + SWA * halo_row(p)) & 7); per-tile
+                         // kernel only (the persistent / row-step kernels need 0)
   int chunks_per_split;  // 64-channel input slices per K-split
   const bf16* zero;      // 16-byte zero page (set by the launcher)
 };

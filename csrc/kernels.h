@@ -80,6 +80,20 @@ struct HeadArgs {
   int log_softmax_input;         // logits are already log-probs (VGG) -> NLL
   int score_kind;                // losses[] holds 0: CE loss, 1: classifier-layer grad norm
   int logits_ready;              // (set by head_fwd_launch) pooled/logits already computed
+  // final BatchNorm (+ identity residual) + activation applied while pooling (scoring / eval:
+  // nothing else reads the last block's output): act is then the raw conv output y and
+  // pooled = mean_hw(act(bn(y) [+ bn_res])) -- no bn_apply pass over the last activation
+  const bf16* bn_res = nullptr;  // [B][HW][C] identity residual or null
+  const float* bn_stats = nullptr;   // [G][2][C] ghost-group sums (or null: running stats)
+  const float* bn_rmean = nullptr;
+  const float* bn_rvar = nullptr;
+  const float* bn_gamma = nullptr;   // non-null: the BN prologue is on
+  const float* bn_beta = nullptr;
+  float bn_inv_count = 0.f;
+  float bn_eps = 0.f;
+  int bn_group_imgs = 1;
+  int bn_act = 0;                // 0 none, 1 relu, 2 relu6
+  int pooled_ready = 0;          // (set by head_fwd_launch) pooled[] already written
 };
 void head_fwd_launch(const HeadArgs& a, hipStream_t st);
 void head_loss_launch(const HeadArgs& a, hipStream_t st);

@@ -179,6 +179,9 @@ class EngineOptions:
     # issue the RCCL all-reduce even on a one-rank communicator (forced buckets at W = 1; it is
     # the identity there -- the tests exercise RCCL with it, the bench measures without)
     rccl_one_rank: bool = False
+    # scoring / eval: the last block's BN (+ identity residual) + activation applied by the
+    # classifier head's average pool instead of a bn_apply pass over the last activation
+    head_bn: bool = True
     # DP bucket plan from a start-up timing of the engine's RCCL all-reduce (parallel/buckets.py
     # calibrate_allreduce): 'auto' when the engine chose the bucket size (W > 1, or W = 1 with
     # rccl_one_rank), 'on' always (an explicit bucket_bytes still wins; the last-bucket size is

@@ -728,6 +728,8 @@ class NativeEngine(object):
         """Forward through all blocks; returns the final activation buffer."""
         x = m.input if x is None else x
         stats_on = m.train or m.group_imgs
+        m.head_bn = None     # (set below when the head's pool applies the last block's BN)
+        x_last = None
         pend = None          # an intra-block BN output the next conv applies in its staging
         nblk = len(self.lw.blocks)
         pool_bn = None       # BN + activation the block's max pool applies (scoring/eval stem)
@@ -789,6 +791,22 @@ class NativeEngine(object):
                         # the next block's first (pointwise) conv applies this BN (+ identity
                         # residual) + activation in its operand tiles and writes ``out``
                         pgp = dict(y=y, pro=pgd)
+                    elif (nb is None and not m.train and not blk.pool and ru is None and
+                          self.opts.head_bn and self.lw.head_pool != 'mlp2' and
+                          blk.final_act in ('relu', 'relu6', 'none') and u.K % 8 == 0):
+                        # scoring / eval: nothing reads the last block's output but the head's
+                        # average pool, which applies this BN (+ identity residual) +
+                        # activation itself (ops.head_fwd ``bn``): no bn_apply pass
+                        hb = dict(gamma=self._gamma(u), beta=self._beta(u), act=blk.final_act,
+                                  eps=BN_EPS, res=res)
+                        if m.group_imgs:
+                            su = m.spec[u.name]
+                            hb.update(stats=m.stats[u.name], count=su.group_rows or su.M,
+                                      group_imgs=m.group_imgs)
+                        else:
+                            hb.update(rmean=u.bn.running_mean, rvar=u.bn.running_var)
+                        m.head_bn = hb
+                        x_last = y
                     elif (blk.pool and not m.train and res is None and
                           blk.final_act in ('relu', 'relu6', 'none')):
                         # scoring / eval (nothing reads the pre-pool activation): the pool
@@ -805,6 +823,8 @@ class NativeEngine(object):
                                True, m.buf.get((bi, 'argmax')), bn=pool_bn)
                 pool_bn = None
             x = m.buf[bi, 'out']
+        if m.head_bn is not None:
+            return x_last            # the raw last conv output: the head applies its BN
         return x
 
     # ------------------------------------------------------------------ speech-VGG head
@@ -840,12 +860,13 @@ class NativeEngine(object):
     def head(self, m, x, mode, isw=None, meters=None):
         if self.lw.head_pool == 'mlp2':
             return self._mlp_head(m, x, mode, isw=isw, meters=meters)
+        hb = getattr(m, 'head_bn', None) if mode != 'train' else None
         ops.head_fwd(x, self._pview(self.lw.fc_w), self._pview(self.lw.fc_b), m.label, m.N,
                      m.final_hw, m.final_C, self.classes, mode, pooled=m.pooled,
                      logits=m.logits,
                      dlogits=getattr(m, 'dlogits', None) if mode == 'train' else None,
                      losses=m.losses, isw=isw, meters=meters,
-                     score=self.score if mode == 'score' else 'loss')
+                     score=self.score if mode == 'score' else 'loss', bn=hb)
 
     def flush_dw_reduces(self, m):
         """The deferred depthwise wgrad reduces of this backward, in one launch."""

@@ -173,6 +173,7 @@ def _conflict_cycles(g, bm, bn):
     wm = _WM[bm, bn]
     TM = bm // (16 * wm)
     IMG, TR, Q, SR, HWP, HALF, R = g['IMG'], g['TR'], g['Q'], g['SR'], g['HWP'], g['HALF'], g['R']
+    swa = g.get('SWA', 0)
     per_img = g['HT'] * HWP
     cyc = 0
     for w in range(wm):
@@ -194,14 +195,22 @@ def _conflict_cycles(g, bm, bn):
                         for lane in grp:
                             p = pix[lane & 15] + toff
                             c = kk * 4 + (lane >> 4)
-                            u = (p * 8 + (c ^ (p & 7))) % 16
+                            sw = (p + swa * ((p % per_img) // HWP)) & 7
+                            u = (p * 8 + (c ^ sw)) % 16
                             seen[u] = seen.get(u, 0) + 1
                         cyc += max(seen.values())
     return cyc
 
 
-def geometry(spec: ConvSpec, bm, bn):
-    """HconvGeom as a dict (csrc/igemm.h), or None when this tile does not fit the conv."""
+def geometry(spec: ConvSpec, bm, bn, swa=False):
+    """HconvGeom as a dict (csrc/igemm.h), or None when this tile does not fit the conv.
+
+    The halo image stores pixel p's 64-channel slice as 8 16-byte chunks, logical chunk c at
+    slot c ^ swz(p) with swz(p) = (p + SWA * halo_row(p)) & 7.  The row pitch HWP and (for the
+    per-tile kernel, ``swa=True``) the row term SWA are chosen by the lane-group model so the
+    A-fragment reads are bank-conflict-free: for layer4's 4x4 images the pitch-6 image with
+    SWA = 0 costs 2x the ideal LDS cycles (PMC: 2.03 conflict cycles per LDS instruction in
+    hconv_kernel<128,128,2>), SWA = 6 none.  The persistent / row-step kernels take SWA = 0."""
     if not supported(spec) or (bm, bn) not in _WM:
         return None
     ts = _tile_shape(spec, bm)
@@ -225,27 +234,28 @@ def geometry(spec: ConvSpec, bm, bn):
             hp = IMG * HT * hwp
             if hp > HRMAX_PIX:
                 break
-            g.update(HWP=hwp, HALF=half, HPIX=hp)
-            c = _conflict_cycles(g, bm, bn)
-            key = (c, hp)
-            if best is None or key < best[0]:
-                best = (key, dict(g))
+            for sa in (range(8) if swa else (0,)):
+                g.update(HWP=hwp, HALF=half, HPIX=hp, SWA=sa)
+                c = _conflict_cycles(g, bm, bn)
+                key = (c, hp, sa)
+                if best is None or key < best[0]:
+                    best = (key, dict(g))
     return None if best is None else best[1]
 
 
 _GEO_CACHE = {}
 
 
-def geometry_cached(spec: ConvSpec, bm, bn):
+def geometry_cached(spec: ConvSpec, bm, bn, swa=False):
     key = (spec.N, spec.H, spec.W, spec.C, spec.K, spec.R, spec.stride, spec.pad,
-           spec.group_rows, bm, bn)
+           spec.group_rows, bm, bn, bool(swa))
     if key not in _GEO_CACHE:
-        _GEO_CACHE[key] = geometry(spec, bm, bn)
+        _GEO_CACHE[key] = geometry(spec, bm, bn, swa)
     return _GEO_CACHE[key]
 
 
 _ORDER = ('N', 'H', 'W', 'C', 'P', 'Q', 'K', 'R', 'stride', 'pad', 'IMG', 'TR', 'HT', 'HWd',
-          'HWP', 'HALF', 'HS', 'SR', 'HPIX')
+          'HWP', 'HALF', 'HS', 'SR', 'HPIX', 'SWA')
 
 
 def plan(spec: ConvSpec, min_blocks=256):
@@ -255,7 +265,7 @@ def plan(spec: ConvSpec, min_blocks=256):
     for bm in (256, 128, 64):
         if (bm, bn) not in _WM:
             continue
-        g = geometry_cached(spec, bm, bn)
+        g = geometry_cached(spec, bm, bn, swa=True)
         if g is None or lds_bytes(g, bm, bn, 1) > LDS_MAX:
             continue
         blocks = math.ceil(spec.M / bm) * math.ceil(spec.K / bn)
@@ -263,7 +273,7 @@ def plan(spec: ConvSpec, min_blocks=256):
             break
     else:
         return None
-    g = geometry_cached(spec, bm, bn)
+    g = geometry_cached(spec, bm, bn, swa=True)
     if g is None:
         return None
     blocks = math.ceil(spec.M / bm) * math.ceil(spec.K / bn)
@@ -337,7 +347,7 @@ def engine_plan(spec: ConvSpec, bias=False, train=None):
     if found and spec.H == spec.W:
         if p is None:
             return None
-        g = geometry_cached(spec, p[0], p[1])
+        g = geometry_cached(spec, p[0], p[1], swa=p[2] > 0)
         if g is not None and lds_bytes(g, *p) <= LDS_MAX and (p[2] != 0 or (
                 not bias and persistent_ok(spec, p[0], p[1]))):
             return p
@@ -360,7 +370,7 @@ def engine_plan(spec: ConvSpec, bias=False, train=None):
         return None
     p = MEASURED.get(key)
     if p is not None:
-        g = geometry_cached(spec, p[0], p[1])
+        g = geometry_cached(spec, p[0], p[1], swa=True)
         if g is not None and lds_bytes(g, *p) <= LDS_MAX:
             return p
     if spec.C >= 128:
@@ -418,7 +428,7 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
     if p is None:
         raise ValueError('hconv does not support this conv')
     bm, bn, splits = p[:3]
-    g = geometry_cached(spec, bm, bn)
+    g = geometry_cached(spec, bm, bn, swa=splits > 0)
     if splits < 0:
         if g is None or row_lds_bytes(g, bm, bn, splits) > LDS_MAX:
             raise ValueError('hconv: row-step tile %dx%d does not fit this conv' % (bm, bn))

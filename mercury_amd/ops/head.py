@@ -11,16 +11,35 @@ MODE = {'score': 0, 'train': 1, 'eval': 2}
 SCORE = {'loss': 0, 'gradnorm': 1}
 
 
+_ACT = {'none': 0, 'relu': 1, 'relu6': 2}
+
+
 def head_fwd(act, w, b, label, B, HW, C, classes, mode, pooled=None, logits=None, dlogits=None,
-             losses=None, isw=None, meters=None, score='loss'):
+             losses=None, isw=None, meters=None, score='loss', bn=None):
     """``score``: what score mode writes into ``losses`` -- 'loss' (per-sample CE, the
-    reference) or 'gradnorm' (exact per-sample gradient norm of the classifier layer)."""
+    reference) or 'gradnorm' (exact per-sample gradient norm of the classifier layer).
+
+    ``bn`` (scoring / eval): ``act`` is the last conv's raw output and the head pools
+    act(bn(act) [+ res]) -- dict(gamma, beta, eps, act, res=None, and stats + count +
+    group_imgs (ghost / batch statistics) or rmean + rvar (running)) -- instead of reading a
+    block output that a bn_apply pass wrote."""
     _chk(act, torch.bfloat16, 'act', B * HW * C)
     _chk(w, torch.float32, 'w', classes * C)
     _chk(label, torch.int32, 'label', B)
+    bnargs = (0, 0, 0, 0, 0, 0, 0.0, 0.0, 1, 0)
+    if bn is not None:
+        if pooled is None:
+            raise ValueError('head_fwd: the BN prologue writes pooled[]')
+        if bn.get('res') is not None:
+            _chk(bn['res'], torch.bfloat16, 'bn res', B * HW * C)
+        st = bn.get('stats')
+        bnargs = (ptr(bn.get('res')), ptr(st), ptr(bn.get('rmean')), ptr(bn.get('rvar')),
+                  ptr(bn['gamma']), ptr(bn['beta']),
+                  1.0 / float(bn['count']) if st is not None else 0.0, float(bn['eps']),
+                  int(bn.get('group_imgs') or B), _ACT[bn['act']])
     lib().head_fwd(ptr(act), ptr(w), ptr(b), ptr(label), ptr(isw), ptr(pooled), ptr(logits),
                    ptr(dlogits), ptr(losses), ptr(meters), B, HW, C, classes, MODE[mode],
-                   stream_ptr(), SCORE[score])
+                   stream_ptr(), SCORE[score], *bnargs)
 
 
 def head_bwd(pooled, dlogits, w, dw, db, dact, B, HW, C, classes, bw=None):

@@ -40,6 +40,8 @@ CASES = [
     (16, 4, 128, 128, 3, 1, (64, 128, 2)),   # IMG = 4, split
     (8, 16, 256, 128, 3, 1, (256, 128, 2)),  # 256 x 128 tile, two slices per split block
     (4, 8, 192, 64, 3, 1, (64, 64, 1)),      # three slices in one block (halo prefetch)
+    (16, 4, 256, 128, 3, 1, (128, 128, 1)),  # layer4 images: row-term halo swizzle (SWA 6)
+    (16, 8, 128, 128, 3, 1, (256, 128, 1)),  # layer3 images, 256-row tile: SWA 6
 ]
 
 
@@ -70,7 +72,7 @@ def test_hconv_per_tile(case, ghost):
     G = 2 if gimgs else 1
     if gimgs:
         spec.group_rows = gimgs * spec.P * spec.Q
-    if H.geometry(spec, plan[0], plan[1]) is None:
+    if H.geometry(spec, plan[0], plan[1], swa=True) is None:
         pytest.skip('tile does not fit')
     g = torch.Generator(device='cpu').manual_seed(11)
     x = bf(torch.randn(N, C, Hh, Hh, generator=g) * 1.5 + 0.3).to(DEV)

@@ -302,3 +302,43 @@ def test_step_tuner_keeps_engine_consistent():
         eng.step()
     assert math.isfinite(float(eng.read_meters()['loss_sum']))
     assert tune._key('fwd', coords[0][2][0][2]).startswith('fwd|')
+
+
+@pytest.mark.parametrize('arch', ['resnet18', 'mobilenetv2'])
+def test_head_applies_final_bn_in_pool(arch):
+    """EngineOptions.head_bn: the scoring / eval head pools act(bn(y) + res) straight from the
+    last conv's output (no bn_apply pass).  Same losses as the engine that writes the block
+    output first (to the bf16 rounding of that output), in the ghost-BN scoring pass and in
+    eval mode (running statistics)."""
+    from mercury_amd import ops
+    from mercury_amd.config import EngineOptions
+    from mercury_amd.models import build_model
+    ncls = 100 if arch == 'mobilenetv2' else 10
+    res = {}
+    for on in (True, False):
+        torch.manual_seed(2)
+        net = build_model(arch, ncls).to(DEV)
+        with torch.no_grad():
+            for mod in net.modules():       # non-trivial running statistics for the eval pass
+                if isinstance(mod, torch.nn.BatchNorm2d):
+                    mod.running_mean.uniform_(-0.2, 0.2)
+                    mod.running_var.uniform_(0.5, 2.0)
+        eng = _engine(net, opts=EngineOptions(head_bn=on))
+        sm = eng.score_mode
+        sm.stats_arena.zero_()
+        ops.pool_build(eng.shard, eng.shard_labels, eng.ctrl, sm.input, sm.label, sm.index, 320,
+                       32, eng.seed)
+        x = eng.forward(sm)
+        assert (sm.head_bn is not None) == on
+        eng.head(sm, x, 'score')
+        torch.cuda.synchronize()
+        rng = np.random.RandomState(3)
+        ev = eng.evaluate_arrays(rng.randint(0, 256, (64, 32, 32, 3), dtype=np.uint8),
+                                 rng.randint(0, ncls, 64), batch=64)
+        res[on] = (sm.losses.clone(), sm.pooled.clone(), ev)
+        eng.close()
+    (l1, p1, e1), (l0, p0, e0) = res[True], res[False]
+    assert torch.isfinite(l1).all()
+    assert float((l1 - l0).abs().max()) < 2e-2 * max(1.0, float(l0.abs().max()))
+    assert _cos(p1, p0) > 0.9999
+    assert abs(e1[0] - e0[0]) < 2e-2 * max(1.0, abs(e0[0])) and e1[2] == e0[2] == 64
