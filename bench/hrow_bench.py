@@ -24,6 +24,8 @@ def main():
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--shapes', default='0,1,2,3', help='indices into SHAPES')
     ap.add_argument('--plans', default='engine,row4')
+    ap.add_argument('--wm8', type=int, default=0, help='8-wave layout override (hconv_configure)')
+    ap.add_argument('--swa', type=int, default=1, help='per-tile row-term halo swizzle (0: off)')
     ap.add_argument('--pro', action='store_true',
                     help="the input's ghost-BN + ReLU in the halo staging (MODE 1)")
     args = ap.parse_args()
@@ -32,9 +34,10 @@ def main():
     from mercury_amd.ops import hconv as H
     from mercury_amd.ops.conv import ConvSpec, slab_bytes
     ops.lib()
+    H._CFG['swa'] = bool(args.swa)
     dev = 'cuda'
     for grid in [int(x) for x in args.grids.split(',')]:
-        ops.lib().hconv_configure(grid, 8)
+        ops.lib().hconv_configure(grid, 8, args.wm8)
         for (N, Hh, C, K) in [SHAPES[int(i)] for i in args.shapes.split(',')]:
             sp = ConvSpec(N, Hh, Hh, C, K, 3, 3, 1, 1)
             sp.group_rows = 32 * Hh * Hh

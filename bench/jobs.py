@@ -152,6 +152,7 @@ def job_presets(o, a):
 def job_ab(o, a):
     envs = a.env or []
     res = {e: [] for e in envs}
+    solo = {}
     for rnd in range(a.rounds):
         for j, e in enumerate(envs):
             kv = dict(x.split('=', 1) for x in e.split())
@@ -159,11 +160,13 @@ def job_ab(o, a):
             run([PY, 'bench.py'] + shlex.split(a.args or '') +
                 ['--steps', '300', '--warmup', '30', '--no-overhead'], out, 200, env=kv)
             with open(out) as f:
-                res[e].append(json.loads(f.read().strip().splitlines()[-1])['ms_per_step'])
+                d = json.loads(f.read().strip().splitlines()[-1])
+            res[e].append(d['ms_per_step'])
+            solo.setdefault(e, []).append(d.get('solo_ms'))
     for e, v in res.items():
-        print('%-40s %s' % (e, v), flush=True)
+        print('%-40s %s solo %s' % (e, v, solo.get(e)), flush=True)
     with open(os.path.join(o, 'ab.json'), 'w') as f:
-        json.dump(res, f, indent=1)
+        json.dump({'ms_per_step': res, 'solo_ms': solo}, f, indent=1)
 
 
 def job_ab_ext(o, a):

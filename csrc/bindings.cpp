@@ -25,7 +25,7 @@ int igemm_dual_launch(const bf16* srcA, const bf16* wtA, const ConvGeom& gA, con
                       int splitsA, const bf16* srcB, const bf16* wtB, const ConvGeom& gB,
                       const EpiParams& eB, int splitsB, int bm, int bn, hipStream_t st);
 int hconv_read_stamps(unsigned long long* host, int n);
-void hconv_configure(int grid, int waves);
+void hconv_configure(int grid, int waves, int wm8);
 // native RCCL communicator (comm.hip)
 std::string comm_unique_id();
 uintptr_t comm_init(const std::string& id_bytes, int rank, int nranks);

@@ -1423,8 +1423,12 @@ int launch_persist_w(const bf16* src, const bf16* wt, const HconvGeom& g, const 
 // WM4 / WM8: wave rows of the 4- and 8-wave blocks (MERCURY_HCONV_PERSIST_WAVES picks, 0 = none)
 int g_persist_grid = 0;      // 0: half the CUs
 int g_persist_waves = 8;     // 8 or 4
+int g_persist_wm8 = 0;       // 8-wave wave-row count override (0: the tile's default WM8)
 
-template <int BM, int BN, int WM4, int WM8>
+// WM8B: an alternative 8-wave layout of the same tile, selected by g_persist_wm8 == WM8B.  For
+// 128 x 64 the default 8 x 1 wave grid gives every wave a 16 x 64 tile (1.25 KB of fragment
+// reads per MFMA, each wave reading the whole weight tile); 4 x 2 gives 32 x 32 (1 KB per MFMA)
+template <int BM, int BN, int WM4, int WM8, int WM8B = 0>
 int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const EpiParams& e,
                    const HconvPro& pro, hipStream_t st) {
   static int cus = 0;
@@ -1449,6 +1453,10 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
   const int grid = ntiles < gmax ? ntiles : gmax;
   if constexpr (WM8 > 0) {
+    if constexpr (WM8B > 0) {
+      if (waves == 8 && g_persist_wm8 == WM8B)
+        return launch_persist_w<BM, BN, WM8B, 8>(src, wt, g, e, pro, grid, st);
+    }
     if (waves == 8) return launch_persist_w<BM, BN, WM8, 8>(src, wt, g, e, pro, grid, st);
   }
   return launch_persist_w<BM, BN, WM4, 4>(src, wt, g, e, pro, grid, st);
@@ -1484,9 +1492,10 @@ int hconv_read_stamps(unsigned long long* host, int n) {
 #endif
 }
 
-void hconv_configure(int grid, int waves) {
+void hconv_configure(int grid, int waves, int wm8) {
   g_persist_grid = grid > 0 ? grid : 0;
   g_persist_waves = waves == 4 ? 4 : 8;
+  g_persist_wm8 = wm8 > 0 ? wm8 : 0;
 }
 
 int hconv_lds_bytes(const HconvGeom& g, int bm, int bn, int splits_gt1) {
@@ -1548,12 +1557,13 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
                     e.bias == nullptr && !e.accumulate &&
                     e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
                     (e.stats == nullptr || e.group_rows % bm == 0);
-#define HP_CASE(BM_, BN_, WM4_, WM8_)                                                 \
-  if (ok && bm == BM_ && bn == BN_ && launch_persist<BM_, BN_, WM4_, WM8_>(src, wt, g, e, pro, st)) \
+#define HP_CASE(BM_, BN_, WM4_, WM8_, WM8B_)                                          \
+  if (ok && bm == BM_ && bn == BN_ &&                                                  \
+      launch_persist<BM_, BN_, WM4_, WM8_, WM8B_>(src, wt, g, e, pro, st))              \
     return 1;
-    HP_CASE(256, 64, 4, 8)
-    HP_CASE(128, 64, 2, 8)
-    HP_CASE(64, 64, 1, 0)
+    HP_CASE(256, 64, 4, 8, 0)
+    HP_CASE(128, 64, 2, 8, 4)
+    HP_CASE(64, 64, 1, 0, 0)
 #undef HP_CASE
   }
   if (pro.mode != 0) return 0;      // the per-tile kernel stages plain input only

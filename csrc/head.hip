@@ -50,11 +50,14 @@ __global__ __launch_bounds__(NT) void head_pool_kernel(const bf16* act, float* p
 // one thread per (sample, 8 channels), the raw conv output and the residual read once, each
 // element normalised exactly as bn_apply_kernel would (scale / shift from the ghost-group sums or
 // the running statistics) but kept in fp32 up to the mean
+// (four consecutive lanes split one (sample, 8 channels)'s pixels and add up with two xor
+// shuffles: 4x the threads of a one-lane pool, which left a 320-sample head latency-bound)
 __global__ __launch_bounds__(NT) void head_pool_bn_kernel(HeadArgs a) {
   const int C8 = a.C >> 3;
-  const int i = blockIdx.x * NT + threadIdx.x;
-  if (i >= a.B * C8) return;
-  const int b = i / C8, c = (i - b * C8) * 8;
+  const int t = blockIdx.x * NT + threadIdx.x;
+  const int i = t >> 2, sub = t & 3;
+  const bool live = i < a.B * C8;
+  const int b = live ? i / C8 : 0, c = live ? (i - b * C8) * 8 : 0;
   float sc[8], sh[8];
   {
     float m8[8], v8[8];
@@ -78,18 +81,26 @@ __global__ __launch_bounds__(NT) void head_pool_bn_kernel(HeadArgs a) {
   float s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = 0.f;
-#pragma unroll 4
-  for (int hw = 0; hw < a.HW; ++hw) {
-    const bf16x8 v = *(const bf16x8*)(x + (size_t)hw * a.C);
-    bf16x8 rv;
-    if (r) rv = *(const bf16x8*)(r + (size_t)hw * a.C);
+  if (live) {
+#pragma unroll 2
+    for (int hw = sub; hw < a.HW; hw += 4) {
+      const bf16x8 v = *(const bf16x8*)(x + (size_t)hw * a.C);
+      bf16x8 rv;
+      if (r) rv = *(const bf16x8*)(r + (size_t)hw * a.C);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float t = bf2f(v[k]) * sc[k] + sh[k];
-      if (r) t += bf2f(rv[k]);
-      s[k] += fminf(fmaxf(t, lo), hi);
+      for (int k = 0; k < 8; ++k) {
+        float u = bf2f(v[k]) * sc[k] + sh[k];
+        if (r) u += bf2f(rv[k]);
+        s[k] += fminf(fmaxf(u, lo), hi);
+      }
     }
   }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s[k] += __shfl_xor(s[k], 1, 64);
+    s[k] += __shfl_xor(s[k], 2, 64);
+  }
+  if (!live || sub) return;
   const float inv = 1.f / (float)a.HW;
   float* o = a.pooled + (size_t)b * a.C + c;
   *(float4*)o = make_float4(s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv);
@@ -482,8 +493,8 @@ void head_fwd_launch(const HeadArgs& a0, hipStream_t st) {
   // the zeroed logits)
   if (a.bn_gamma) {
     // the final BN (+ residual) + activation in the pool: pooled[] first, then the FC
-    hipLaunchKernelGGL(head_pool_bn_kernel, dim3((a.B * (a.C / 8) + NT - 1) / NT), dim3(NT), 0,
-                       st, a);
+    hipLaunchKernelGGL(head_pool_bn_kernel, dim3((4 * a.B * (a.C / 8) + NT - 1) / NT), dim3(NT),
+                       0, st, a);
     a.pooled_ready = 1;
   }
   if (wide && a.pooled && a.logits && a.C % 16 == 0) {

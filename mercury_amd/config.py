@@ -132,6 +132,14 @@ class EngineOptions:
     hconv_persist_grid: int = 0
     # waves per persistent halo block (8: 1.513 vs 1.521 ms/step over 4)
     hconv_persist_waves: int = 8
+    # 8-wave layout of the 128 x 64 persistent tile: wave rows (8 = 8 x 1, 16 x 64 per wave,
+    # every wave reading the whole weight tile; 4 = 4 x 2, 32 x 32 per wave, 20 % fewer LDS
+    # fragment bytes per MFMA: layer3 scoring conv 57.5-58.1 vs 60.2-61.5 us, scoring solo
+    # 1.034-1.036 vs 1.041-1.046 ms, step within noise, profiles/r6/ab_r6a/)
+    hconv_persist_wm8: int = 4
+    # per-tile halo kernel: the row-term halo swizzle (HconvGeom.SWA) where the lane-group model
+    # finds it conflict-free (layer4: 2.03 -> 0.08 LDS conflict cycles per LDS instruction)
+    hconv_swa: bool = True
     # stride-1 3x3 convs on the row-step persistent kernel (csrc/hconv.hip hrow_kernel) where it
     # measured faster: '1' both batch modes, 'score' / 'train' one, '0' off (hconv.MEASURED_ROW;
     # layer1 scoring conv 51.6 vs 60.4 us, profiles/r5/hrow_bench_v3.jsonl)
@@ -196,6 +204,7 @@ class EngineOptions:
     # kernel's (hconv_row), '0' none.  On the per-tap kernel the staging transform costs more
     # than the pass it saves (layer3 81.5 vs 57 us): 'row' 1.307 vs '1' 1.333 ms/step with the
     # layer1 + layer2 convs on the row-step kernel (profiles/r5/ab_persist_bn_scope.json)
+    # ('stat': the row-step kernel's weight-stationary layer1 convs only)
     persist_bn: str = 'row'
 
     @classmethod

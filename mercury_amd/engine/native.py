@@ -229,7 +229,7 @@ class NativeEngine(object):
         self.res_pro = o.fuse_bn_fwd and o.res_pro
         self.head_bw = o.head_bw
         self.dw_pair = o.dw_pair
-        self.persist_bn = o.persist_bn if o.persist_bn in ('0', '1', 'row') else (
+        self.persist_bn = o.persist_bn if o.persist_bn in ('0', '1', 'row', 'stat') else (
             '1' if str(o.persist_bn).lower() in ('true', 'on', 'yes') else '0')
         self._apply_globals()
 
@@ -451,7 +451,8 @@ class NativeEngine(object):
                     if not train and group_imgs and self.persist_bn != '0' and \
                             u is not blk.units[0] and u is not blk.shortcut:
                         hb = hconv.persist_bn_plan(sp, group_imgs,
-                                                   row_only=self.persist_bn == 'row')
+                                                   row_only=self.persist_bn in ('row', 'stat'),
+                                                   stat_only=self.persist_bn == 'stat')
                     if hb is not None:
                         m.plan[u.name, 'hconv_bn'] = hb
                         slab = max(slab, slab_bytes(sp.M, sp.K, *hb))

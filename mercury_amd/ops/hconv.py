@@ -71,7 +71,7 @@ def lds_bytes(g, bm, bn, splits):
 
 
 # engine-selected settings (config.EngineOptions via ``configure``)
-_CFG = dict(persist=True, plans='', waves=8, grid=0, row='score')
+_CFG = dict(persist=True, plans='', waves=8, grid=0, row='score', wm8=0, swa=True)
 
 
 def configure(opts):
@@ -79,8 +79,9 @@ def configure(opts):
     wave count are also handed to the C++ launcher)."""
     _CFG.update(persist=bool(opts.hconv_persist), plans=opts.hconv_plans or '',
                 waves=8 if opts.hconv_persist_waves == 8 else 4,
-                grid=int(opts.hconv_persist_grid), row=opts.hconv_row)
-    lib().hconv_configure(_CFG['grid'], _CFG['waves'])
+                grid=int(opts.hconv_persist_grid), row=opts.hconv_row,
+                wm8=int(opts.hconv_persist_wm8), swa=bool(opts.hconv_swa))
+    lib().hconv_configure(_CFG['grid'], _CFG['waves'], _CFG['wm8'])
 
 
 def persist_waves():
@@ -247,8 +248,9 @@ _GEO_CACHE = {}
 
 
 def geometry_cached(spec: ConvSpec, bm, bn, swa=False):
+    swa = bool(swa) and _CFG['swa']
     key = (spec.N, spec.H, spec.W, spec.C, spec.K, spec.R, spec.stride, spec.pad,
-           spec.group_rows, bm, bn, bool(swa))
+           spec.group_rows, bm, bn, swa)
     if key not in _GEO_CACHE:
         _GEO_CACHE[key] = geometry(spec, bm, bn, swa)
     return _GEO_CACHE[key]
@@ -378,12 +380,18 @@ def engine_plan(spec: ConvSpec, bias=False, train=None):
     return None
 
 
-def persist_bn_plan(spec: ConvSpec, group_imgs, row_only=False):
+def persist_bn_plan(spec: ConvSpec, group_imgs, row_only=False, stat_only=False):
     """The persistent plan with the input's BN + activation in the halo staging (no residual),
     or None: the row-step kernel where it runs this conv, else (unless ``row_only``) the per-tap
     persistent kernel.  Scoring pass only (EngineOptions.persist_bn, engine)."""
     p = engine_plan(spec, train=False)
     if p is not None and p[2] < 0:
+        # stat_only: only where the row-step kernel keeps its weights stationary (C = K = 64,
+        # one slice, one channel tile: each halo element is transformed once per tile).  With
+        # several slices x channel tiles the transform runs once per (slice, channel tile) pass
+        # on the slice's critical path
+        if stat_only and not (spec.C == 64 and spec.K == p[1]):
+            return None
         return p
     if row_only:
         return None

@@ -178,6 +178,20 @@ def test_hconv_persistent(case, with_stats):
     ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
     H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, (bm, bn, 0), stats=ostats, pro=pro)
     torch.cuda.synchronize()
+    if (bm, bn) == (128, 64) and H.persist_waves() == 8:
+        # the 4 x 2 wave layout of the same tile (EngineOptions.hconv_persist_wm8) must agree
+        out2 = torch.full_like(out, float('nan'))
+        ost2 = torch.zeros_like(ostats) if ostats is not None else None
+        ops.lib().hconv_configure(H._CFG['grid'], 8, 4)
+        try:
+            H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out2, spec, (bm, bn, 0), stats=ost2,
+                        pro=pro)
+            torch.cuda.synchronize()
+        finally:
+            ops.lib().hconv_configure(H._CFG['grid'], H.persist_waves(), H._CFG['wm8'])
+        close(out2.float(), out.float(), rtol=1e-2, atol=1e-2)
+        if ostats is not None:
+            close(ost2, ostats, rtol=1e-3, atol=0.5)
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
     assert not torch.isnan(got).any()
     close(got, ref)
@@ -251,13 +265,13 @@ def test_hconv_row_step(case, with_stats):
     out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
     if grid4:
-        ops.lib().hconv_configure(4, H.persist_waves())
+        ops.lib().hconv_configure(4, H.persist_waves(), H._CFG['wm8'])
     try:
         H.hconv_fwd(xn, wk, out, spec, (bm, bn, splits), stats=ostats, pro=pro)
         torch.cuda.synchronize()
     finally:
         if grid4:
-            ops.lib().hconv_configure(H._CFG['grid'], H.persist_waves())
+            ops.lib().hconv_configure(H._CFG['grid'], H.persist_waves(), H._CFG['wm8'])
     got = out.view(N, spec.P, spec.Q, K).permute(0, 3, 1, 2).float().cpu()
     assert not torch.isnan(got).any()
     close(got, ref)

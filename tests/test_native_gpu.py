@@ -306,10 +306,11 @@ def test_step_tuner_keeps_engine_consistent():
 
 @pytest.mark.parametrize('arch', ['resnet18', 'mobilenetv2'])
 def test_head_applies_final_bn_in_pool(arch):
-    """EngineOptions.head_bn: the scoring / eval head pools act(bn(y) + res) straight from the
-    last conv's output (no bn_apply pass).  Same losses as the engine that writes the block
-    output first (to the bf16 rounding of that output), in the ghost-BN scoring pass and in
-    eval mode (running statistics)."""
+    """EngineOptions.head_bn: the scoring / eval head pools act(bn(y) [+ res]) straight from the
+    last conv's output (no bn_apply pass).  Checked against a torch recompute from the SAME
+    run's conv output, ghost statistics and residual (exact up to fp32 summation order), and
+    against an engine that writes the block output first (losses to the bf16 rounding of that
+    output and the run-to-run spread of atomically reduced statistics)."""
     from mercury_amd import ops
     from mercury_amd.config import EngineOptions
     from mercury_amd.models import build_model
@@ -332,13 +333,27 @@ def test_head_applies_final_bn_in_pool(arch):
         assert (sm.head_bn is not None) == on
         eng.head(sm, x, 'score')
         torch.cuda.synchronize()
+        if on:
+            blk = eng.lw.blocks[-1]
+            u = blk.units[-1]
+            y = sm.buf[u.name, 'y'].float().view(10, 32, -1, u.K)
+            st = sm.stats[u.name].view(10, 2, u.K)
+            cnt = sm.spec[u.name].group_rows
+            mean = st[:, 0] / cnt
+            var = (st[:, 1] / cnt - mean * mean).clamp_min(0)
+            sc = eng._gamma(u) / torch.sqrt(var + 1e-5)
+            z = y * sc.view(10, 1, 1, u.K) + (eng._beta(u) - mean * sc).view(10, 1, 1, u.K)
+            if sm.head_bn.get('res') is not None:
+                z = z + sm.head_bn['res'].float().view(10, 32, -1, u.K)
+            z = z.clamp(0, 6.0 if blk.final_act == 'relu6' else float('inf'))
+            pref = z.mean(2).reshape(320, u.K)
+            assert float((sm.pooled - pref).abs().max()) < 1e-4 * max(1.0, float(pref.abs().max()))
         rng = np.random.RandomState(3)
         ev = eng.evaluate_arrays(rng.randint(0, 256, (64, 32, 32, 3), dtype=np.uint8),
                                  rng.randint(0, ncls, 64), batch=64)
-        res[on] = (sm.losses.clone(), sm.pooled.clone(), ev)
+        res[on] = (sm.losses.clone(), ev)
         eng.close()
-    (l1, p1, e1), (l0, p0, e0) = res[True], res[False]
+    (l1, e1), (l0, e0) = res[True], res[False]
     assert torch.isfinite(l1).all()
-    assert float((l1 - l0).abs().max()) < 2e-2 * max(1.0, float(l0.abs().max()))
-    assert _cos(p1, p0) > 0.9999
+    assert float((l1 - l0).abs().mean()) < 2e-2 * max(1.0, float(l0.abs().mean()))
     assert abs(e1[0] - e0[0]) < 2e-2 * max(1.0, abs(e0[0])) and e1[2] == e0[2] == 64
