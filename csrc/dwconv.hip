@@ -19,6 +19,8 @@
 //
 // Thread index -> (chunk fastest, then strip, row, image): adjacent lanes touch adjacent 16 B
 // chunks of the same pixel, so every wave access is a contiguous run of the NHWC row.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -517,13 +519,26 @@ __global__ __launch_bounds__(DT) void dw_wgrad_reduce_kernel(const float* slab, 
 }
 }  // namespace
 
+// blocks of the statistics-adding depthwise launches (every block's per-channel atomics land on
+// the same few cache lines: fewer adders, less same-address serialisation at the memory side);
+// MERCURY_DW_STAT_BLOCKS overrides for A/B runs
+int dw_stat_blocks() {
+  static const int v = [] {
+    const char* e = getenv("MERCURY_DW_STAT_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 256;
+  }();
+  return v;
+}
+
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const int QS = (a.Q + DWL - 1) / DWL;
   const long long total = (long long)a.N * a.P * QS * (a.C / 8);
   long long blocks = (total + DT - 1) / DT;
   // one statistics group: at most ~one block per CU adds the BN sums (grid-stride kernel)
-  const bool loop = a.stats && a.group_rows / (a.P * a.Q) >= a.N && blocks > 256;
-  if (loop) blocks = 256;
+  const int cap = dw_stat_blocks();
+  const bool loop = a.stats && a.group_rows / (a.P * a.Q) >= a.N && blocks > cap;
+  if (loop) blocks = cap;
   const dim3 grid((unsigned)blocks);
   const size_t shm = a.stats ? (size_t)DT * ST_LD * sizeof(float) : 0;
   const bool pro = a.pro_gamma != nullptr;
@@ -546,7 +561,7 @@ void dwconv_dgrad_launch(const bf16* dy, const float* w, bf16* dx, int N, int H,
   const long long total = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
   // BW: at most ~one block per CU (each adds 2C atomics; C8 <= DT keeps a block's chunks whole)
   long long blocks = (total + DT - 1) / DT;
-  if (bw && blocks > 256) blocks = 256;
+  if (bw && blocks > dw_stat_blocks()) blocks = dw_stat_blocks();
   const dim3 grid((unsigned)blocks);
   const DwBw none{};
   const size_t shm = bw ? (size_t)DT * ST_LD * sizeof(float) : 0;
@@ -581,7 +596,7 @@ void dwconv_bwd_launch(const bf16* dy, const bf16* x, const float* w, bf16* dx, 
   const int nwg = dwconv_wgrad_blocks(N, P, Q, C);
   const long long dtotal = (long long)N * H * ((W + DWL - 1) / DWL) * (C / 8);
   long long ndg = (dtotal + DT - 1) / DT;
-  if (bw && ndg > 256) ndg = 256;
+  if (bw && ndg > dw_stat_blocks()) ndg = dw_stat_blocks();
   const size_t shm = (size_t)DT * WG_LD * sizeof(float);   // >= the dgrad's [DT][ST_LD]
   static const bool attr = [] {
     const void* ks[] = {(const void*)dw_bwd_kernel<1, false>, (const void*)dw_bwd_kernel<1, true>,

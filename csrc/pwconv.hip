@@ -26,6 +26,8 @@ constexpr int PW_BN = 64;        // output channels per N-tile
 constexpr int PW_NT = 256;       // 4 waves, 2 (M) x 2 (N): 64 x 32 per wave
 constexpr int PW_KMAX = 128;     // input channels held in the panel
 constexpr unsigned PW_OOB = 0xFFFFFF00u;
+constexpr int PW_OP = PW_BN * 2 + 16;   // staging row pitch (bytes): 16-B aligned, 36 dwords
+constexpr int PW_OBYTES = PW_BM * PW_OP;
 
 MA_DEV unsigned pw_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
@@ -51,6 +53,25 @@ MA_DEV float pw_row16_sum(float v) {
 }
 typedef uint32_t pw_u32x2 __attribute__((ext_vector_type(2)));
 
+// 16-byte stores per thread of a staged [BM][BN] output tile: a row's BN * 2 = 128 bytes are 8
+// consecutive lanes, so one wave instruction writes 8 whole 128-byte row segments (the
+// direct-from-accumulator form wrote 16 rows x 32 bytes per instruction: these expansion convs
+// are write-bound, 2 GB out per 0.5 GB in at ResNet-50's layer1)
+constexpr int PW_ST = PW_BM * PW_BN * 2 / 16 / PW_NT;   // stores per thread per N-tile (4)
+MA_DEV void pw_store_tile(const char* sO, __amdgpu_buffer_rsrc_t rs_o, const PgemmArgs& g,
+                          int m0, int n0, int tid) {
+#pragma unroll
+  for (int i = 0; i < PW_ST; ++i) {
+    const int c = tid + PW_NT * i;                   // 16-byte chunk of the tile
+    const int r = c >> 3, piece = c & 7;             // (PW_BN * 2 / 16 = 8 chunks per row)
+    const u32x4 v = *(const u32x4*)(sO + r * PW_OP + piece * 16);
+    const int row = m0 + r, col = n0 + piece * 8;
+    const bool ok = row < g.M && col < g.N;          // (N % 8 == 0: a chunk is whole or out)
+    __builtin_amdgcn_raw_buffer_store_b128(
+        v, rs_o, ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PW_OOB, 0, 0);
+  }
+}
+
 // KB = 32-deep k-blocks of the panel (K <= 32 * KB); PRO: input prologue on
 template <int KB, bool PRO, bool STATS>
 __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro pro) {
@@ -58,12 +79,18 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
   constexpr int TM = 4, TN = 2;                      // 64 x 32 per wave
   constexpr int SA = KB * BM * 64;                   // A panel bytes
   constexpr int SBT = KB * BN * 64;                  // one weight tile
+  // the staged epilogue's 18 KB tile keeps up to two blocks per CU only with a shallow panel
+  // (KB <= 2: 64 -> 256 @56 810 -> 644 us; at KB = 4 it cost the second block, 479 -> 552)
+  constexpr bool STAGE = KB <= 2;
   constexpr int PA = KB * (BM / 16) / 4;             // A pieces per wave (KB * 2)
   constexpr int PB = KB * (BN / 16) / 4;             // B pieces per wave per N-tile (KB)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sA = smem;
   char* sB = smem + SA;                              // [2][SBT]
   float* red = (float*)(smem + SA + 2 * SBT);        // [2 wave rows][2][BN]
+  // output staging tile [BM][BN] bf16, rows padded to PW_OP bytes: the accumulators land here
+  // (8 bytes per lane) and leave as 16-byte row-contiguous stores (see the epilogue)
+  char* sO = smem + SA + 2 * SBT + 2 * 2 * BN * 4;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -188,10 +215,16 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
-        const bool ok = row < g.M && col < g.N;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pw_u32x2, o), rs_o,
-                                              ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PW_OOB,
-                                              0, 0);
+        if constexpr (STAGE) {
+          // (tile-local row / column of this lane's 4 channels)
+          *(pw_u32x2*)(sO + (row - m0) * PW_OP + (col - nt * BN) * 2) =
+              __builtin_bit_cast(pw_u32x2, o);
+        } else {
+          const bool ok = row < g.M && col < g.N;
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(pw_u32x2, o), rs_o,
+              ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PW_OOB, 0, 0);
+        }
         if constexpr (STATS) {
           const float mk = row < g.M ? 1.f : 0.f;
           const float m1 = row < bnd ? mk : 0.f, m2 = mk - m1;
@@ -227,17 +260,35 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
           atomicAdd(dst, red[tid] + red[2 * BN + tid]);
           atomicAdd(dst + g.stats_ld, red[BN + tid] + red[3 * BN + tid]);
         }
+        if (STAGE && part == 0) pw_store_tile(sO, rs_o, g, m0, nt * BN, tid);
         pw_bar_lds();
       }
+    } else if constexpr (STAGE) {
+      pw_bar_lds();                                  // the staging tile is complete
+      pw_store_tile(sO, rs_o, g, m0, nt * BN, tid);
     }
-    pw_wait<0>();                                    // weight tile nt + 1 landed (+ stores)
+    // weight tile nt + 1 landed -- a COUNTED wait: the PW_ST stores of this tile (and wave 0's
+    // statistics atomics) are younger than that DMA and stay in flight under the next tile's
+    // MFMAs (vmcnt retires in issue order).  A vmcnt(0) here waited for every store's
+    // acknowledgement once per N-tile: four store round trips per 128-row block at 2 blocks per
+    // CU left these HBM-bound expansion convs at ~3.1 TB/s
+    if (nt + 1 < ntn) {
+      constexpr int NS = STAGE ? PW_ST : TM * TN;    // this thread's output stores of the tile
+      if (STATS && wu == 0) {
+        if (straddle) pw_wait<NS + 4>();
+        else pw_wait<NS + 2>();
+      } else {
+        pw_wait<NS>();
+      }
+    }
     pw_bar_lds();
   }
 }
 
 template <int KB, bool PRO, bool STATS>
 void pw_launch(const PgemmArgs& g, const PgemmPro& pro, hipStream_t st) {
-  constexpr int bytes = KB * PW_BM * 64 + 2 * KB * PW_BN * 64 + 2 * 2 * PW_BN * 4;
+  constexpr int bytes = KB * PW_BM * 64 + 2 * KB * PW_BN * 64 + 2 * 2 * PW_BN * 4 +
+                        (KB <= 2 ? PW_OBYTES : 0);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)pwconv_kernel<KB, PRO, STATS>,

@@ -150,6 +150,9 @@ class EngineOptions:
     pgemm: bool = True
     # narrow-input expansion 1x1 convs on the panel-resident kernel (pwconv_engine_ab.json)
     pwconv: bool = True
+    # plain (no prologue) narrow-input expansion 1x1 convs on the panel-resident kernel too
+    # (ResNet-50 layer1.0 shortcut; ops.conv.pwconv_plain_wins)
+    pwconv_plain: bool = True
     # first conv on the dense-k stem kernel (stem_bench_v2.jsonl)
     stem: bool = True
     # a downsampling block's first conv and its shortcut conv in one launch (profiles/r4/
@@ -195,6 +198,9 @@ class EngineOptions:
     # rccl_one_rank), 'on' always (an explicit bucket_bytes still wins; the last-bucket size is
     # taken from the calibration), 'off' never (16 MiB buckets, 1 MiB last bucket)
     bucket_calib: str = 'auto'
+    # the last DP bucket's budget in MiB when nothing was calibrated (0: no forced last-bucket
+    # cut -- the 16 MiB walk decides alone)
+    last_bucket_mb: float = 1.0
     # scoring-pass conv tile target in blocks (128 vs 256: 1.656 vs 1.667 ms/step)
     score_min_blocks: int = 128
     # debug mode: print each phase as it completes
@@ -216,7 +222,7 @@ class EngineOptions:
         if not spec:
             return o
         types = {f.name: f.type for f in dataclasses.fields(cls)}
-        for item in re.split(r',(?=[a-z_]+=)', spec):
+        for item in re.split(r',(?=[a-z_][a-z0-9_]*=)', spec):
             if '=' not in item:
                 raise ValueError('MERCURY_ENGINE_OPTS: %r is not name=value' % item)
             k, v = item.split('=', 1)
@@ -228,6 +234,8 @@ class EngineOptions:
                 val = v.strip().lower() in ('1', 'true', 'yes', 'on')
             elif t in ('int', int):
                 val = int(v)
+            elif t in ('float', float):
+                val = float(v)
             else:
                 val = v.strip()
             setattr(o, k, val)

@@ -34,7 +34,8 @@ import torch.distributed as dist
 from .. import ops
 from ..ops import hconv, tune
 from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plain_wins,
-                        pgemm_plan, pgemm_pro_wins, pwconv_ok, pwconv_pro_wins, slab_bytes,
+                        pgemm_plan, pgemm_pro_wins, pwconv_ok, pwconv_plain_wins,
+                        pwconv_pro_wins, slab_bytes,
                         stem_ok, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
 from ..parallel.buckets import default_bucket_bytes
@@ -173,7 +174,7 @@ class NativeEngine(object):
         self.bucket_bytes = bucket_bytes or default_bucket_bytes(world_size)
         # the last bucket (closed when the backward ends, so fully exposed) holds only the
         # leading blocks' parameters up to this many bytes (bucket_plan)
-        self.last_bucket_bytes = 1 << 20
+        self.last_bucket_bytes = int(self.opts.last_bucket_mb * (1 << 20))
         # measured all-reduce cost model (alpha, beta) and the plan derived from it: under DP on
         # the engine's RCCL communicator the bucket sizes come from timing the real collective
         # at start-up, not from an assumed link bandwidth (parallel/buckets.py)
@@ -542,6 +543,10 @@ class NativeEngine(object):
         if pro is not None and pro.get('pw'):
             ops.pwconv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, pro=pro)
             return
+        if pro is None and (u.name, 'pwconv') in m.plan and pwconv_plain_wins(sp) and \
+                self.opts.pwconv_plain:
+            ops.pwconv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats)
+            return
         pg = m.plan.get((u.name, 'pgemm'))
         if pg is not None and (pro is not None and pro.get('pg') or
                                pro is None and pgemm_plain_wins(sp)):
@@ -565,6 +570,9 @@ class NativeEngine(object):
         if u.depthwise or u.b_seg is not None:
             return False
         if any((u.name, k) in m.plan for k in ('stem', 'hconv')):
+            return False
+        if (u.name, 'pwconv') in m.plan and pwconv_plain_wins(m.spec[u.name]) and \
+                self.opts.pwconv_plain:
             return False
         return not ((u.name, 'pgemm') in m.plan and pgemm_plain_wins(m.spec[u.name]))
 
@@ -1293,7 +1301,7 @@ class NativeEngine(object):
         # the last bucket: blocks 0 .. kl - 1, the largest leading run within last_bucket_bytes
         # (a cut at block kl's start is forced; 0: no forced cut)
         kl = 0
-        for k in range(1, len(starts)):
+        for k in range(1, len(starts) if self.last_bucket_bytes > 0 else 1):
             if starts[k] * 4 > self.last_bucket_bytes:
                 break
             kl = k

@@ -419,6 +419,13 @@ def pwconv_pro_wins(spec: ConvSpec):
     return pwconv_ok(spec) and spec.K >= 2 * spec.C and spec.M >= 65536
 
 
+def pwconv_plain_wins(spec: ConvSpec):
+    """Plain (no prologue) narrow-input expansion conv on the panel-resident kernel instead of
+    igemm: ResNet-50's layer1.0 projection shortcut 64 -> 256 @56 at B = 1280 (write-bound,
+    2 GB out), 817 vs 875 us with the statistics epilogue (scratch measurement, round 6)."""
+    return pwconv_ok(spec) and spec.K >= 2 * spec.C and spec.M >= 65536
+
+
 def pwconv_fwd(x, w, out, spec: ConvSpec, stats=None, pro=None):
     """out[M][K] = conv1x1(x, w) with the input panel normalised ONCE in LDS (``pro`` as in
     ``pgemm_fwd``, identity residual excluded) and reused by all output-channel tiles."""
