@@ -26,8 +26,12 @@ constexpr int PW_BN = 64;        // output channels per N-tile
 constexpr int PW_NT = 256;       // 4 waves, 2 (M) x 2 (N): 64 x 32 per wave
 constexpr int PW_KMAX = 128;     // input channels held in the panel
 constexpr unsigned PW_OOB = 0xFFFFFF00u;
-constexpr int PW_OP = PW_BN * 2 + 16;   // staging row pitch (bytes): 16-B aligned, 36 dwords
-constexpr int PW_OBYTES = PW_BM * PW_OP;
+// output staging tile [BM][BN] bf16: 128-byte rows, 16-byte chunk p of row r at slot p ^ (r & 7)
+// (the 8-byte accumulator writes of 16 rows then hit 2-way at most, the 16-byte row reads none)
+constexpr int PW_OBYTES = PW_BM * PW_BN * 2;
+MA_DEV int pw_soff(int r, int c) {       // byte offset of (row r, channel c) in the staging tile
+  return r * (PW_BN * 2) + (((c >> 3) ^ (r & 7)) << 4) + ((c & 7) << 1);
+}
 
 MA_DEV unsigned pw_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
@@ -64,7 +68,7 @@ MA_DEV void pw_store_tile(const char* sO, __amdgpu_buffer_rsrc_t rs_o, const Pge
   for (int i = 0; i < PW_ST; ++i) {
     const int c = tid + PW_NT * i;                   // 16-byte chunk of the tile
     const int r = c >> 3, piece = c & 7;             // (PW_BN * 2 / 16 = 8 chunks per row)
-    const u32x4 v = *(const u32x4*)(sO + r * PW_OP + piece * 16);
+    const u32x4 v = *(const u32x4*)(sO + pw_soff(r, piece * 8));
     const int row = m0 + r, col = n0 + piece * 8;
     const bool ok = row < g.M && col < g.N;          // (N % 8 == 0: a chunk is whole or out)
     __builtin_amdgcn_raw_buffer_store_b128(
@@ -79,18 +83,21 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
   constexpr int TM = 4, TN = 2;                      // 64 x 32 per wave
   constexpr int SA = KB * BM * 64;                   // A panel bytes
   constexpr int SBT = KB * BN * 64;                  // one weight tile
-  // the staged epilogue's 18 KB tile keeps up to two blocks per CU only with a shallow panel
-  // (KB <= 2: 64 -> 256 @56 810 -> 644 us; at KB = 4 it cost the second block, 479 -> 552)
-  constexpr bool STAGE = KB <= 2;
+  // staged epilogue: a 16 KB tile area of its own for a shallow panel (KB <= 2: 64 -> 256 @56
+  // 810 -> 644 us); deeper panels stage into the weight tile the MFMAs just finished (one more
+  // barrier per N-tile): a separate area there cost the second block per CU (128 -> 512 @28
+  // 479 -> 552 us with a padded 18 KB area)
+  constexpr bool STAGE = true;
+  constexpr bool OWN = KB <= 2 || SBT < PW_OBYTES;
   constexpr int PA = KB * (BM / 16) / 4;             // A pieces per wave (KB * 2)
   constexpr int PB = KB * (BN / 16) / 4;             // B pieces per wave per N-tile (KB)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sA = smem;
   char* sB = smem + SA;                              // [2][SBT]
   float* red = (float*)(smem + SA + 2 * SBT);        // [2 wave rows][2][BN]
-  // output staging tile [BM][BN] bf16, rows padded to PW_OP bytes: the accumulators land here
-  // (8 bytes per lane) and leave as 16-byte row-contiguous stores (see the epilogue)
-  char* sO = smem + SA + 2 * SBT + 2 * 2 * BN * 4;
+  // output staging tile [BM][BN] bf16 (pw_soff layout): the accumulators land here (8 bytes per
+  // lane) and leave as 16-byte row-contiguous stores (see the epilogue)
+  char* sO = smem + SA + 2 * SBT + 2 * 2 * BN * 4;   // (OWN; else the weight tile, per N-tile)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -199,7 +206,9 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
         for (int tn = 0; tn < TN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
     }
-    // epilogue: bf16 NHWC stores straight from the accumulators + statistics
+    // epilogue: the tile through LDS (row-contiguous 16-byte stores) + statistics
+    char* sOt = OWN ? sO : sB + buf * SBT;
+    if constexpr (!OWN) pw_bar_lds();               // every wave's reads of the weight tile done
     const int cbase = nt * BN + wn * 32 + 4 * (lane >> 4);
     float s[TN][4], ss[TN][4], s2[TN][4], ss2[TN][4];
 #pragma unroll
@@ -217,8 +226,7 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
         for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
         if constexpr (STAGE) {
           // (tile-local row / column of this lane's 4 channels)
-          *(pw_u32x2*)(sO + (row - m0) * PW_OP + (col - nt * BN) * 2) =
-              __builtin_bit_cast(pw_u32x2, o);
+          *(pw_u32x2*)(sOt + pw_soff(row - m0, col - nt * BN)) = __builtin_bit_cast(pw_u32x2, o);
         } else {
           const bool ok = row < g.M && col < g.N;
           __builtin_amdgcn_raw_buffer_store_b64(
@@ -260,12 +268,12 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
           atomicAdd(dst, red[tid] + red[2 * BN + tid]);
           atomicAdd(dst + g.stats_ld, red[BN + tid] + red[3 * BN + tid]);
         }
-        if (STAGE && part == 0) pw_store_tile(sO, rs_o, g, m0, nt * BN, tid);
+        if (STAGE && part == 0) pw_store_tile(sOt, rs_o, g, m0, nt * BN, tid);
         pw_bar_lds();
       }
     } else if constexpr (STAGE) {
       pw_bar_lds();                                  // the staging tile is complete
-      pw_store_tile(sO, rs_o, g, m0, nt * BN, tid);
+      pw_store_tile(sOt, rs_o, g, m0, nt * BN, tid);
     }
     // weight tile nt + 1 landed -- a COUNTED wait: the PW_ST stores of this tile (and wave 0's
     // statistics atomics) are younger than that DMA and stay in flight under the next tile's
@@ -287,8 +295,9 @@ __global__ __launch_bounds__(PW_NT, 2) void pwconv_kernel(PgemmArgs g, PgemmPro 
 
 template <int KB, bool PRO, bool STATS>
 void pw_launch(const PgemmArgs& g, const PgemmPro& pro, hipStream_t st) {
-  constexpr int bytes = KB * PW_BM * 64 + 2 * KB * PW_BN * 64 + 2 * 2 * PW_BN * 4 +
-                        (KB <= 2 ? PW_OBYTES : 0);
+  constexpr int SBT = KB * PW_BN * 64;
+  constexpr int bytes = KB * PW_BM * 64 + 2 * SBT + 2 * 2 * PW_BN * 4 +
+                        ((KB <= 2 || SBT < PW_OBYTES) ? PW_OBYTES : 0);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)pwconv_kernel<KB, PRO, STATS>,
