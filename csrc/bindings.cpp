@@ -194,11 +194,12 @@ PYBIND11_MODULE(_C, m) {
                     int splits, uintptr_t st, int mode, uintptr_t p_stats, uintptr_t p_rmean,
                     uintptr_t p_rvar, uintptr_t p_gamma, uintptr_t p_beta, int p_group_imgs,
                     float p_inv_count, float p_eps, int p_act) {
-    if (geo.size() != 20) throw std::invalid_argument("hconv: geometry needs 20 ints");
+    if (geo.size() != 21) throw std::invalid_argument("hconv: geometry needs 21 ints");
     if (geo[19] < 0 || geo[19] > 7) throw std::invalid_argument("hconv: SWA in 0..7");
+    if (geo[20] < 0 || geo[20] > 4096) throw std::invalid_argument("hconv: PGRID in 0..4096");
     HconvGeom g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9],
                 geo[10], geo[11], geo[12], geo[13], geo[14], geo[15], geo[16], geo[17], geo[18],
-                geo[19], 0, nullptr};
+                geo[19], geo[20], 0, nullptr};
     const int K = geo[6];
     EpiParams e{P<bf16>(out), K, P<const float>(bias), P<float>(stats), K, group_rows, 0,
                 P<float>(slab), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0};
@@ -415,6 +416,7 @@ PYBIND11_MODULE(_C, m) {
     check_launch("wgrad");
   });
 
+  m.def("bn_configure", &bn_configure);
   m.def("bn_apply", [](uintptr_t y, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                        uintptr_t rmean, uintptr_t rvar, int use_running, int res_mode, uintptr_t res,
                        uintptr_t stats2, uintptr_t gamma2, uintptr_t beta2, uintptr_t rmean2,

@@ -80,10 +80,18 @@ MA_DEV void mean_rstd8(const float* stats, int ld, float inv_cnt, float eps, flo
   }
 }
 
+// 16-byte store, streaming (nontemporal) when NTS: the large-batch passes write tensors far
+// larger than L2 + the Infinity Cache that the next kernel re-reads from HBM anyway
+template <bool NTS>
+MA_DEV void st16(bf16* p, bf16x8 v) {
+  if constexpr (NTS) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)p);
+  else *(bf16x8*)p = v;
+}
+
 // grid.x covers the rows of ONE stat group (grid.y = group), stride multiple of C/8.
 // ACT / RES are compile-time (activation 0-2, residual mode 0-2): with runtime values the
 // per-element code evaluated every activation and residual form and selected.
-template <int ACT, int RES>
+template <int ACT, int RES, bool NTS>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
   const int C8 = a.C >> 3;
   const int T = gridDim.x * NT;
@@ -134,7 +142,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnApplyArgs a) {
         else if (RES == 2) v += bf2f(r[u][k]) * sc2[k] + sh2[k];
         o[k] = f2bf(act_fwd(v, ACT));
       }
-      *(bf16x8*)(a.out + (size_t)(row + u * rpi) * a.C + c) = o;
+      st16<NTS>(a.out + (size_t)(row + u * rpi) * a.C + c, o);
     }
     if (row + U * rpi < row1) load(row + U * rpi);
   }
@@ -354,15 +362,24 @@ int grid_for(size_t chunks, int C8, int per_thread, int cap) {
 }
 }  // namespace
 
+// outputs of at least this many bytes leave through streaming stores (bn_configure): the
+// large-batch passes (ResNet-50 B = 1280: 0.5-2 GB) measured 1-4 % faster with them
+// (bench/bn_bench.py, profiles/r6/bn_bench.jsonl); small ones stay cacheable for their reader
+static long long g_bn_nt_min = 256ll << 20;
+
+void bn_configure(long long nt_min_bytes) { g_bn_nt_min = nt_min_bytes; }
+
 void bn_apply_launch(const BnApplyArgs& a, hipStream_t st) {
   const int G = (a.M + a.group_rows - 1) / a.group_rows;
   const size_t chunks = (size_t)a.group_rows * (a.C / 8);
   const int gx = grid_for(chunks, a.C / 8, 4, (2048 + G - 1) / G);
   const dim3 grid(gx, G);
-#define BN_APPLY_CASE(A, R)                                                   \
-  if (a.act == A && a.res_mode == R) {                                        \
-    hipLaunchKernelGGL((bn_apply_kernel<A, R>), grid, dim3(NT), 0, st, a);    \
-    return;                                                                   \
+  const bool nts = (long long)a.M * a.C * 2 >= g_bn_nt_min;
+#define BN_APPLY_CASE(A, R)                                                             \
+  if (a.act == A && a.res_mode == R) {                                                  \
+    if (nts) hipLaunchKernelGGL((bn_apply_kernel<A, R, true>), grid, dim3(NT), 0, st, a); \
+    else hipLaunchKernelGGL((bn_apply_kernel<A, R, false>), grid, dim3(NT), 0, st, a);    \
+    return;                                                                             \
   }
   BN_APPLY_CASE(0, 0) BN_APPLY_CASE(0, 1) BN_APPLY_CASE(0, 2)
   BN_APPLY_CASE(1, 0) BN_APPLY_CASE(1, 1) BN_APPLY_CASE(1, 2)

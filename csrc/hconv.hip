@@ -324,33 +324,39 @@ constexpr int PHP = 4;              // taps of a slice carrying the next slice's
 template <int BM, int BN, int WM, int NW>
 MA_DEV void epi_lean(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
                      float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM / (16 * NW)][4],
-                     bool stats, const EpiParams& e, int m0, int n0) {
+                     bool stats, const EpiParams& e, int m0, int n0, int vr) {
   constexpr int WN = NW / WM, TM = BM / (16 * WM), TN = BN / (16 * WN);
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w / WN, wn = w % WN;
   const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)e.out, 0, 0x7fffffff, 0x00020000);
-  // lane part of the byte offset (tile-invariant) + the tile origin as the scalar offset
-  const int voff = (((wm * (BM / WM) + (lane & 15)) * e.ldo) + wn * (BN / WN) + 4 * (lane >> 4)) * 2;
-  const int soff = (m0 * e.ldo + n0) * 2;
+  // tile row of this lane's fragment-0 pixel; rows >= vr pad a tile of whole image rows that
+  // do not fill BM (56- / 28-wide images): their stores go past the resource (dropped) and
+  // they add nothing to the statistics -- every wave still issues all TM x TN stores, so the
+  // counted waits stay exact
+  const int rl = wm * (BM / WM) + (lane & 15);
+  const unsigned voff = (unsigned)((((m0 + rl) * e.ldo) + n0 + wn * (BN / WN) + 4 * (lane >> 4)) * 2);
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
+  for (int tm = 0; tm < TM; ++tm) {
+    const bool ok = rl + tm * 16 < vr;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, o), ro,
-                                            voff + (tm * 16 * e.ldo + tn * 16) * 2, soff, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(
+          __builtin_bit_cast(u32x2v, o), ro,
+          ok ? voff + (unsigned)((tm * 16 * e.ldo + tn * 16) * 2) : 0x80000000u, 0, 0);
       if (stats) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float f = bf2f(o[j]);
+          const float f = ok ? bf2f(o[j]) : 0.f;
           rs[tn][j] += f;
           rss[tn][j] = fmaf(f, f, rss[tn][j]);
         }
       }
     }
+  }
 }
 
 // the running sums of (group g, channel tile n0) -> e.stats: DPP row sums, one LDS slot per
@@ -499,11 +505,15 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   const bool ew = wu * 64 < BN;                     // this wave issues the stat atomics
   const int ntn = g.K / BN;
   const int PQ = g.P * g.Q;
-  const int ntiles = (g.N * PQ / BM) * ntn;
+  // output rows per tile: IMG whole images or TR whole rows of one image -- BM, or fewer when
+  // no whole-row count fills BM (56- / 28-wide images: 2 x 56 or 4 x 28 = 112 of 128 rows; the
+  // remaining fragment rows are computed on a clamped halo pixel and dropped in epi_lean)
+  const int VR = g.IMG * g.TR * g.Q;
+  const int ntiles = (g.N * PQ / VR) * ntn;
   const int G = gridDim.x, b = blockIdx.x;
   // a contiguous range of tiles per block, N-tile-major (consecutive tiles share their channel
   // tile and, mostly, their statistics group: epi_lean's running sums)
-  const int mtiles = g.N * PQ / BM;
+  const int mtiles = g.N * PQ / VR;
   const int t0 = (int)((long long)ntiles * b / G);
   const int my = (int)((long long)ntiles * (b + 1) / G) - t0;
   if (my == 0) return;
@@ -558,7 +568,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   auto tile_of = [&](int k, int& m0, int& n0) {
     const int t = t0 + k;
     const int nt = udiv24(t, mtiles, rmt), mt = t - nt * mtiles;
-    m0 = mt * BM;
+    m0 = mt * VR;
     n0 = nt * BN;
   };
   auto set_halo = [&](int m0) {
@@ -577,7 +587,8 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   int aoff[T][TM];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
-    const int row = wm * (BM / WM) + tm * 16 + (lane & 15);
+    const int rowt = wm * (BM / WM) + tm * 16 + (lane & 15);
+    const int row = rowt < VR ? rowt : 0;           // padding rows: a real pixel, result dropped
     const int img = row / (g.TR * g.Q), rem = row - img * g.TR * g.Q;
     const int tr = rem / g.Q, q = rem - tr * g.Q;
     const int hc = q * g.SR;
@@ -836,7 +847,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
       MA_LAP(4, tl);
       if (t == T - 1 && last_sl) {
         // staged in this slice's halo buffer: fully read, refilled only from the next slice on
-        epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0);
+        epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0, VR);
         if (STATS) {
           // flush when the next tile of this block starts another (group, channel tile)
           const int gcur = m0 / e.group_rows;
@@ -1266,7 +1277,7 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
       }
     }
     if (last_sl) {
-      epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0);
+      epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0, BM);
       if (STATS) {
         const int gcur = m0 / e.group_rows;
         if (!hd || n0n != n0 || m0n / e.group_rows != gcur)
@@ -1447,10 +1458,10 @@ int launch_persist(const bf16* src, const bf16* wt, const HconvGeom& g, const Ep
   // 8 waves (two per SIMD: one wave's waits, barriers and DMA issue overlap the other's MFMAs)
   // where the tile has an 8-wave layout; measured 1.513 vs 1.521 and 1.534 vs 1.549 ms/step
   // (two same-box A/Bs), layer2 alone 33.4 vs 35.4 us
-  int gmax = g_persist_grid > 0 ? g_persist_grid : cus / 2;
+  int gmax = g.PGRID > 0 ? g.PGRID : (g_persist_grid > 0 ? g_persist_grid : cus / 2);
   if (gmax > cus) gmax = cus;
   const int waves = g_persist_waves;
-  const int ntiles = (g.N * g.P * g.Q / BM) * (g.K / BN);
+  const int ntiles = (g.N * g.P * g.Q / (g.IMG * g.TR * g.Q)) * (g.K / BN);
   const int grid = ntiles < gmax ? ntiles : gmax;
   if constexpr (WM8 > 0) {
     if constexpr (WM8B > 0) {
@@ -1514,6 +1525,9 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
   const int gx = ((M + bm - 1) / bm) * ((g.K + bn - 1) / bn);
   const int nchunks = g.C >> 6;
   if (splits <= 0 && g.SWA != 0) return 0;       // persistent / row-step halo images: SWA 0
+  // rows per tile: bm, or (persistent kernel only) fewer whole image rows padded to bm
+  const int vr = g.IMG * g.TR * g.Q;
+  if (vr > bm || vr <= 0 || (vr != bm && splits != 0)) return 0;
   if (splits < 0) {
     // row-step persistent kernel (splits -1; 8 waves, 256 x 64 tiles): plain stride-1 input,
     // whole tiles, ghost-BN groups made of whole tiles
@@ -1555,8 +1569,8 @@ int hconv_launch(const bf16* src, const bf16* wt, const HconvGeom& g_in, const E
     // persistent plan (splits == 0): plain whole tiles only, else the per-tile kernel below
     const bool ok = (pro.mode == 0 || pro.mode == 1) &&
                     e.bias == nullptr && !e.accumulate &&
-                    e.bw_sums == nullptr && M % bm == 0 && g.K % bn == 0 &&
-                    (e.stats == nullptr || e.group_rows % bm == 0);
+                    e.bw_sums == nullptr && M % vr == 0 && g.K % bn == 0 &&
+                    (e.stats == nullptr || e.group_rows % vr == 0);
 #define HP_CASE(BM_, BN_, WM4_, WM8_, WM8B_)                                          \
   if (ok && bm == BM_ && bn == BN_ &&                                                  \
       launch_persist<BM_, BN_, WM4_, WM8_, WM8B_>(src, wt, g, e, pro, st))              \

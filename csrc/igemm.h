@@ -134,6 +134,7 @@ struct HconvGeom {
   int HPIX;              // halo pixels per tile = IMG * HT * HWP
   int SWA;               // halo chunk swizzle c ^ ((p + SWA * halo_row(p)) & 7); per-tile
                          // kernel only (the persistent / row-step kernels need 0)
+  int PGRID;             // persistent kernel: this launch's grid (0: the configured default)
   int chunks_per_split;  // 64-channel input slices per K-split
   const bf16* zero;      // 16-byte zero page (set by the launcher)
 };

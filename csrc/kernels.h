@@ -28,6 +28,7 @@ struct BnApplyArgs {
   float eps;
 };
 void bn_apply_launch(const BnApplyArgs& a, hipStream_t st);
+void bn_configure(long long nt_min_bytes);
 
 struct BnBwdArgs {
   const bf16* dout;              // grad of the activation output

@@ -140,6 +140,9 @@ class EngineOptions:
     # per-tile halo kernel: the row-term halo swizzle (HconvGeom.SWA) where the lane-group model
     # finds it conflict-free (layer4: 2.03 -> 0.08 LDS conflict cycles per LDS instruction)
     hconv_swa: bool = True
+    # ResNet-50's stride-1 3x3 convs on the persistent halo kernel with padded row tiles where
+    # measured faster (hconv.MEASURED_PAD; 56-/28-wide images have no whole-row 128/256 tile)
+    hconv_pad: bool = True
     # stride-1 3x3 convs on the row-step persistent kernel (csrc/hconv.hip hrow_kernel) where it
     # measured faster: '1' both batch modes, 'score' / 'train' one, '0' off (hconv.MEASURED_ROW;
     # layer1 scoring conv 51.6 vs 60.4 us, profiles/r5/hrow_bench_v3.jsonl)

@@ -445,7 +445,7 @@ class NativeEngine(object):
                                            train=train) if uh else None
                     if hp is not None:
                         m.plan[u.name, 'hconv'] = hp
-                        slab = max(slab, slab_bytes(sp.M, sp.K, *hp))
+                        slab = max(slab, slab_bytes(sp.M, sp.K, *hp[:3]))
                     # scoring pass: an intra-block conv on the persistent kernel takes its
                     # input's BN + activation in the halo staging (no residual there)
                     hb = None
@@ -456,7 +456,7 @@ class NativeEngine(object):
                                                    stat_only=self.persist_bn == 'stat')
                     if hb is not None:
                         m.plan[u.name, 'hconv_bn'] = hb
-                        slab = max(slab, slab_bytes(sp.M, sp.K, *hb))
+                        slab = max(slab, slab_bytes(sp.M, sp.K, *hb[:3]))
                     if train:
                         if u.need_dgrad and sp.K % 8 == 0:
                             dp, wp = tune.bwd_plans_for(sp, dgrad_plan(sp), wgrad_plan(sp))

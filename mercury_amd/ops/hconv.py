@@ -71,7 +71,7 @@ def lds_bytes(g, bm, bn, splits):
 
 
 # engine-selected settings (config.EngineOptions via ``configure``)
-_CFG = dict(persist=True, plans='', waves=8, grid=0, row='score', wm8=0, swa=True)
+_CFG = dict(persist=True, plans='', waves=8, grid=0, row='score', wm8=0, swa=True, pad=True)
 
 
 def configure(opts):
@@ -80,7 +80,8 @@ def configure(opts):
     _CFG.update(persist=bool(opts.hconv_persist), plans=opts.hconv_plans or '',
                 waves=8 if opts.hconv_persist_waves == 8 else 4,
                 grid=int(opts.hconv_persist_grid), row=opts.hconv_row,
-                wm8=int(opts.hconv_persist_wm8), swa=bool(opts.hconv_swa))
+                wm8=int(opts.hconv_persist_wm8), swa=bool(opts.hconv_swa),
+                pad=bool(opts.hconv_pad))
     lib().hconv_configure(_CFG['grid'], _CFG['waves'], _CFG['wm8'])
 
 
@@ -136,34 +137,50 @@ def row_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
 def persistent_ok(spec: ConvSpec, bm, bn, stats=True, bias=None, pro=None):
     """The persistent kernel runs this conv (else the launcher falls back to the per-tile
     kernel): plain input or the input's BN + activation (no residual, no kept activation), no
-    bias, whole tiles, ghost-BN groups made of whole tiles."""
+    bias, whole tiles (of whole image rows, padded to ``bm`` where none fills it), ghost-BN groups
+    made of whole tiles."""
     if pro is not None and any(pro.get(k) is not None for k in ('res', 'y2', 'keep')):
         return False      # rejected by _pro_args too
     if bias is not None or (bm, bn) not in PERSIST_TILES:
         return False
-    if spec.M % bm or spec.K % bn:
+    ts = _tile_shape(spec, bm, pad=True)
+    if ts is None:
+        return False
+    vr = ts[0] * ts[1] * spec.Q
+    if spec.M % vr or spec.K % bn:
         return False
     grp = spec.group_rows or spec.M
-    return not stats or grp % bm == 0
+    return not stats or grp % vr == 0
 
 
-def _tile_shape(spec: ConvSpec, bm):
-    """(IMG, TR) for a BM-row tile, or None."""
+# padded tiles whose valid rows are below this fraction of BM are not offered
+PAD_MIN = 0.75
+
+
+def _tile_shape(spec: ConvSpec, bm, pad=False):
+    """(IMG, TR) for a BM-row tile, or None.  ``pad`` (the persistent kernel): when no whole
+    image / whole-row count fills BM exactly, the largest that fits (ResNet-50's 56- and 28-wide
+    images: 2 x 56 or 4 x 28 = 112 rows of a 128-row tile); the kernel drops the padding rows."""
     P, Q = spec.P, spec.Q
     PQ = P * Q
+    grp_imgs = spec.group_rows // PQ if spec.group_rows else spec.N
     if bm >= PQ:
-        if bm % PQ:
+        if bm % PQ and not pad:
             return None
         img = bm // PQ
-        if spec.N % img:
+        while img > 1 and (spec.N % img or grp_imgs % img):
+            img -= 1               # a tile's images share one ghost-BN group
+        if spec.N % img or grp_imgs % img or img * PQ < (PAD_MIN * bm if pad else bm):
             return None
-        if spec.group_rows and (spec.group_rows // PQ) % img:
-            return None                       # a tile's images share one ghost-BN group
         return img, P
-    if bm % Q:
+    if bm % Q and not pad:
         return None
     tr = bm // Q
-    if P % tr:
+    while tr > 1 and P % tr:
+        if not pad:
+            return None
+        tr -= 1
+    if P % tr or tr * Q < (PAD_MIN * bm if pad else bm):
         return None
     return 1, tr
 
@@ -177,11 +194,13 @@ def _conflict_cycles(g, bm, bn):
     swa = g.get('SWA', 0)
     per_img = g['HT'] * HWP
     cyc = 0
+    vr = IMG * TR * Q
     for w in range(wm):
         for tm in range(TM):
             pix = []
             for l in range(16):
                 row = w * (bm // wm) + tm * 16 + l
+                row = row if row < vr else 0           # padding rows (the kernel's clamp)
                 img, rem = divmod(row, TR * Q)
                 tr, q = divmod(rem, Q)
                 hc = q * SR
@@ -203,7 +222,7 @@ def _conflict_cycles(g, bm, bn):
     return cyc
 
 
-def geometry(spec: ConvSpec, bm, bn, swa=False):
+def geometry(spec: ConvSpec, bm, bn, swa=False, pad=False):
     """HconvGeom as a dict (csrc/igemm.h), or None when this tile does not fit the conv.
 
     The halo image stores pixel p's 64-channel slice as 8 16-byte chunks, logical chunk c at
@@ -211,10 +230,11 @@ def geometry(spec: ConvSpec, bm, bn, swa=False):
     per-tile kernel, ``swa=True``) the row term SWA are chosen by the lane-group model so the
     A-fragment reads are bank-conflict-free: for layer4's 4x4 images the pitch-6 image with
     SWA = 0 costs 2x the ideal LDS cycles (PMC: 2.03 conflict cycles per LDS instruction in
-    hconv_kernel<128,128,2>), SWA = 6 none.  The persistent / row-step kernels take SWA = 0."""
+    hconv_kernel<128,128,2>), SWA = 6 none.  The persistent / row-step kernels take SWA = 0;
+    ``pad`` allows the persistent kernel's padded row tiles (``_tile_shape``)."""
     if not supported(spec) or (bm, bn) not in _WM:
         return None
-    ts = _tile_shape(spec, bm)
+    ts = _tile_shape(spec, bm, pad)
     if ts is None:
         return None
     IMG, TR = ts
@@ -226,7 +246,7 @@ def geometry(spec: ConvSpec, bm, bn, swa=False):
         HS, SR = 1, st
         HT, HWd = (TR - 1) * st + R, (spec.Q - 1) * st + R
     g = dict(N=spec.N, H=spec.H, W=spec.W, C=spec.C, P=spec.P, Q=spec.Q, K=spec.K, R=R,
-             stride=st, pad=spec.pad, IMG=IMG, TR=TR, HT=HT, HWd=HWd, HS=HS, SR=SR)
+             stride=st, pad=spec.pad, IMG=IMG, TR=TR, HT=HT, HWd=HWd, HS=HS, SR=SR, PGRID=0)
     best = None
     halves = [0] if SR == 1 else [(HWd + 1) // 2 + d for d in range(0, 9)]
     for half in halves:
@@ -247,17 +267,18 @@ def geometry(spec: ConvSpec, bm, bn, swa=False):
 _GEO_CACHE = {}
 
 
-def geometry_cached(spec: ConvSpec, bm, bn, swa=False):
+def geometry_cached(spec: ConvSpec, bm, bn, swa=False, pad=False):
     swa = bool(swa) and _CFG['swa']
     key = (spec.N, spec.H, spec.W, spec.C, spec.K, spec.R, spec.stride, spec.pad,
-           spec.group_rows, bm, bn, swa)
+           spec.group_rows, bm, bn, swa, bool(pad))
     if key not in _GEO_CACHE:
-        _GEO_CACHE[key] = geometry(spec, bm, bn, swa)
+        _GEO_CACHE[key] = geometry(spec, bm, bn, swa, pad)
     return _GEO_CACHE[key]
 
 
+# PGRID: the persistent kernel's grid for this launch (0: the configured default, half the CUs)
 _ORDER = ('N', 'H', 'W', 'C', 'P', 'Q', 'K', 'R', 'stride', 'pad', 'IMG', 'TR', 'HT', 'HWd',
-          'HWP', 'HALF', 'HS', 'SR', 'HPIX', 'SWA')
+          'HWP', 'HALF', 'HS', 'SR', 'HPIX', 'SWA', 'PGRID')
 
 
 def plan(spec: ConvSpec, min_blocks=256):
@@ -337,6 +358,38 @@ def _plan_override(key):
 # (1.307 vs 1.333 ms/step, profiles/r5/ab_persist_bn_scope.json)
 MEASURED_ROW = {(320, 32, 64, 64): (256, 64, -1), (320, 16, 128, 128): (256, 64, -1)}
 
+# Padded-row persistent plans: ResNet-50's stride-1 3x3 convs (56/28/14/7-wide images, no
+# whole-row 64/128/256-pixel tile), keyed (N, H, C, K) -> (plan, input BN in the halo staging).
+# The 4th plan element is the launch's grid: all 256 CUs (these run at B = 1280 / 128, not beside
+# a latency-bound train chain).  bench/hconv_r50_bench.py, graph-timed (profiles/r6/
+# hconv_r50.jsonl), us: scoring B = 1280 layer1 441.6 vs igemm 586 (with its input BN folded
+# 518 vs 586 + a 188 us bn_apply pass), layer3 354 vs 406; train B = 128 layer1 53.8 vs 88.5,
+# layer2 50.1 vs 65.5, layer3 44.4 vs 53.4, layer4 44.0 vs 68.7.  Layer2 / layer4 scoring stay
+# on igemm (415 / 349 vs the engine's tuned 420 / 335), and the folded BN only pays at layer1
+# (layer2 568 vs 415 + 100, layer3 596 vs 354 + 42: the transform runs once per N tile)
+MEASURED_PAD = {
+    (1280, 56, 64, 64): ((256, 64, 0, 256), True),
+    (1280, 14, 256, 256): ((256, 64, 0, 256), False),
+    (128, 56, 64, 64): ((256, 64, 0, 256), False),
+    (128, 28, 128, 128): ((256, 64, 0, 256), False),
+    (128, 14, 256, 256): ((256, 64, 0, 256), False),
+    (128, 7, 512, 512): ((256, 64, 0, 256), False),
+}
+
+
+def _pad_plan(spec: ConvSpec, bias=False):
+    """(plan, bn_ok) of MEASURED_PAD for this conv when it runs there, else None."""
+    if not _CFG['pad'] or bias or spec.H != spec.W or spec.stride != 1:
+        return None
+    e = MEASURED_PAD.get((spec.N, spec.H, spec.C, spec.K))
+    if e is None:
+        return None
+    p = e[0]
+    g = geometry_cached(spec, p[0], p[1], pad=True)
+    if g is None or lds_bytes(g, p[0], p[1], 0) > LDS_MAX or not persistent_ok(spec, p[0], p[1]):
+        return None
+    return e
+
 
 def engine_plan(spec: ConvSpec, bias=False, train=None):
     """The plan the engine runs hconv with for this conv, or None (use igemm): measured
@@ -346,6 +399,9 @@ def engine_plan(spec: ConvSpec, bias=False, train=None):
     if not supported(spec):
         return None
     found, p = _plan_override((spec.N, spec.H, spec.C, spec.K))
+    pp = None if found else _pad_plan(spec, bias)
+    if pp is not None:
+        return pp[0]
     if found and spec.H == spec.W:
         if p is None:
             return None
@@ -384,6 +440,16 @@ def persist_bn_plan(spec: ConvSpec, group_imgs, row_only=False, stat_only=False)
     """The persistent plan with the input's BN + activation in the halo staging (no residual),
     or None: the row-step kernel where it runs this conv, else (unless ``row_only``) the per-tap
     persistent kernel.  Scoring pass only (EngineOptions.persist_bn, engine)."""
+    pp = _pad_plan(spec)
+    if pp is not None:
+        # padded-row plan: the table says whether the fold pays
+        if not pp[1]:
+            return None
+        g = geometry_cached(spec, pp[0][0], pp[0][1], pad=True)
+        pro = dict(stats=True, group_imgs=group_imgs)
+        if lds_bytes(g, pp[0][0], pp[0][1], 0) + persist_table_bytes(spec, pro) > LDS_MAX:
+            return None
+        return pp[0]
     p = engine_plan(spec, train=False)
     if p is not None and p[2] < 0:
         # stat_only: only where the row-step kernel keeps its weights stationary (C = K = 64,
@@ -436,7 +502,9 @@ def hconv_fwd(x, w, out, spec: ConvSpec, plan_=None, stats=None, bias=None, slab
     if p is None:
         raise ValueError('hconv does not support this conv')
     bm, bn, splits = p[:3]
-    g = geometry_cached(spec, bm, bn, swa=splits > 0)
+    g = geometry_cached(spec, bm, bn, swa=splits > 0, pad=splits == 0)
+    if g is not None and splits == 0 and len(p) > 3 and p[3]:
+        g = dict(g, PGRID=int(p[3]))              # a plan's own persistent grid
     if splits < 0:
         if g is None or row_lds_bytes(g, bm, bn, splits) > LDS_MAX:
             raise ValueError('hconv: row-step tile %dx%d does not fit this conv' % (bm, bn))

@@ -134,6 +134,14 @@ PERSIST_CASES = [
     (128, 32, 64, 128, 2, (64, 64), 32),     # stride 2 (even / odd column halves)
     (320, 8, 256, 256, 1, (128, 64), 32),    # IMG = 2, four slices, four N tiles
     (320, 4, 512, 512, 1, (64, 64), 32),     # IMG = 4, eight slices
+    # padded row tiles (no whole-row count fills BM): ResNet-50's 56/28/14/7-wide images
+    (16, 56, 64, 64, 1, (128, 64), 8),       # 2 x 56 = 112 of 128 rows
+    (16, 56, 64, 64, 1, (256, 64), 8),       # 4 x 56 = 224 of 256
+    (16, 28, 128, 128, 1, (128, 64), 8),     # 4 x 28 = 112, two slices, two N tiles
+    (16, 28, 64, 64, 1, (64, 64), 8),        # 2 x 28 = 56 of 64
+    (16, 14, 256, 256, 1, (128, 64), 8),     # 7 x 14 = 98 of 128
+    (16, 7, 512, 512, 1, (128, 64), 8),      # IMG = 2 images of 49 = 98 of 128
+    (16, 56, 128, 128, 2, (64, 64), 8),      # stride 2 to 28 wide: 2 x 28 = 56 of 64
 ]
 
 
@@ -152,9 +160,12 @@ def test_hconv_persistent(case, with_stats):
     G = N // gimgs if gimgs else 1
     if gimgs:
         spec.group_rows = gimgs * spec.P * spec.Q
-    geo = H.geometry(spec, bm, bn)
+    geo = H.geometry(spec, bm, bn, pad=True)
     assert geo is not None and H.lds_bytes(geo, bm, bn, 0) <= H.LDS_MAX
     assert H.persistent_ok(spec, bm, bn, stats=with_stats)
+    padded = geo['IMG'] * geo['TR'] * geo['Q'] < bm
+    # padded tiles also run on this launch's own grid (the plan's 4th element, PGRID)
+    plan = (bm, bn, 0, 256) if padded else (bm, bn, 0)
     g = torch.Generator(device='cpu').manual_seed(5)
     x = bf(torch.randn(N, C, Hh, Hh, generator=g) * 1.5 + 0.3)
     w = bf(torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9))
@@ -176,7 +187,7 @@ def test_hconv_persistent(case, with_stats):
     wk, _ = ops.pack_conv_weight(w.to(DEV))
     out = torch.full((spec.M, K), float('nan'), dtype=torch.bfloat16, device=DEV)
     ostats = torch.zeros(G, 2, K, device=DEV) if with_stats else None
-    H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, (bm, bn, 0), stats=ostats, pro=pro)
+    H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out, spec, plan, stats=ostats, pro=pro)
     torch.cuda.synchronize()
     if (bm, bn) == (128, 64) and H.persist_waves() == 8:
         # the 4 x 2 wave layout of the same tile (EngineOptions.hconv_persist_wm8) must agree
@@ -184,8 +195,7 @@ def test_hconv_persistent(case, with_stats):
         ost2 = torch.zeros_like(ostats) if ostats is not None else None
         ops.lib().hconv_configure(H._CFG['grid'], 8, 4)
         try:
-            H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out2, spec, (bm, bn, 0), stats=ost2,
-                        pro=pro)
+            H.hconv_fwd(ops.to_nhwc(x.to(DEV)), wk, out2, spec, plan, stats=ost2, pro=pro)
             torch.cuda.synchronize()
         finally:
             ops.lib().hconv_configure(H._CFG['grid'], H.persist_waves(), H._CFG['wm8'])
