@@ -143,6 +143,9 @@ class EngineOptions:
     # ResNet-50's stride-1 3x3 convs on the persistent halo kernel with padded row tiles where
     # measured faster (hconv.MEASURED_PAD; 56-/28-wide images have no whole-row 128/256 tile)
     hconv_pad: bool = True
+    # forward convs with the BN-apply prologue on their measured split-K plans
+    # (ops.conv.MEASURED_PRO; MobileNetV2's train-batch project convs)
+    pro_plans: bool = True
     # stride-1 3x3 convs on the row-step persistent kernel (csrc/hconv.hip hrow_kernel) where it
     # measured faster: '1' both batch modes, 'score' / 'train' one, '0' off (hconv.MEASURED_ROW;
     # layer1 scoring conv 51.6 vs 60.4 us, profiles/r5/hrow_bench_v3.jsonl)

@@ -34,7 +34,7 @@ import torch.distributed as dist
 from .. import ops
 from ..ops import hconv, tune
 from ..ops.conv import (ConvSpec, cpad8, dgrad_plan, fwd_plan, pgemm_ok, pgemm_plain_wins,
-                        pgemm_plan, pgemm_pro_wins, pwconv_ok, pwconv_plain_wins,
+                        pgemm_plan, pgemm_pro_wins, pro_plan, pwconv_ok, pwconv_plain_wins,
                         pwconv_pro_wins, slab_bytes,
                         stem_ok, wgrad_plan)
 from ..ops.conv import pro_ok as conv_pro_ok
@@ -431,6 +431,11 @@ class NativeEngine(object):
                     m.plan[u.name, 'fwd'] = p = tune.fwd_plan_for(
                         sp, fwd_plan(sp, min_blocks=mb) if mb else fwd_plan(sp))
                     slab = max(slab, slab_bytes(sp.M, sp.K, *p[:3]))
+                    pp = pro_plan(sp) if self.opts.pro_plans else None
+                    if pp is not None:
+                        # the plan it runs with when it takes its input's BN in the prologue
+                        m.plan[u.name, 'fwd_pro'] = pp
+                        slab = max(slab, slab_bytes(sp.M, sp.K, *pp))
                     if self.use_pgemm and pgemm_ok(sp) and u.b_seg is None:
                         m.plan[u.name, 'pgemm'] = pgemm_plan(sp)
                         coef = max(coef, m.G * 2 * sp.Cp)
@@ -562,8 +567,12 @@ class NativeEngine(object):
                             bias=self._pview(u.b_seg) if u.b_seg is not None else None)
         else:
             ops.conv_fwd(x, self.w_krsc[u.name], y, sp, stats=stats, slab=m.slab,
-                         plan=m.plan[u.name, 'fwd'],
+                         plan=self._pro_plan(m, u) if pro is not None else m.plan[u.name, 'fwd'],
                          bias=self._pview(u.b_seg) if u.b_seg is not None else None, pro=pro)
+
+    def _pro_plan(self, m, u):
+        """igemm plan of ``u`` when it applies its input's BN in the prologue."""
+        return m.plan.get((u.name, 'fwd_pro'), m.plan[u.name, 'fwd'])
 
     def _igemm_only(self, m, u):
         """True when _conv_fwd(m, u, ..., pro=None) runs u on the plain igemm kernel."""
@@ -624,7 +633,7 @@ class NativeEngine(object):
         if pg is not None:
             return pg
         sp = m.spec[nxt.name]
-        if not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=m.train):
+        if not conv_pro_ok(sp, self._pro_plan(m, nxt), keep=m.train):
             return None
         su = m.spec[u.name]
         d = dict(gamma=self._gamma(u), beta=self._beta(u), act=u.act, eps=BN_EPS,
@@ -673,7 +682,7 @@ class NativeEngine(object):
         sp = m.spec[nxt.name]
         if (nxt.name, 'pgemm') in m.plan and pgemm_plain_wins(sp):
             return None
-        if sp.R != 1 or not conv_pro_ok(sp, m.plan[nxt.name, 'fwd'], keep=True):
+        if sp.R != 1 or not conv_pro_ok(sp, self._pro_plan(m, nxt), keep=True):
             return None
         su = m.spec[u.name]
         d = dict(gamma=self._gamma(u), beta=self._beta(u), act=act, eps=BN_EPS, keep=out,

@@ -110,6 +110,26 @@ def dgrad_plan(spec: ConvSpec):
     return pick_tiles(M, N, kchunks, 0)
 
 
+# Forward convs that take the BN-apply prologue (``pro``): the prologue adds per-chunk loads and
+# VALU to every K stage, so deep-input / narrow-output convs at the train batch want more K
+# splits than the plain-conv tuning picked.  MobileNetV2-CIFAR's project convs at B = 32, keyed
+# (N, H, C, K) of a 1x1 conv (bench/pro_split_bench.py, graph-timed, profiles/r6/pro_split.jsonl),
+# us vs the tuned plain plan: 960->160 @4 12.9 vs 16.4, 960->320 @4 14.9 vs 16.6, 576->160 @4
+# 11.5 vs 15.6, 576->96 @8 12.3 vs 15.8, 384->64 @8 10.8 vs 13.1, 384->96 @8 11.2 vs 15.0
+MEASURED_PRO = {
+    (32, 4, 960, 160): (64, 64, 6), (32, 4, 960, 320): (64, 128, 6),
+    (32, 4, 576, 160): (64, 64, 8), (32, 8, 576, 96): (64, 64, 8),
+    (32, 8, 384, 64): (64, 64, 3), (32, 8, 384, 96): (64, 64, 4),
+}
+
+
+def pro_plan(spec: ConvSpec):
+    """The measured plan for this conv when it runs with the input prologue, or None."""
+    if spec.R != 1 or spec.S != 1 or spec.H != spec.W or spec.group_rows not in (0, spec.M):
+        return None
+    return MEASURED_PRO.get((spec.N, spec.H, spec.C, spec.K))
+
+
 ATOMIC_BUDGET = 1_200_000   # fp32 atomic adds per wgrad launch before splitting stops paying
 
 
