@@ -2,7 +2,7 @@
 convs (narrow output, deep input, 4x4 / 8x8 images at B = 32: 16-48 blocks per launch),
 graph-timed.
 
-    python bench/pro_split_bench.py
+    python bench/pro_split_bench.py [--all]
 
 One JSON line per (shape, tile, splits): microseconds, with the tuned plain-conv plan marked.
 """
@@ -17,7 +17,12 @@ from gtime import gtime  # noqa: E402
 
 # (N, H, C, K): MobileNetV2-CIFAR project / expand convs at the train batch
 SHAPES = [(32, 4, 960, 160), (32, 4, 960, 320), (32, 4, 576, 160), (32, 8, 576, 96),
-          (32, 8, 384, 64), (32, 8, 384, 96), (32, 16, 192, 32), (32, 16, 144, 32)]
+          (32, 8, 384, 64), (32, 8, 384, 96), (32, 16, 192, 32), (32, 16, 144, 32),
+          # expand / remaining 1x1 convs (--all)
+          (32, 4, 160, 960), (32, 4, 320, 1280), (32, 4, 160, 320), (32, 8, 64, 384),
+          (32, 8, 96, 576), (32, 8, 192, 64), (32, 8, 64, 96), (32, 16, 32, 192),
+          (32, 32, 24, 144), (32, 32, 16, 96), (32, 32, 96, 24), (32, 32, 144, 24),
+          (32, 32, 32, 16), (32, 32, 32, 32)]
 
 
 def main():
@@ -26,7 +31,7 @@ def main():
     from mercury_amd.ops import tune
     from mercury_amd.ops.conv import ConvSpec, fwd_plan, slab_bytes
     dev = 'cuda'
-    for N, H, C, K in SHAPES:
+    for N, H, C, K in (SHAPES if '--all' in sys.argv else SHAPES[:8]):
         sp = ConvSpec(N, H, H, C, K, 1, 1, 1, 0)
         torch.manual_seed(0)
         y = ops.to_nhwc(torch.randn(N, C, H, H, device=dev))
@@ -41,7 +46,7 @@ def main():
         ost = torch.zeros(2 * K, device=dev)
         tuned = tuple(tune.fwd_plan_for(sp, fwd_plan(sp))[:3])
         ref = None
-        for bm, bn in ((64, 64), (64, 128), (128, 64)):
+        for bm, bn in ((64, 64), (64, 128), (128, 64), (128, 128)):
             for s in (1, 2, 3, 4, 6, 8):
                 if s > max(1, (C // 8 + 7) // 8):
                     continue

@@ -115,11 +115,15 @@ def dgrad_plan(spec: ConvSpec):
 # splits than the plain-conv tuning picked.  MobileNetV2-CIFAR's project convs at B = 32, keyed
 # (N, H, C, K) of a 1x1 conv (bench/pro_split_bench.py, graph-timed, profiles/r6/pro_split.jsonl),
 # us vs the tuned plain plan: 960->160 @4 12.9 vs 16.4, 960->320 @4 14.9 vs 16.6, 576->160 @4
-# 11.5 vs 15.6, 576->96 @8 12.3 vs 15.8, 384->64 @8 10.8 vs 13.1, 384->96 @8 11.2 vs 15.0
+# 11.5 vs 15.6, 576->96 @8 12.3 vs 15.8, 384->64 @8 10.8 vs 13.1, 384->96 @8 11.2 vs 15.0; the
+# narrow-input expansions want different tiles (profiles/r6/pro_split_all.jsonl): 64->96 @8 7.3
+# vs 8.3, 32->192 @16 9.6 vs 11.1, 16->96 @32 14.7 vs 16.1
 MEASURED_PRO = {
     (32, 4, 960, 160): (64, 64, 6), (32, 4, 960, 320): (64, 128, 6),
     (32, 4, 576, 160): (64, 64, 8), (32, 8, 576, 96): (64, 64, 8),
     (32, 8, 384, 64): (64, 64, 3), (32, 8, 384, 96): (64, 64, 4),
+    (32, 8, 64, 96): (64, 64, 1), (32, 16, 32, 192): (128, 64, 1),
+    (32, 32, 16, 96): (128, 64, 1),
 }
 
 
