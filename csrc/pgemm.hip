@@ -77,6 +77,16 @@ MA_DEV float pg_row16_sum(float v) {
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// Output-channel order of the weight tile in LDS: within every 32 rows, LDS row
+// h * 16 + 4 q + j (fragment half h, lane group q, accumulator element j) holds channel
+// 8 q + 4 h + j, so a lane's accumulators of the fragment pair (2t, 2t + 1) are 8 CONSECUTIVE
+// channels of one pixel: the epilogue leaves as 16-byte stores (16 pixels x 64 contiguous bytes
+// per wave instruction instead of 16 x 32)
+MA_DEV int pg_perm(int r) {
+  const int r5 = r & 31;
+  return (r & ~31) | (((r5 >> 2) & 3) << 3) | ((r5 >> 4) << 2) | (r5 & 3);
+}
+
 // wait until a step's DMA pieces have landed: `newer` = whole steps (P pieces each) this wave
 // issued after it (0 .. S-2; wave-uniform, so the branches are scalar).  VMEM ops issued after
 // those (epilogue stores, stat atomics) are not counted: the wait then also covers some of
@@ -164,7 +174,7 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro p
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int nr = 16 * (wu + PG_NW * j) + prow;
-      const int n = nt * BN + nr;
+      const int n = nt * BN + pg_perm(nr);
       boff[j] = (n < g.N && nr < BN) ? (unsigned)((n * g.K + lc * 8) * 2) : PG_OOB;
     }
   };
@@ -279,7 +289,8 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro p
         rss[tn][j] = pg_row16_sum(rss[tn][j]);
       }
       if ((lane & 15) == 0) {
-        const int cl = wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+        // (pg_perm: fragment tn = 2 t + h holds channels 32 t + 8 q + 4 h + j)
+        const int cl = wn * (BN / WN) + (tn >> 1) * 32 + 8 * (lane >> 4) + 4 * (tn & 1);
         *(f32x4*)(red + (wm * 2) * BN + cl) = f32x4{rs[tn][0], rs[tn][1], rs[tn][2], rs[tn][3]};
         *(f32x4*)(red + (wm * 2 + 1) * BN + cl) = f32x4{rss[tn][0], rss[tn][1], rss[tn][2], rss[tn][3]};
       }
@@ -303,12 +314,14 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro p
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
 
-  // ---- epilogue of one tile: bf16 round, 8-byte stores from the registers, statistics
+  // ---- epilogue of one tile: bf16 round, 16-byte stores from the registers (a fragment pair's
+  // 8 consecutive channels per lane, pg_perm), statistics
+  static_assert(TN % 2 == 0, "fragment pairs");
   auto epilogue = [&](int t) {
     const int mt = t / ntn, nt = t - mt * ntn;
     const int m0 = mt * BM, n0 = nt * BN;
     const int rbase = m0 + wm * (BM / WM) + (lane & 15);
-    const int cbase = n0 + wn * (BN / WN) + 4 * (lane >> 4);
+    const int cbase = n0 + wn * (BN / WN) + 8 * (lane >> 4);
     int g0 = 0, bnd = 0x7fffffff;
     bool straddle = false;
     if constexpr (STATS) {
@@ -322,25 +335,30 @@ __global__ __launch_bounds__(PG_NT, 1) void pgemm_kernel(PgemmArgs g, PgemmPro p
     }
     // rows < bnd of this tile (all rows unless it straddles a group edge)
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int col = cbase + tn * 16;
-      const bool cok = col < g.N;
+    for (int tp = 0; tp < TN / 2; ++tp) {
+      const int col = cbase + tp * 32;
+      const bool cok = col < g.N;                 // (N % 8 == 0: 8 channels whole or out)
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int row = rbase + tm * 16;
-        bf16x4 o;
+        bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[tm][tn][j]);
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(acc[tm][2 * tp][j]);
+          o[4 + j] = f2bf(acc[tm][2 * tp + 1][j]);
+        }
         const bool ok = row < g.M && cok;
         const unsigned voff = ok ? (unsigned)(((long long)row * g.ldo + col) * 2) : PG_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rs_o, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs_o, voff, 0, 0);
         if constexpr (STATS) {
           const float mk = row < g.M && row < bnd ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]) * mk;
-            rs[tn][j] += f;
-            rss[tn][j] += f * f;
+            const float f = bf2f(o[j]) * mk, f2 = bf2f(o[4 + j]) * mk;
+            rs[2 * tp][j] += f;
+            rss[2 * tp][j] += f * f;
+            rs[2 * tp + 1][j] += f2;
+            rss[2 * tp + 1][j] += f2 * f2;
           }
         }
       }
