@@ -26,6 +26,22 @@ DEFAULT_TIMEOUT_S = int(os.environ.get('MERCURY_PG_TIMEOUT', '600'))
 
 
 def free_port():
+    """A free TCP port for a local rendezvous, drawn BELOW the kernel's ephemeral range
+    (32768-60999): a port the OS hands out for binding 0 is one any other socket (an RCCL / gloo
+    connection of a neighbouring test, the TCPStore clients) may be given before rank 0 listens on
+    it -- a 2-rank GPU test once failed with EADDRINUSE that way."""
+    import random
+    rng = random.Random()
+    for _ in range(64):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(('127.0.0.1', p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
     p = s.getsockname()[1]
