@@ -321,20 +321,67 @@ constexpr int PHP = 4;              // taps of a slice carrying the next slice's
 // tile) and the cross-lane / cross-wave reduction and the global atomics (epi_flush) run once per
 // (group, channel tile) the block touches instead of once per tile.  PMC, ResNet-18 scoring pass:
 // the per-tile staged epilogue made the kernel 4.15 VALU per MFMA (profiles/r4/pmc).
-template <int BM, int BN, int WM, int NW>
+// Weight-row order of the persistent kernels' ring with PERM: within every 32 rows, LDS row
+// h * 16 + 4 q + j (fragment half h, lane group q, accumulator element j) holds channel
+// 8 q + 4 h + j, so a lane's accumulators of fragments (2t, 2t + 1) are 8 consecutive channels
+// of one pixel and leave as ONE 16-byte store (pgemm.hip pg_perm)
+MA_DEV int hc_perm(int r) {
+  const int r5 = r & 31;
+  return (r & ~31) | (((r5 >> 2) & 3) << 3) | ((r5 >> 4) << 2) | (r5 & 3);
+}
+
+// stores per wave of one tile (the counted waits include them)
+template <int BM, int BN, int WM, int NW, bool PERM>
+constexpr int epi_stores() {
+  return (BM / (16 * WM)) * (BN * WM / (16 * NW)) / (PERM ? 2 : 1);
+}
+
+template <int BM, int BN, int WM, int NW, bool PERM = false>
 MA_DEV void epi_lean(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
                      float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM / (16 * NW)][4],
                      bool stats, const EpiParams& e, int m0, int n0, int vr) {
   constexpr int WN = NW / WM, TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(!PERM || TN % 2 == 0, "fragment pairs");
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w / WN, wn = w % WN;
   const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)e.out, 0, 0x7fffffff, 0x00020000);
   // tile row of this lane's fragment-0 pixel; rows >= vr pad a tile of whole image rows that
   // do not fill BM (56- / 28-wide images): their stores go past the resource (dropped) and
-  // they add nothing to the statistics -- every wave still issues all TM x TN stores, so the
+  // they add nothing to the statistics -- every wave still issues all its stores, so the
   // counted waits stay exact
   const int rl = wm * (BM / WM) + (lane & 15);
+  if constexpr (PERM) {
+    const unsigned voff =
+        (unsigned)((((m0 + rl) * e.ldo) + n0 + wn * (BN / WN) + 8 * (lane >> 4)) * 2);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const bool ok = rl + tm * 16 < vr;
+#pragma unroll
+      for (int tp = 0; tp < TN / 2; ++tp) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(acc[tm][2 * tp][j]);
+          o[4 + j] = f2bf(acc[tm][2 * tp + 1][j]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, o), ro,
+            ok ? voff + (unsigned)((tm * 16 * e.ldo + tp * 32) * 2) : 0x80000000u, 0, 0);
+        if (stats) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float f = ok ? bf2f(o[j]) : 0.f, f2 = ok ? bf2f(o[4 + j]) : 0.f;
+            rs[2 * tp][j] += f;
+            rss[2 * tp][j] = fmaf(f, f, rss[2 * tp][j]);
+            rs[2 * tp + 1][j] += f2;
+            rss[2 * tp + 1][j] = fmaf(f2, f2, rss[2 * tp + 1][j]);
+          }
+        }
+      }
+    }
+    return;
+  }
   const unsigned voff = (unsigned)((((m0 + rl) * e.ldo) + n0 + wn * (BN / WN) + 4 * (lane >> 4)) * 2);
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
@@ -362,7 +409,7 @@ MA_DEV void epi_lean(const f32x4 (&acc)[BM / (16 * WM)][BN * WM / (16 * NW)],
 // the running sums of (group g, channel tile n0) -> e.stats: DPP row sums, one LDS slot per
 // (wave row, channel), one atomic pair per channel.  ``red``: 2 * WM * BN floats of LDS that no
 // wave reads or DMAs into until the next slice's first barrier.  Block-uniform call.
-template <int BM, int BN, int WM, int NW>
+template <int BM, int BN, int WM, int NW, bool PERM = false>
 MA_DEV void epi_flush(float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM / (16 * NW)][4],
                       float* red, const EpiParams& e, int g, int n0) {
   constexpr int WN = NW / WM, TN = BN / (16 * WN);
@@ -379,7 +426,8 @@ MA_DEV void epi_flush(float (&rs)[BN * WM / (16 * NW)][4], float (&rss)[BN * WM 
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      float* r = red + wm * 2 * BN + wn * (BN / WN) + tn * 16 + 4 * (lane >> 4);
+      float* r = red + wm * 2 * BN + wn * (BN / WN) +
+                 (PERM ? (tn >> 1) * 32 + 8 * (lane >> 4) + 4 * (tn & 1) : tn * 16 + 4 * (lane >> 4));
       *(f32x4*)r = f32x4{rs[tn][0], rs[tn][1], rs[tn][2], rs[tn][3]};
       *(f32x4*)(r + BN) = f32x4{rss[tn][0], rss[tn][1], rss[tn][2], rss[tn][3]};
     }
@@ -492,7 +540,9 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   static_assert(BI >= 1 && BN % PPX == 0, "whole weight pieces per wave");
   constexpr int SLOT = BN * 128;
   constexpr int R = 3, T = R * R;
-  constexpr int ST = TM * TN;                       // epilogue stores per wave (epi_lean)
+  // 16-byte epilogue stores from fragment pairs (hc_perm weight-row order) where TN is even
+  constexpr bool PERM = TN % 2 == 0;
+  constexpr int ST = epi_stores<BM, BN, WM, NW, PERM>();   // epilogue stores per wave
   constexpr int PHI = HRC / PHP;                    // halo pieces per wave on a carrying tap
   static_assert(PHP <= T - 3, "a slice's halo lands >= 2 steps before its first read");
   static_assert(HRC % PHP == 0 && HRC <= HRMAX, "halo piece capacity");
@@ -603,7 +653,10 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
   }
   unsigned boff[BI];                                 // weight rows this lane fetches (bytes)
 #pragma unroll
-  for (int j = 0; j < BI; ++j) boff[j] = ((8 * (w + NW * j) + (lane >> 3)) * Kt + lc * 8) * 2;
+  for (int j = 0; j < BI; ++j) {
+    const int r = 8 * (w + NW * j) + (lane >> 3);  // ring row; the channel it holds:
+    boff[j] = (((PERM ? hc_perm(r) : r)) * Kt + lc * 8) * 2;
+  }
   // B-fragment byte offsets inside a ring slot (tap-invariant)
   int bfo[2][TN];
 #pragma unroll
@@ -847,12 +900,13 @@ __global__ __launch_bounds__(64 * NW, 1) void hconv_persist_kernel(const bf16* _
       MA_LAP(4, tl);
       if (t == T - 1 && last_sl) {
         // staged in this slice's halo buffer: fully read, refilled only from the next slice on
-        epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0, VR);
+        epi_lean<BM, BN, WM, NW, PERM>(acc, rsum, rsq, STATS, e, m0, n0, VR);
         if (STATS) {
           // flush when the next tile of this block starts another (group, channel tile)
           const int gcur = m0 / e.group_rows;
           if (!hn || n0n != n0 || m0n / e.group_rows != gcur)
-            epi_flush<BM, BN, WM, NW>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur, n0);
+            epi_flush<BM, BN, WM, NW, PERM>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur,
+                                            n0);
         }
         MA_LAP(5, tl);
 #pragma unroll

@@ -364,11 +364,13 @@ MEASURED_ROW = {(320, 32, 64, 64): (256, 64, -1), (320, 16, 128, 128): (256, 64,
 # a latency-bound train chain).  bench/hconv_r50_bench.py, graph-timed (profiles/r6/
 # hconv_r50.jsonl), us: scoring B = 1280 layer1 441.6 vs igemm 586 (with its input BN folded
 # 518 vs 586 + a 188 us bn_apply pass), layer3 354 vs 406; train B = 128 layer1 53.8 vs 88.5,
-# layer2 50.1 vs 65.5, layer3 44.4 vs 53.4, layer4 44.0 vs 68.7.  Layer2 / layer4 scoring stay
-# on igemm (415 / 349 vs the engine's tuned 420 / 335), and the folded BN only pays at layer1
-# (layer2 568 vs 415 + 100, layer3 596 vs 354 + 42: the transform runs once per N tile)
+# layer2 50.1 vs 65.5, layer3 44.4 vs 53.4, layer4 44.0 vs 68.7.  With the 16-byte epilogue
+# stores (hc_perm; profiles/r6/hconv_perm/) scoring layer2 398-404 vs the engine's tuned igemm
+# ~420 joined; layer4 scoring stays on igemm (363 vs 335), and the folded BN only pays at
+# layer1 (layer2 568 vs 415 + 100, layer3 596 vs 354 + 42: the transform runs once per N tile)
 MEASURED_PAD = {
     (1280, 56, 64, 64): ((256, 64, 0, 256), True),
+    (1280, 28, 128, 128): ((256, 64, 0, 256), False),
     (1280, 14, 256, 256): ((256, 64, 0, 256), False),
     (128, 56, 64, 64): ((256, 64, 0, 256), False),
     (128, 28, 128, 128): ((256, 64, 0, 256), False),
