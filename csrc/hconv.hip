@@ -972,7 +972,8 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
   constexpr int WSLOT = WROWS * 128;                // bytes per ring slot
   static_assert(HRC % 2 == 0 && HRC <= HRMAX, "halo pieces split over rows 0 and 1");
   constexpr int HH = HRC / 2;                       // halo pieces per wave on rows 0 and 1
-  constexpr int ST = TM * TN;                       // epilogue stores per wave (epi_lean)
+  constexpr bool PERM = TN % 2 == 0;                // 16-byte epilogue stores (hc_perm rows)
+  constexpr int ST = epi_stores<BM, BN, WM, NW, PERM>();   // epilogue stores per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1132,8 +1133,8 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
 #pragma unroll
   for (int q = 0; q < BI; ++q) {
     const int row = 8 * (w + NW * q) + (lane >> 3);
-    const int j = row / BN, n = row - j * BN;
-    boff[q] = (unsigned)((n * Kt + j * g.C + lc * 8) * 2);
+    const int j = row / BN, n = row - j * BN;      // (tap, ring row); the channel it holds:
+    boff[q] = (unsigned)(((PERM ? hc_perm(n) : n) * Kt + j * g.C + lc * 8) * 2);
   }
   // B-fragment byte offsets inside a slot, tap 0 of the row (tap j adds j * BN * 128)
   int bfo[2][TN];
@@ -1331,11 +1332,12 @@ __global__ __launch_bounds__(64 * NW, 1) void hrow_kernel(const bf16* __restrict
       }
     }
     if (last_sl) {
-      epi_lean<BM, BN, WM, NW>(acc, rsum, rsq, STATS, e, m0, n0, BM);
+      epi_lean<BM, BN, WM, NW, PERM>(acc, rsum, rsq, STATS, e, m0, n0, BM);
       if (STATS) {
         const int gcur = m0 / e.group_rows;
         if (!hd || n0n != n0 || m0n / e.group_rows != gcur)
-          epi_flush<BM, BN, WM, NW>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur, n0);
+          epi_flush<BM, BN, WM, NW, PERM>(rsum, rsq, (float*)(smem + buf * HBYTES), e, gcur,
+                                          n0);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
