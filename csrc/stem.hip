@@ -33,9 +33,20 @@ MA_DEV float st_row16_sum(float v) {
 }
 typedef uint32_t st_u32x2 __attribute__((ext_vector_type(2)));
 
+// Output-channel order of the weight rows in LDS: within every 32 rows, row h * 16 + 4 q + j
+// (fragment half h, lane group q, accumulator element j) holds channel 8 q + 4 h + j, so a lane's
+// accumulators of fragments (2t, 2t + 1) are 8 consecutive channels of its pixel and leave as
+// one 16-byte store (16 pixels x 64 bytes per wave instruction instead of x 32: the ResNet-50
+// stem writes 2 GB at B = 1280)
+MA_DEV int st_perm(int r) {
+  const int r5 = r & 31;
+  return (r & ~31) | (((r5 >> 2) & 3) << 3) | ((r5 >> 4) << 2) | (r5 & 3);
+}
+
 // R x R taps, stride S, K = 16 * KT output channels
 template <int R, int S, int KT>
 __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
+  static_assert(KT % 2 == 0, "fragment pairs (st_perm)");
   constexpr int RR = R * R;
   constexpr int KS = (RR * 4 + 31) / 32;           // 32-deep k-steps
   constexpr int K = 16 * KT;
@@ -55,7 +66,7 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
   for (int i = tid; i < K * KS * 8; i += ST_NT) {
     const int k = i / (KS * 8), t = i - k * (KS * 8);
     st_u32x2 v = {0u, 0u};
-    if (t < RR) v = *(const st_u32x2*)(a.w + ((size_t)k * RR + t) * 8);
+    if (t < RR) v = *(const st_u32x2*)(a.w + ((size_t)st_perm(k) * RR + t) * 8);
     const int ks = t >> 3, ch = (t & 7) >> 1;
     *(st_u32x2*)(sw + (ks * K + k) * 64 + ((ch ^ ((k >> 1) & 3)) * 16) + (t & 1) * 8) = v;
   }
@@ -81,7 +92,8 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bias[kt][j] = a.bias ? a.bias[16 * kt + 4 * (lane >> 4) + j] : 0.f;
+    for (int j = 0; j < 4; ++j)
+      bias[kt][j] = a.bias ? a.bias[st_perm(16 * kt + 4 * (lane >> 4) + j)] : 0.f;
 
   const st_u32x2* xin = (const st_u32x2*)a.x + (size_t)n * a.H * a.W * 2;   // 16-byte pixels
   // the next tile's input window is loaded into registers while this tile computes
@@ -130,24 +142,30 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
           acc[g][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[kt], fx, acc[g][kt], 0, 0, 0);
       }
     }
-    // epilogue: (+ bias) -> bf16 NHWC, BN sums of the rounded values
+    // epilogue: (+ bias) -> bf16 NHWC (one 16-byte store per fragment pair, st_perm), BN sums
+    // of the rounded values
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int p = p0 + 4 * w + g, q = q0 + (lane & 15);
       const bool ok = p < a.P && q < a.Q;
-      bf16* yp = a.y + (((size_t)n * a.P + p) * a.Q + q) * K + 4 * (lane >> 4);
+      bf16* yp = a.y + (((size_t)n * a.P + p) * a.Q + q) * K + 8 * (lane >> 4);
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        bf16x4 o;
+      for (int tp = 0; tp < KT / 2; ++tp) {
+        bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[g][kt][j] + bias[kt][j]);
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(acc[g][2 * tp][j] + bias[2 * tp][j]);
+          o[4 + j] = f2bf(acc[g][2 * tp + 1][j] + bias[2 * tp + 1][j]);
+        }
         if (ok) {
-          *(bf16x4*)(yp + 16 * kt) = o;
+          *(bf16x8*)(yp + 32 * tp) = o;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float f = bf2f(o[j]);
-            s[kt][j] += f;
-            ss[kt][j] += f * f;
+            const float f = bf2f(o[j]), f2 = bf2f(o[4 + j]);
+            s[2 * tp][j] += f;
+            ss[2 * tp][j] += f * f;
+            s[2 * tp + 1][j] += f2;
+            ss[2 * tp + 1][j] += f2 * f2;
           }
         }
       }
@@ -160,8 +178,8 @@ __global__ __launch_bounds__(ST_NT) void stem_kernel(StemArgs a) {
     for (int j = 0; j < 4; ++j) {
       const float v1 = st_row16_sum(s[kt][j]), v2 = st_row16_sum(ss[kt][j]);
       if ((lane & 15) == 0) {
-        red[w][0][16 * kt + 4 * (lane >> 4) + j] = v1;
-        red[w][1][16 * kt + 4 * (lane >> 4) + j] = v2;
+        red[w][0][st_perm(16 * kt + 4 * (lane >> 4) + j)] = v1;
+        red[w][1][st_perm(16 * kt + 4 * (lane >> 4) + j)] = v2;
       }
     }
   __syncthreads();
