@@ -60,11 +60,15 @@ constexpr int ST_LD = 17;   // floats per thread row of the forward's BN partial
 // LOOP: one statistics group (the train batch) on a capped grid that walks the strips (the
 // stride a multiple of C8, so a thread keeps its channels): fewer blocks add the BN sums, which
 // contend at the memory side (profiles/r5/stats_cost/: B = 32 dw 96 ch 16.8 us with, 8.4 without)
-template <int S, bool PRO, bool LOOP>
+// DH: output rows per thread.  Each loaded input row (and, with PRO, its BN transform -- most of
+// the kernel's VALU) serves DH output rows: DH = 2 loads / transforms 4 rows per 2 output rows
+// at stride 1 instead of 6
+template <int S, bool PRO, bool LOOP, int DH>
 __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
   extern __shared__ float part[];  // [DT][ST_LD] per-thread BN partial sums (sum, sumsq)
   const int C8 = a.C >> 3, QS = (a.Q + DWL - 1) / DWL;
-  const int per_img = a.P * QS * C8;
+  const int PR = (a.P + DH - 1) / DH;             // row groups per image
+  const int per_img = PR * QS * C8;
   const int total = a.N * per_img;
   const int g0 = blockIdx.x * DT, gt = g0 + threadIdx.x;
   const int imgs_per_group = a.group_rows / (a.P * a.Q);
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
     int r = gi / C8;
     const int qs = r % QS;
     r /= QS;
-    const int p = r % a.P, n = r / a.P;
+    const int p = (r % PR) * DH, n = r / PR;      // first output row of this thread
     float wr[9][8];
     load_w72(a.w, c8, wr);
     constexpr int NCOL = (DWL - 1) * S + 3;
@@ -108,13 +112,15 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
       plo = a.pro_act == 0 ? __builtin_nanf("") : 0.f;
       phi = a.pro_act == 2 ? 6.f : (a.pro_act == 0 ? __builtin_nanf("") : __builtin_huge_valf());
     }
-    float acc[DWL][8];
+    float acc[DH][DWL][8];
 #pragma unroll
-    for (int o = 0; o < DWL; ++o)
+    for (int d = 0; d < DH; ++d)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+      for (int o = 0; o < DWL; ++o)
 #pragma unroll
-    for (int rr = 0; rr < 3; ++rr) {
+        for (int k = 0; k < 8; ++k) acc[d][o][k] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < (DH - 1) * S + 3; ++rr) {
       const int h = p * S - a.pad + rr;
       if (h >= 0 && h < a.H) {
         const bf16* row = a.x + (size_t)(n * a.H + h) * a.W * a.C + c8 * 8;
@@ -129,34 +135,44 @@ __global__ __launch_bounds__(DT) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
               for (int k = 0; k < 8; ++k)
                 col[j][k] = f2bf(fminf(fmaxf(bf2f(col[j][k]) * psc[k] + psh[k], plo), phi));
-              // the strip owning input (h, ww) writes the activation once: rows p*S .. p*S+S-1
-              // (rr >= pad), columns of its own output strip
-              if (a.keep && rr >= a.pad && rr < a.pad + S && j >= a.pad && j < a.pad + DWL * S)
+              // the strip owning input (h, ww) writes the activation once: rows p*S ..
+              // p*S+DH*S-1 (rr >= pad), columns of its own output strip
+              if (a.keep && rr >= a.pad && rr < a.pad + DH * S && j >= a.pad && j < a.pad + DWL * S)
                 *(bf16x8*)(a.keep + (size_t)(n * a.H + h) * a.W * a.C + (size_t)ww * a.C + c8 * 8) = col[j];
             }
           }
         }
 #pragma unroll
-        for (int o = 0; o < DWL; ++o)
+        for (int d = 0; d < DH; ++d) {
+          const int kr = rr - d * S;                   // this input row's kernel row for output row d
+          if (kr < 0 || kr > 2) continue;              // (compile-time after unrolling)
 #pragma unroll
-          for (int t = 0; t < 3; ++t)
+          for (int o = 0; o < DWL; ++o)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) acc[o][k] += bf2f(col[o * S + t][k]) * wr[rr * 3 + t][k];
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+              for (int k = 0; k < 8; ++k)
+                acc[d][o][k] += bf2f(col[o * S + t][k]) * wr[kr * 3 + t][k];
+        }
       }
     }
-    bf16* yrow = a.y + (size_t)(n * a.P + p) * a.Q * a.C + c8 * 8;
 #pragma unroll
-    for (int o = 0; o < DWL; ++o) {
-      if (q0 + o < a.Q) {
-        bf16x8 v;
+    for (int d = 0; d < DH; ++d) {
+      if (p + d >= a.P) break;
+      bf16* yrow = a.y + (size_t)(n * a.P + p + d) * a.Q * a.C + c8 * 8;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          v[k] = f2bf(acc[o][k]);
-          const float f = bf2f(v[k]);
-          s[k] += f;
-          ss[k] += f * f;
+      for (int o = 0; o < DWL; ++o) {
+        if (q0 + o < a.Q) {
+          bf16x8 v;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            v[k] = f2bf(acc[d][o][k]);
+            const float f = bf2f(v[k]);
+            s[k] += f;
+            ss[k] += f * f;
+          }
+          *(bf16x8*)(yrow + (size_t)(q0 + o) * a.C) = v;
         }
-        *(bf16x8*)(yrow + (size_t)(q0 + o) * a.C) = v;
       }
     }
     if (a.stats && !lds_stats) {  // block straddles two BN groups (tiny images): global atomics
@@ -531,9 +547,24 @@ int dw_stat_blocks() {
   return v;
 }
 
+// output rows per thread of the forward: 2 for the stride-1 convs of a large batch (the scoring
+// pass, B = 320: 96 @32 96 -> 82 us, 144 @32 146 -> 119, 384 @8 31 -> 23), 1 elsewhere (at the
+// B = 32 train batch the halved thread count cost 47 us over the chain, and the stride-2 convs
+// at 16 / 8 wide lost 6 us each; bench/dw_stats_bench.py, profiles/r6/dw_dh/).  MERCURY_DW_DH=1/2
+// forces one (A/B runs)
+static int dw_dh(const DwArgs& a) {
+  static const int force = [] {
+    const char* e = getenv("MERCURY_DW_DH");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 1 || force == 2) return force;
+  return a.stride == 1 && a.N >= 128 ? 2 : 1;
+}
+
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const int QS = (a.Q + DWL - 1) / DWL;
-  const long long total = (long long)a.N * a.P * QS * (a.C / 8);
+  const int DHr = dw_dh(a);
+  const long long total = (long long)a.N * ((a.P + DHr - 1) / DHr) * QS * (a.C / 8);
   long long blocks = (total + DT - 1) / DT;
   // one statistics group: at most ~one block per CU adds the BN sums (grid-stride kernel)
   const int cap = dw_stat_blocks();
@@ -542,7 +573,11 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const dim3 grid((unsigned)blocks);
   const size_t shm = a.stats ? (size_t)DT * ST_LD * sizeof(float) : 0;
   const bool pro = a.pro_gamma != nullptr;
-#define DW_FWD(S_, P_, L_) hipLaunchKernelGGL((dw_fwd_kernel<S_, P_, L_>), grid, dim3(DT), shm, st, a)
+#define DW_FWD(S_, P_, L_)                                                                       \
+  do {                                                                                           \
+    if (DHr == 2) hipLaunchKernelGGL((dw_fwd_kernel<S_, P_, L_, 2>), grid, dim3(DT), shm, st, a); \
+    else hipLaunchKernelGGL((dw_fwd_kernel<S_, P_, L_, 1>), grid, dim3(DT), shm, st, a);          \
+  } while (0)
 #define DW_FWD_L(S_, P_) \
   if (loop) DW_FWD(S_, P_, true); \
   else DW_FWD(S_, P_, false)
