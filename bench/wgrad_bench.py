@@ -1,10 +1,12 @@
-"""Standalone weight-gradient kernel (csrc/wgrad.hip) on engine shapes, graph-timed, with and
-without the XCD-aware block renumbering (``wgrad_configure``).
+"""Standalone weight-gradient kernel (csrc/wgrad.hip) on engine shapes, graph-timed: the
+engine's plan and 2x / 4x its pixel splits (atomic splits add into a zeroed gradient, which
+the engine zeroes once per step; here the zeroing runs outside the timed graph).
 
     python bench/wgrad_bench.py
 
-One JSON line per (shape, xcd): the plan, microseconds, TF/s over the padded columns, and
-whether the result equals the other setting's (fp32 split sums: within 1e-3 relative).
+One JSON line per (shape, plan): microseconds, TF/s over the padded columns, and whether the
+result matches the engine plan's (fp32 split sums: within 1e-3 relative).  (An XCD-grouped
+block order measured equal, profiles/r6/wgrad_xcd_rejected.jsonl.)
 """
 import argparse
 import json
@@ -31,8 +33,8 @@ def main():
     args = ap.parse_args()
     import torch
     from mercury_amd import ops
-    from mercury_amd.ops.conv import ConvSpec, wgrad_plan, wgrad_slab_bytes
-    lib = ops.lib()
+    from mercury_amd.ops.conv import ConvSpec, wgrad_plan
+    ops.lib()
     dev = 'cuda'
     for name, N, H, C, K, R, st, pd in SHAPES:
         sp = ConvSpec(N, H, H, C, K, R, R, st, pd)
@@ -40,30 +42,26 @@ def main():
         x = ops.to_nhwc(torch.randn(N, C, H, H, device=dev).to(torch.bfloat16).float())
         dy = (torch.randn(sp.M * K, device=dev) * 0.1).to(torch.bfloat16)
         dw = torch.zeros(K * R * R * C, device=dev)
-        plan = wgrad_plan(sp)
-        nsl = wgrad_slab_bytes(sp, plan)
-        slab = torch.zeros(max(1, (nsl + 3) // 4), device=dev) if nsl else None
+        base = wgrad_plan(sp)
         flop = 2.0 * sp.M * K * R * R * sp.Cp
         ref = None
-        for xcd in (0, 1):
-            lib.wgrad_configure(xcd)
+        for mult in (1, 2, 4):
+            plan = (base[0], base[1], base[2] * mult)
 
-            def fn():
-                if slab is None:
-                    dw.zero_()
-                ops.conv_wgrad(dy, x, dw, sp, plan=plan, slab=slab)
-            us = gtime(fn, reps=args.reps)
+            def fn():      # atomic splits into the zeroed gradient, as the engine's stem runs it
+                ops.conv_wgrad(dy, x, dw, sp, plan=plan)
+            dw.zero_()
             fn()
             torch.cuda.synchronize()
+            got = dw.clone()
+            us = gtime(fn, reps=args.reps)
             ok = None
             if ref is None:
-                ref = dw.clone()
+                ref = got
             else:
-                ok = bool(((dw - ref).abs().max() <= 1e-3 * ref.abs().max()).item())
-            print(json.dumps({'shape': name, 'plan': list(plan[:3]), 'xcd': xcd,
-                              'us': round(us, 2), 'tflops': round(flop / us / 1e6, 1),
-                              'equal': ok}), flush=True)
-        lib.wgrad_configure(0)
+                ok = bool(((got - ref).abs().max() <= 1e-3 * ref.abs().max()).item())
+            print(json.dumps({'shape': name, 'plan': list(plan), 'us': round(us, 2),
+                              'tflops': round(flop / us / 1e6, 1), 'equal': ok}), flush=True)
 
 
 if __name__ == '__main__':
